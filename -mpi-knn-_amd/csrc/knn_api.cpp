@@ -1,0 +1,446 @@
+// knn_api.cpp -- C ABI (include/knn_amd.h) over the gfx950 kernels.
+//
+// One knn_ctx per GPU (≙ one MPI rank of the reference, cpp:121-125).  The
+// train set lives in HBM in two forms: the caller's fp64 rows (exact
+// re-rank, ≙ Data_train cpp:140) and a padded fp32 copy + per-row seeds for
+// the MFMA candidate pass.  Queries are classified by the pipeline in
+// knn_kernels.hip; there is no host compute path.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/knn_amd.h"
+#include "knn_api_internal.h"
+#include "knn_kernels.h"
+
+using namespace knnk;
+
+namespace {
+thread_local std::string g_err;
+}
+
+void knn_set_error(const char* fmt, const char* a, long long b) {
+  char buf[512];
+  snprintf(buf, sizeof buf, fmt, a, b);
+  g_err = buf;
+}
+
+int knn_fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return knn_fail(KNN_ERR_DEVICE, std::string(#expr " failed: ") + hipGetErrorString(e_)); \
+  } while (0)
+
+int DevBuf::ensure(size_t bytes) {
+  if (cap >= bytes && p) return KNN_OK;
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  cap = 0;
+  if (bytes == 0) bytes = 16;
+  if (hipMalloc(&p, bytes) != hipSuccess) {
+    p = nullptr;
+    return knn_fail(KNN_ERR_NOMEM, "hipMalloc of " + std::to_string(bytes) + " bytes failed");
+  }
+  cap = bytes;
+  return KNN_OK;
+}
+void DevBuf::release() {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  cap = 0;
+}
+
+static int device_guard(knn_ctx* ctx) {
+  if (!ctx) return knn_fail(KNN_ERR_ARG, "null context");
+  HIP_TRY(hipSetDevice(ctx->device));
+  return KNN_OK;
+}
+
+extern "C" {
+
+const char* knn_version(void) { return "mpi-knn-amd 0.1 (gfx950)"; }
+const char* knn_last_error(void) { return g_err.c_str(); }
+
+int knn_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int knn_create(knn_ctx** out, int device) {
+  if (!out) return knn_fail(KNN_ERR_ARG, "null out pointer");
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+    return knn_fail(KNN_ERR_DEVICE, "no HIP device available (the KNN path has no CPU fallback)");
+  if (device < 0 || device >= n) return knn_fail(KNN_ERR_ARG, "device index out of range");
+  HIP_TRY(hipSetDevice(device));
+  knn_ctx* c = new knn_ctx();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return knn_fail(KNN_ERR_DEVICE, "hipStreamCreate failed");
+  }
+  if (hipHostMalloc((void**)&c->h_count, sizeof(int) * 4, hipHostMallocDefault) != hipSuccess) {
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return knn_fail(KNN_ERR_DEVICE, "hipHostMalloc failed");
+  }
+  *out = c;
+  return KNN_OK;
+}
+
+int knn_destroy(knn_ctx* ctx) {
+  if (!ctx) return KNN_OK;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  for (DevBuf* b : ctx->all_bufs()) b->release();
+  for (auto& e : ctx->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (ctx->h_count) (void)hipHostFree(ctx->h_count);
+  (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return KNN_OK;
+}
+
+}  // extern "C"
+
+// Builds the fp32 candidate copy + seeds + norm stats from fp64 rows that
+// already sit on the device.
+static int build_train(knn_ctx* ctx, const double* dX, const int32_t* dlab, int64_t n, int d,
+                       int class_cnt, int64_t idx_off) {
+  const int DP = pad_dim(d);
+  if (!cand_supported(DP))
+    return knn_fail(KNN_ERR_ARG, "dimension " + std::to_string(d) + " not supported by this build");
+  const int64_t n_pad = (n + kTR - 1) / kTR * kTR;
+  int rc;
+  if ((rc = ctx->X32.ensure((size_t)n_pad * DP * sizeof(float)))) return rc;
+  if ((rc = ctx->xl2.ensure((size_t)n_pad * sizeof(float)))) return rc;
+  if ((rc = ctx->xl1.ensure((size_t)n_pad * sizeof(float)))) return rc;
+  if ((rc = ctx->stats.ensure(2 * sizeof(unsigned long long)))) return rc;
+  HIP_TRY(hipMemsetAsync(ctx->stats.p, 0, 2 * sizeof(unsigned long long), ctx->stream));
+  launch_prep_train(dX, n, d, DP, n_pad, (float*)ctx->X32.p, (float*)ctx->xl2.p,
+                    (float*)ctx->xl1.p, (unsigned long long*)ctx->stats.p, ctx->stream);
+  HIP_TRY(hipGetLastError());
+  unsigned long long st[2];
+  HIP_TRY(hipMemcpyAsync(st, ctx->stats.p, sizeof st, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  double x2, x1;
+  memcpy(&x2, &st[0], 8);
+  memcpy(&x1, &st[1], 8);
+  TrainDev& t = ctx->train;
+  t.X64 = dX;
+  t.lab = dlab;
+  t.X32 = (const float*)ctx->X32.p;
+  t.xinit_l2 = (const float*)ctx->xl2.p;
+  t.xinit_l1 = (const float*)ctx->xl1.p;
+  t.n = n;
+  t.n_pad = n_pad;
+  t.d = d;
+  t.DP = DP;
+  t.x2max = x2;
+  t.x1max = x1;
+  ctx->class_cnt = class_cnt;
+  ctx->idx_off = idx_off;
+  ctx->trained = true;
+  return KNN_OK;
+}
+
+static int check_train_args(int64_t n, int d, int class_cnt) {
+  if (n <= 0) return knn_fail(KNN_ERR_ARG, "n_train must be > 0");
+  if (n >= (int64_t)INT32_MAX - 4096)
+    return knn_fail(KNN_ERR_ARG, "n_train per context must be < 2^31 (shard the train set)");
+  if (d <= 0) return knn_fail(KNN_ERR_ARG, "dim must be > 0");
+  if (class_cnt <= 0) return knn_fail(KNN_ERR_ARG, "class_cnt must be > 0");
+  return KNN_OK;
+}
+
+extern "C" {
+
+int knn_set_train(knn_ctx* ctx, const double* X, const int32_t* labels, int64_t n, int32_t d,
+                  int32_t class_cnt) {
+  int rc;
+  if ((rc = device_guard(ctx))) return rc;
+  if ((rc = check_train_args(n, d, class_cnt))) return rc;
+  if (!X || !labels) return knn_fail(KNN_ERR_ARG, "null train pointer");
+  // label range check (the reference indexes label_cnt[label] unchecked, cpp:330)
+  for (int64_t i = 0; i < n; i++)
+    if (labels[i] < 0 || labels[i] >= class_cnt)
+      return knn_fail(KNN_ERR_ARG, "train label out of [0, class_cnt) at row " + std::to_string(i));
+  if ((rc = ctx->X64_own.ensure((size_t)n * d * sizeof(double)))) return rc;
+  if ((rc = ctx->lab_own.ensure((size_t)n * sizeof(int32_t)))) return rc;
+  HIP_TRY(hipMemcpyAsync(ctx->X64_own.p, X, (size_t)n * d * sizeof(double),
+                         hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(hipMemcpyAsync(ctx->lab_own.p, labels, (size_t)n * sizeof(int32_t),
+                         hipMemcpyHostToDevice, ctx->stream));
+  return build_train(ctx, (const double*)ctx->X64_own.p, (const int32_t*)ctx->lab_own.p, n, d,
+                     class_cnt, 0);
+}
+
+int knn_set_train_device(knn_ctx* ctx, const double* dX, const int32_t* dlabels, int64_t n,
+                         int32_t d, int32_t class_cnt, int64_t idx_offset) {
+  int rc;
+  if ((rc = device_guard(ctx))) return rc;
+  if ((rc = check_train_args(n, d, class_cnt))) return rc;
+  if (!dX || !dlabels) return knn_fail(KNN_ERR_ARG, "null train pointer");
+  return build_train(ctx, dX, dlabels, n, d, class_cnt, idx_offset);
+}
+
+}  // extern "C"
+
+// Splits per query tile: enough workgroups to fill 256 CUs a few times over,
+// enough lists to hold C candidates, at least 2 tiles per split.
+static int choose_splits(int n_qt, int64_t n_tiles, int C, int R) {
+  int S = (2048 + n_qt - 1) / n_qt;
+  S = std::max(S, (C + 2 * R - 1) / (2 * R));
+  S = std::min(S, 32);
+  S = (int)std::min<int64_t>(S, std::max<int64_t>(1, n_tiles / 2));
+  return std::max(S, 1);
+}
+
+static double err_factor(int metric, int DP) {
+  const double u = std::ldexp(1.0, -24);
+  const int n = metric == 0 ? DP + 1 : DP;
+  const double gam = n * u / (1.0 - n * u);
+  return (gam + (metric == 0 ? 5.0 : 3.0) * u) * 1.01;
+}
+
+// Core search: candidate pass + merge/re-rank/certify + rescan.
+int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric, const Sink& sink,
+                   hipStream_t s) {
+  const TrainDev& t = ctx->train;
+  const int DP = t.DP;
+  const int R = 16;
+  const int n_qt = (int)((m + kQPB - 1) / kQPB);
+  const int64_t m_pad = (int64_t)n_qt * kQPB;
+  const int64_t n_tiles = t.n_pad / kTR;
+  int C = (int)std::min<int64_t>(t.n, std::max(2 * W, W + 16));
+  C = std::min(C, kMaxUnion);
+  const int S = choose_splits(n_qt, n_tiles, C, R);
+  const int NL = 2 * S;
+  C = std::min(C, NL * R);
+  int rc;
+  if ((rc = ctx->Q32.ensure((size_t)m_pad * DP * sizeof(float)))) return rc;
+  if ((rc = ctx->cand_v.ensure((size_t)m_pad * NL * R * sizeof(float)))) return rc;
+  if ((rc = ctx->cand_i.ensure((size_t)m_pad * NL * R * sizeof(int)))) return rc;
+  if ((rc = ctx->rescan_q.ensure((size_t)m * sizeof(int) + 16))) return rc;
+  if ((rc = ctx->rescan_cnt.ensure(16))) return rc;
+
+  ctx->geom[0] = (int64_t)n_qt * S;
+  ctx->geom[1] = S;
+  ctx->geom[2] = NL;
+  ctx->geom[3] = C;
+  const bool tm = ctx->timing;
+  if (tm) HIP_TRY(hipEventRecord(ctx->ev[0], s));
+  launch_prep_queries(dQ, m, t.d, DP, m_pad, metric == 0 ? -2.0f : 1.0f, (float*)ctx->Q32.p, s);
+  if (tm) HIP_TRY(hipEventRecord(ctx->ev[1], s));
+  launch_cand(metric, DP, t.X32, metric == 0 ? t.xinit_l2 : t.xinit_l1, (const float*)ctx->Q32.p,
+              (int)n_tiles, S, n_qt, (float*)ctx->cand_v.p, (int*)ctx->cand_i.p, s);
+  HIP_TRY(hipGetLastError());
+  if (tm) HIP_TRY(hipEventRecord(ctx->ev[2], s));
+  HIP_TRY(hipMemsetAsync(ctx->rescan_cnt.p, 0, sizeof(int), s));
+  launch_merge_rerank(metric, (const float*)ctx->cand_v.p, (const int*)ctx->cand_i.p, NL, t, dQ, m,
+                      W, C, err_factor(metric, DP), sink, (int*)ctx->rescan_q.p,
+                      (int*)ctx->rescan_cnt.p, s);
+  HIP_TRY(hipGetLastError());
+  if (tm) HIP_TRY(hipEventRecord(ctx->ev[3], s));
+  HIP_TRY(hipMemcpyAsync(ctx->h_count, ctx->rescan_cnt.p, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  const int nflag = ctx->h_count[0];
+  ctx->last_rescan = nflag;
+  if (tm) {
+    float ms;
+    for (int p = 0; p < 3; p++) {
+      HIP_TRY(hipEventElapsedTime(&ms, ctx->ev[p], ctx->ev[p + 1]));
+      ctx->phase_ms[p] = ms;
+    }
+    ctx->phase_ms[3] = 0.0;
+  }
+  if (nflag > 0) {
+    const size_t per = rescan_scratch_entries(t.n, W);
+    int64_t batch = (int64_t)((256ull << 20) / (per * 12 + 1));
+    batch = std::max<int64_t>(1, std::min<int64_t>(batch, 4096));
+    batch = std::min<int64_t>(batch, nflag);
+    if ((rc = ctx->ra_k.ensure(per * batch * sizeof(double)))) return rc;
+    if ((rc = ctx->ra_i.ensure(per * batch * sizeof(int)))) return rc;
+    if ((rc = ctx->rb_k.ensure(per * batch * sizeof(double)))) return rc;
+    if ((rc = ctx->rb_i.ensure(per * batch * sizeof(int)))) return rc;
+    for (int f0 = 0; f0 < nflag; f0 += (int)batch) {
+      const int nf = (int)std::min<int64_t>(batch, nflag - f0);
+      launch_rescan(metric, t, dQ, (const int*)ctx->rescan_q.p, f0, nf, W, (double*)ctx->ra_k.p,
+                    (int*)ctx->ra_i.p, (double*)ctx->rb_k.p, (int*)ctx->rb_i.p, sink, s);
+      HIP_TRY(hipGetLastError());
+    }
+    if (tm) {
+      HIP_TRY(hipEventRecord(ctx->ev[4], s));
+      HIP_TRY(hipEventSynchronize(ctx->ev[4]));
+      float ms;
+      HIP_TRY(hipEventElapsedTime(&ms, ctx->ev[3], ctx->ev[4]));
+      ctx->phase_ms[3] = ms;
+    }
+  }
+  return KNN_OK;
+}
+
+static int check_query_args(knn_ctx* ctx, int64_t m, int32_t k, int32_t metric) {
+  if (!ctx->trained) return knn_fail(KNN_ERR_STATE, "classify before set_train");
+  if (m < 0) return knn_fail(KNN_ERR_ARG, "m must be >= 0");
+  if (m >= (int64_t)INT32_MAX) return knn_fail(KNN_ERR_ARG, "m must be < 2^31 per call");
+  if (k < 0) return knn_fail(KNN_ERR_ARG, "k must be >= 0");
+  if (k > ctx->train.n)
+    return knn_fail(KNN_ERR_ARG, "k exceeds n_train (the reference reads past its array, cpp:328)");
+  if (k > kMaxK) return knn_fail(KNN_ERR_ARG, "k above the supported maximum (1000)");
+  if (metric != KNN_METRIC_L2 && metric != KNN_METRIC_L1)
+    return knn_fail(KNN_ERR_ARG, "metric must be 0 (L2) or 1 (L1)");
+  return KNN_OK;
+}
+
+extern "C" {
+
+int knn_classify_device(knn_ctx* ctx, const double* dQ, int64_t m, int32_t k, int32_t metric,
+                        int32_t* d_labels, int64_t* d_idx, double* d_dist, int32_t* d_flags,
+                        void* stream) {
+  int rc;
+  if ((rc = device_guard(ctx))) return rc;
+  if ((rc = check_query_args(ctx, m, k, metric))) return rc;
+  if (!d_labels) return knn_fail(KNN_ERR_ARG, "null labels output");
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  ctx->last_rescan = 0;
+  if (m == 0) return KNN_OK;
+  if (!dQ) return knn_fail(KNN_ERR_ARG, "null query pointer");
+  if (k == 0) {  // cpp:324: max_label stays -1
+    launch_fill_i32(d_labels, m, -1, s);
+    if (d_flags) launch_fill_i32(d_flags, m, 0, s);
+    HIP_TRY(hipGetLastError());
+    return KNN_OK;
+  }
+  Sink sink{};
+  sink.mode = MODE_SINGLE;
+  sink.k = k;
+  sink.idx_off = ctx->idx_off;
+  sink.labels = d_labels;
+  sink.idx = d_idx;
+  sink.dist = d_dist;
+  sink.flags = d_flags;
+  const int W = (int)std::min<int64_t>((int64_t)k + 1, ctx->train.n);
+  return knn_run_search(ctx, dQ, m, W, metric, sink, s);
+}
+
+int knn_classify(knn_ctx* ctx, const double* Q, int64_t m, int32_t k, int32_t metric,
+                 int32_t* out_labels, int64_t* out_idx, double* out_dist, int32_t* out_flags) {
+  int rc;
+  if ((rc = device_guard(ctx))) return rc;
+  if ((rc = check_query_args(ctx, m, k, metric))) return rc;
+  if (!out_labels) return knn_fail(KNN_ERR_ARG, "null labels output");
+  if (m == 0) return KNN_OK;
+  if (!Q) return knn_fail(KNN_ERR_ARG, "null query pointer");
+  const int d = ctx->train.d;
+  if ((rc = ctx->Q64.ensure((size_t)m * d * sizeof(double)))) return rc;
+  if ((rc = ctx->o_lab.ensure((size_t)m * sizeof(int32_t)))) return rc;
+  if ((rc = ctx->o_flags.ensure((size_t)m * sizeof(int32_t)))) return rc;
+  if (out_idx && (rc = ctx->o_idx.ensure((size_t)m * std::max(k, 1) * sizeof(int64_t)))) return rc;
+  if (out_dist && (rc = ctx->o_dist.ensure((size_t)m * std::max(k, 1) * sizeof(double)))) return rc;
+  hipStream_t s = ctx->stream;
+  HIP_TRY(hipMemcpyAsync(ctx->Q64.p, Q, (size_t)m * d * sizeof(double), hipMemcpyHostToDevice, s));
+  rc = knn_classify_device(ctx, (const double*)ctx->Q64.p, m, k, metric, (int32_t*)ctx->o_lab.p,
+                           out_idx ? (int64_t*)ctx->o_idx.p : nullptr,
+                           out_dist ? (double*)ctx->o_dist.p : nullptr,
+                           (int32_t*)ctx->o_flags.p, s);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(out_labels, ctx->o_lab.p, (size_t)m * sizeof(int32_t),
+                         hipMemcpyDeviceToHost, s));
+  if (out_flags)
+    HIP_TRY(hipMemcpyAsync(out_flags, ctx->o_flags.p, (size_t)m * sizeof(int32_t),
+                           hipMemcpyDeviceToHost, s));
+  if (out_idx && k > 0)
+    HIP_TRY(hipMemcpyAsync(out_idx, ctx->o_idx.p, (size_t)m * k * sizeof(int64_t),
+                           hipMemcpyDeviceToHost, s));
+  if (out_dist && k > 0)
+    HIP_TRY(hipMemcpyAsync(out_dist, ctx->o_dist.p, (size_t)m * k * sizeof(double),
+                           hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return KNN_OK;
+}
+
+int knn_search_partial_device(knn_ctx* ctx, const double* dQ, int64_t m, int32_t w,
+                              int32_t metric, double* d_dist, int64_t* d_idx, int32_t* d_lab,
+                              void* stream) {
+  int rc;
+  if ((rc = device_guard(ctx))) return rc;
+  if (!ctx->trained) return knn_fail(KNN_ERR_STATE, "search before set_train");
+  if (w <= 0 || w > kMaxK + 1) return knn_fail(KNN_ERR_ARG, "w must be in [1, 1001]");
+  if (metric != KNN_METRIC_L2 && metric != KNN_METRIC_L1)
+    return knn_fail(KNN_ERR_ARG, "metric must be 0 (L2) or 1 (L1)");
+  if (m < 0 || m >= (int64_t)INT32_MAX) return knn_fail(KNN_ERR_ARG, "bad m");
+  if (!d_dist || !d_idx || !d_lab) return knn_fail(KNN_ERR_ARG, "null output");
+  if (m == 0) return KNN_OK;
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  Sink sink{};
+  sink.mode = MODE_PARTIAL;
+  sink.w = w;
+  sink.idx_off = ctx->idx_off;
+  sink.idx = d_idx;
+  sink.dist = d_dist;
+  sink.plab = d_lab;
+  // a shard smaller than w yields min(w, n) entries; the tail is padded
+  const int W = (int)std::min<int64_t>(w, ctx->train.n);
+  return knn_run_search(ctx, dQ, m, W, metric, sink, s);
+}
+
+int knn_merge_vote_device(knn_ctx* ctx, const double* d_dist, const int64_t* d_idx,
+                          const int32_t* d_lab, int32_t parts, int64_t m, int32_t w, int32_t k,
+                          int32_t* d_labels, int64_t* d_out_idx, double* d_out_dist,
+                          int32_t* d_flags, void* stream) {
+  int rc;
+  if ((rc = device_guard(ctx))) return rc;
+  if (parts <= 0 || w <= 0 || k < 0 || k > w || (int64_t)parts * w > 4096)
+    return knn_fail(KNN_ERR_ARG, "bad merge geometry (need 0 <= k <= w, parts*w <= 4096)");
+  if (!d_labels) return knn_fail(KNN_ERR_ARG, "null labels output");
+  if (m == 0) return KNN_OK;
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  launch_merge_vote_partials(d_dist, d_idx, d_lab, parts, m, w, k, d_labels, d_out_idx,
+                             d_out_dist, d_flags, s);
+  HIP_TRY(hipGetLastError());
+  return KNN_OK;
+}
+
+int knn_sync(knn_ctx* ctx) {
+  int rc;
+  if ((rc = device_guard(ctx))) return rc;
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return KNN_OK;
+}
+
+int64_t knn_last_rescan_count(knn_ctx* ctx) { return ctx ? ctx->last_rescan : -1; }
+
+int knn_set_timing(knn_ctx* ctx, int enable) {
+  int rc;
+  if ((rc = device_guard(ctx))) return rc;
+  if (enable && !ctx->ev[0])
+    for (auto& e : ctx->ev) HIP_TRY(hipEventCreate(&e));
+  ctx->timing = enable != 0;
+  return KNN_OK;
+}
+
+double knn_last_phase_ms(knn_ctx* ctx, int phase) {
+  if (!ctx || phase < 0 || phase > 3) return -1.0;
+  return ctx->phase_ms[phase];
+}
+
+int knn_last_geometry(knn_ctx* ctx, int64_t out[4]) {
+  if (!ctx || !out) return knn_fail(KNN_ERR_ARG, "null argument");
+  for (int i = 0; i < 4; i++) out[i] = ctx->geom[i];
+  return KNN_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,45 @@
+// knn_api_internal.h -- context state shared by knn_api.cpp and knn_group.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "knn_kernels.h"
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t bytes);  // grow-only; KNN_OK or KNN_ERR_NOMEM
+  void release();
+};
+
+struct knn_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int* h_count = nullptr;  // pinned
+  bool trained = false;
+  int class_cnt = 0;
+  int64_t idx_off = 0;
+  int64_t last_rescan = 0;
+  knnk::TrainDev train{};
+  bool timing = false;
+  hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  double phase_ms[4] = {0, 0, 0, 0};
+  int64_t geom[4] = {0, 0, 0, 0};
+  // train-side HBM
+  DevBuf X64_own, lab_own, X32, xl2, xl1, stats;
+  // per-classify workspace
+  DevBuf Q64, Q32, cand_v, cand_i, rescan_q, rescan_cnt, ra_k, ra_i, rb_k, rb_i;
+  // host-API outputs
+  DevBuf o_lab, o_idx, o_dist, o_flags;
+  std::vector<DevBuf*> all_bufs() {
+    return {&X64_own, &lab_own, &X32, &xl2, &xl1, &stats, &Q64, &Q32, &cand_v, &cand_i,
+            &rescan_q, &rescan_cnt, &ra_k, &ra_i, &rb_k, &rb_i, &o_lab, &o_idx, &o_dist,
+            &o_flags};
+  }
+};
+
+int knn_fail(int code, const std::string& msg);
+int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
+                   const knnk::Sink& sink, hipStream_t s);

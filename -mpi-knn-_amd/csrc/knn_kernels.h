@@ -1,0 +1,65 @@
+// knn_kernels.h -- internal launch interface of the HIP kernels (gfx950).
+// Not part of the public ABI (see include/knn_amd.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace knnk {
+
+constexpr int kQPB = 128;        // queries per candidate workgroup (4 waves x 32)
+constexpr int kTR = 32;          // train rows per LDS tile
+constexpr int kMaxUnion = 1024;  // max candidates kept per query across all lists
+constexpr int kSortN = 2048;     // rows per exact-rescan chunk / reduce block
+constexpr int kMaxK = 1000;      // largest k served (k+1 <= kMaxUnion)
+
+enum { MODE_SINGLE = 0, MODE_PARTIAL = 1 };
+
+// Output sinks of a search: MODE_SINGLE writes the vote, MODE_PARTIAL the
+// exact top-w list with labels (train-sharded building block).
+struct Sink {
+  int mode;
+  int k;                 // neighbours voted / reported (single)
+  int w;                 // list length (partial)
+  int64_t idx_off;       // added to reported indices
+  int32_t* labels;       // single: [m]
+  int64_t* idx;          // single: [m*k] (nullable); partial: [m*w]
+  double* dist;          // single: [m*k] (nullable); partial: [m*w]
+  int32_t* flags;        // single: [m] (nullable)
+  int32_t* plab;         // partial: [m*w]
+};
+
+// Train-set side state resident in HBM.
+struct TrainDev {
+  const double* X64;     // [n][d] fp64 (reference values)
+  const int32_t* lab;    // [n]
+  const float* X32;      // [n_pad][DP] fp32, zero padded
+  const float* xinit_l2; // [n_pad] fl32(||x32||^2); +inf on pad rows
+  const float* xinit_l1; // [n_pad] 0; +inf on pad rows
+  int64_t n, n_pad;
+  int d, DP;
+  double x2max, x1max;   // max ||x||_2^2, max ||x||_1 over the train rows
+};
+
+int pad_dim(int d);                 // DP for a given d (multiple of 8)
+bool cand_supported(int DP);
+
+void launch_prep_train(const double* X64, int64_t n, int d, int DP, int64_t n_pad, float* X32,
+                       float* xl2, float* xl1, unsigned long long* stats, hipStream_t s);
+void launch_prep_queries(const double* Q64, int64_t m, int d, int DP, int64_t m_pad,
+                         float scale, float* Q32, hipStream_t s);
+void launch_cand(int metric, int DP, const float* X32, const float* xinit, const float* Q32,
+                 int n_tiles, int S, int n_qt, float* out_v, int* out_i, hipStream_t s);
+void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, const TrainDev& t,
+                         const double* Q64, int64_t m, int W, int C, double f_err,
+                         const Sink& sink, int* rescan_q, int* rescan_cnt, hipStream_t s);
+void launch_rescan(int metric, const TrainDev& t, const double* Q64, const int* rescan_q,
+                   int f0, int nf, int W, double* pa_k, int* pa_i, double* pb_k, int* pb_i,
+                   const Sink& sink, hipStream_t s);
+size_t rescan_scratch_entries(int64_t n, int W);  // per flagged query, per buffer
+void launch_merge_vote_partials(const double* dist, const int64_t* idx, const int32_t* lab,
+                                int parts, int64_t m, int w, int k, int32_t* out_lab,
+                                int64_t* out_idx, double* out_dist, int32_t* out_flags,
+                                hipStream_t s, int64_t q0 = 0, int64_t mq = -1);
+void launch_fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t s);
+
+}  // namespace knnk

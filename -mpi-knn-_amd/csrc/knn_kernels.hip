@@ -1,0 +1,799 @@
+// knn_kernels.hip -- MI355X (gfx950, CDNA4) kernels of the KNN classify path.
+//
+// Pipeline per classify call (reference loop: cpp:308-381):
+//   1. prep_queries      fp64 queries -> fp32 (x -2 for L2) MFMA operands
+//   2. cand_kernel       fused distance + per-lane top-R selection.
+//        L2: -2 q.x^T on v_mfma_f32_32x32x2_f32 with the accumulator seeded by
+//            ||x||^2, so the chain ends at ||x||^2 - 2 q.x (the rank-equivalent
+//            of ||q - x||^2 for a fixed query; cpp:33-50).
+//        L1: sum |q - x| on the VALU (cpp:51-67; no GEMM identity exists).
+//        The distance matrix is never materialised: each lane keeps a sorted
+//        register list of its R best rows and a threshold filter.
+//   3. merge_rerank      per query: union of all lists -> best C by the fp32
+//        proxy -> exact fp64 reference distances for those C (sequential sum,
+//        no FMA, correctly rounded sqrt) -> sort by (dist, idx) -> certify
+//        that no excluded row can enter the top-w (rigorous fp32 error
+//        bound) -> first-to-max vote (cpp:324-337) or partial list output.
+//   4. rescan (rare)     queries that fail certification get an exact fp64
+//        scan over every row (chunked sort + tree reduce).
+// The result is the reference's fp64 top-k with ties ordered by train index.
+#include "knn_kernels.h"
+
+#include <float.h>
+#include <limits.h>
+
+#pragma clang fp contract(off)
+
+namespace knnk {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define KNN_INF_F __builtin_inff()
+#define KNN_INF_D __builtin_inf()
+
+int pad_dim(int d) { return (d + 7) & ~7; }
+
+// ---------------------------------------------------------------- helpers
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  // Blocks are dispatched round-robin over the 8 XCDs; give each XCD a
+  // contiguous range of logical ids so workgroups that stream the same train
+  // split share an L2 (bijective for any nwg).
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Reference distance, bit-exact with cpp:33-50 (L2: returns the squared sum
+// before sqrt) and cpp:51-67 (L1): fp64, dims in order, multiply then add.
+template <int METRIC>
+__device__ __forceinline__ double exact_dist_raw(const double* __restrict__ q,
+                                                 const double* __restrict__ x, int d) {
+  double r = 0.0;
+#pragma unroll 8
+  for (int i = 0; i < d; ++i) {
+    const double t = q[i] - x[i];
+    if (METRIC == 0) r = r + t * t;
+    else r = r + __builtin_fabs(t);
+  }
+  return r;
+}
+template <int METRIC>
+__device__ __forceinline__ double exact_dist(const double* __restrict__ q,
+                                             const double* __restrict__ x, int d) {
+  const double r = exact_dist_raw<METRIC>(q, x, d);
+  return METRIC == 0 ? __builtin_sqrt(r) : r;  // llvm.sqrt.f64: correctly rounded
+}
+
+template <typename K, typename I>
+__device__ __forceinline__ bool pair_less(K ka, I ia, K kb, I ib) {
+  return ka < kb || (ka == kb && ia < ib);
+}
+
+// Bitonic sort of n (power of two) (key, id) pairs in LDS, ascending by
+// (key, id).  All threads of the block participate.
+template <typename K, typename I>
+__device__ void bitonic_sort_lds(K* key, I* id, int n, int tid, int nthr) {
+  for (int size = 2; size <= n; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      __syncthreads();
+      for (int t = tid; t < (n >> 1); t += nthr) {
+        const int lo = 2 * t - (t & (stride - 1));
+        const int hi = lo + stride;
+        const bool up = (lo & size) == 0;
+        const K ka = key[lo], kb = key[hi];
+        const I ia = id[lo], ib = id[hi];
+        const bool sw = up ? pair_less(kb, ib, ka, ia) : pair_less(ka, ia, kb, ib);
+        if (sw) {
+          key[lo] = kb; key[hi] = ka;
+          id[lo] = ib; id[hi] = ia;
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ int pow2_ceil(int v) {
+  int p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+// ------------------------------------------------------------------ prep
+// One wave per train row: fp64 -> fp32 (zero padded to DP), fl32(||x32||^2)
+// seeds for the L2 accumulator, 0 seeds for L1, +inf on pad rows; running
+// max of ||x||_2^2 and ||x||_1 (fp64, non-negative -> ordered as u64 bits).
+__global__ void __launch_bounds__(256)
+prep_train_kernel(const double* __restrict__ X64, int64_t n, int d, int DP, int64_t n_pad,
+                  float* __restrict__ X32, float* __restrict__ xl2, float* __restrict__ xl1,
+                  unsigned long long* __restrict__ stats) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wstride = (int64_t)gridDim.x * 4;
+  double m2 = 0.0, m1 = 0.0;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n_pad; row += wstride) {
+    double s32 = 0.0, s64 = 0.0, a64 = 0.0;
+    for (int c = lane; c < DP; c += 64) {
+      float v = 0.0f;
+      if (row < n && c < d) {
+        const double x = X64[row * d + c];
+        v = (float)x;
+        s64 += x * x;
+        a64 += __builtin_fabs(x);
+      }
+      X32[row * DP + c] = v;
+      s32 += (double)v * (double)v;
+    }
+    s32 = wave_sum_d(s32);
+    s64 = wave_sum_d(s64);
+    a64 = wave_sum_d(a64);
+    if (lane == 0) {
+      xl2[row] = row < n ? (float)s32 : KNN_INF_F;
+      xl1[row] = row < n ? 0.0f : KNN_INF_F;
+    }
+    m2 = fmax(m2, s64);
+    m1 = fmax(m1, a64);
+  }
+  if (lane == 0) {
+    // small relative slack covers the order of the fp64 sums above
+    atomicMax(&stats[0], (unsigned long long)__double_as_longlong(m2 * (1.0 + 1e-12)));
+    atomicMax(&stats[1], (unsigned long long)__double_as_longlong(m1 * (1.0 + 1e-12)));
+  }
+}
+
+void launch_prep_train(const double* X64, int64_t n, int d, int DP, int64_t n_pad, float* X32,
+                       float* xl2, float* xl1, unsigned long long* stats, hipStream_t s) {
+  int64_t blocks = (n_pad + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(prep_train_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X64, n, d, DP,
+                     n_pad, X32, xl2, xl1, stats);
+}
+
+__global__ void __launch_bounds__(256)
+prep_queries_kernel(const double* __restrict__ Q64, int64_t m, int d, int DP, int64_t m_pad,
+                    float scale, float* __restrict__ Q32) {
+  const int64_t total = m_pad * DP;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * 256) {
+    const int64_t row = e / DP;
+    const int c = (int)(e - row * DP);
+    float v = 0.0f;
+    if (row < m && c < d) v = scale * (float)Q64[row * d + c];  // x(-2) is exact
+    Q32[e] = v;
+  }
+}
+
+void launch_prep_queries(const double* Q64, int64_t m, int d, int DP, int64_t m_pad,
+                         float scale, float* Q32, hipStream_t s) {
+  int64_t blocks = (m_pad * DP + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(prep_queries_kernel, dim3((unsigned)blocks), dim3(256), 0, s, Q64, m, d,
+                     DP, m_pad, scale, Q32);
+}
+
+__global__ void fill_i32_kernel(int32_t* p, int64_t n, int32_t v) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256)
+    p[e] = v;
+}
+void launch_fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t s) {
+  if (n <= 0) return;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(fill_i32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p, n, v);
+}
+
+// ------------------------------------------------------- candidate kernel
+// Sorted insertion of v (< L[R-1]) into the ascending register list (L, I);
+// the previous last entry drops out.  Fully unrolled: no dynamic register
+// indexing (which would go to scratch).
+template <int R>
+__device__ __forceinline__ void list_insert(float (&L)[R], int (&I)[R], float v, int id) {
+#pragma unroll
+  for (int t = R - 1; t > 0; --t) {
+    const bool cp = v < L[t - 1];
+    const bool cc = v < L[t];
+    const float nl = cp ? L[t - 1] : (cc ? v : L[t]);
+    const int ni = cp ? I[t - 1] : (cc ? id : I[t]);
+    L[t] = nl;
+    I[t] = ni;
+  }
+  const bool c0 = v < L[0];
+  I[0] = c0 ? id : I[0];
+  L[0] = c0 ? v : L[0];
+}
+
+// Workgroup = 4 waves = 128 queries; it streams the 32-row train tiles
+// split, split+S, split+2S, ... (round-robin so a run of similar rows is
+// spread over all splits).  Lane (j = lane&31, h = lane>>5) of wave w owns
+// query j of the wave and the train rows rho(i,h) = (i&3) + 8(i>>2) + 4h of
+// every tile (the 32x32 MFMA C/D layout with train rows on A, queries on B).
+//
+// L2, per 32-row tile and wave: DP/2 MFMAs 32x32x2 f32.  A operand (train)
+// from LDS: lane (r, h) reads float4 X[r][8c+4h .. 8c+4h+3] for the four
+// k-steps of group c (ds_read_b128; 16-B row padding makes the 16-lane groups
+// conflict-free since DP/4+1 is odd).  B operand (queries, pre-scaled by -2)
+// stays in VGPRs for the whole kernel with the same k assignment.
+// Accumulators start at ||x_row||^2 (xinit), so acc = ||x||^2 - 2 q.x.
+template <int DP, int R, int METRIC>
+__global__ void __launch_bounds__(256)
+cand_kernel(const float* __restrict__ X32, const float* __restrict__ xinit,
+            const float* __restrict__ Q32, int n_tiles, int S, int n_qt,
+            float* __restrict__ out_v, int* __restrict__ out_i) {
+  constexpr int CPR = DP / 4;      // float4 chunks per row
+  constexpr int LS = DP + 4;       // LDS row stride in floats (16-B pad)
+  constexpr int TF = kTR * LS;     // floats per tile buffer
+  constexpr int NCH = kTR * CPR;   // float4 chunks per tile
+  constexpr int CPT = (NCH + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float lds[2 * TF + 2 * kTR];
+  float* ldsn = lds + 2 * TF;
+
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / n_qt;
+  const int qt = bid - split * n_qt;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int j = lane & 31, h = lane >> 5;
+  const int64_t qg = (int64_t)qt * kQPB + wv * 32 + j;
+  const float* qrow = Q32 + qg * DP;
+
+  float4 qf[METRIC == 0 ? DP / 8 : 1];
+  if constexpr (METRIC == 0) {
+#pragma unroll
+    for (int c = 0; c < DP / 8; ++c) qf[c] = *(const float4*)(qrow + 8 * c + 4 * h);
+  }
+
+  float L[R];
+  int I[R];
+#pragma unroll
+  for (int t = 0; t < R; ++t) { L[t] = KNN_INF_F; I[t] = -1; }
+  float thr = KNN_INF_F;
+
+  const int my_nt = split < n_tiles ? (n_tiles - split + S - 1) / S : 0;
+
+  // Staging registers: global -> VGPR issued before the tile's compute,
+  // VGPR -> LDS after it (named registers, no array: an array here is left
+  // as a scratch alloca by hipcc).
+  static_assert(CPT <= 8, "tile staging supports DP <= 256");
+  float4 st0, st1, st2, st3, st4, st5, st6, st7;
+  float4 stn = make_float4(0.f, 0.f, 0.f, 0.f);
+#define KNN_LD1(i_, v_)                                                               \
+  if constexpr (CPT > i_) {                                                           \
+    const int c_ = tid + 256 * i_;                                                    \
+    if (NCH % 256 == 0 || c_ < NCH) v_ = src_[c_];                                    \
+  }
+#define KNN_ST1(i_, v_)                                                               \
+  if constexpr (CPT > i_) {                                                           \
+    const int c_ = tid + 256 * i_;                                                    \
+    if (NCH % 256 == 0 || c_ < NCH) {                                                 \
+      const int row_ = c_ / CPR, col_ = c_ - row_ * CPR;                              \
+      *(float4*)(base_ + row_ * LS + col_ * 4) = v_;                                  \
+    }                                                                                 \
+  }
+#define KNN_LOAD_TILE(t_)                                                             \
+  do {                                                                                \
+    const float4* src_ = (const float4*)(X32 + (int64_t)(t_) * kTR * DP);             \
+    KNN_LD1(0, st0) KNN_LD1(1, st1) KNN_LD1(2, st2) KNN_LD1(3, st3)                   \
+    KNN_LD1(4, st4) KNN_LD1(5, st5) KNN_LD1(6, st6) KNN_LD1(7, st7)                   \
+    if (tid < kTR / 4) stn = ((const float4*)(xinit + (int64_t)(t_) * kTR))[tid];    \
+  } while (0)
+#define KNN_STORE_TILE(buf_)                                                          \
+  do {                                                                                \
+    float* base_ = lds + (buf_) * TF;                                                 \
+    KNN_ST1(0, st0) KNN_ST1(1, st1) KNN_ST1(2, st2) KNN_ST1(3, st3)                   \
+    KNN_ST1(4, st4) KNN_ST1(5, st5) KNN_ST1(6, st6) KNN_ST1(7, st7)                   \
+    if (tid < kTR / 4) *(float4*)(ldsn + (buf_) * kTR + 4 * tid) = stn;               \
+  } while (0)
+
+  if (my_nt > 0) {
+    KNN_LOAD_TILE(split);
+    KNN_STORE_TILE(0);
+  }
+  __syncthreads();
+
+  for (int it = 0; it < my_nt; ++it) {
+    const int t = split + it * S;
+    const bool more = it + 1 < my_nt;
+    if (more) KNN_LOAD_TILE(t + S);  // in flight during this tile's compute
+    const float* base = lds + (it & 1) * TF;
+    const float* nb = ldsn + (it & 1) * kTR;
+
+    f32x16 acc;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float4 nv = *(const float4*)(nb + 8 * g + 4 * h);
+      acc[4 * g + 0] = nv.x;
+      acc[4 * g + 1] = nv.y;
+      acc[4 * g + 2] = nv.z;
+      acc[4 * g + 3] = nv.w;
+    }
+    if constexpr (METRIC == 0) {
+      const float* arow = base + j * LS + 4 * h;
+#pragma unroll
+      for (int c = 0; c < DP / 8; ++c) {
+        const float4 a = *(const float4*)(arow + 8 * c);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, qf[c].x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, qf[c].y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, qf[c].z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, qf[c].w, acc, 0, 0, 0);
+      }
+    } else {
+      // L1 on the VALU: lane's query against its 16 rows, dims in chunks of 4.
+#pragma unroll 2
+      for (int c = 0; c < CPR; ++c) {
+        const float4 qv = *(const float4*)(qrow + 4 * c);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int r = (i & 3) + 8 * (i >> 2) + 4 * h;
+          const float4 xv = *(const float4*)(base + r * LS + 4 * c);
+          float a = acc[i];
+          a = a + __builtin_fabsf(qv.x - xv.x);
+          a = a + __builtin_fabsf(qv.y - xv.y);
+          a = a + __builtin_fabsf(qv.z - xv.z);
+          a = a + __builtin_fabsf(qv.w - xv.w);
+          acc[i] = a;
+        }
+      }
+    }
+
+    // fused top-R selection: one compare per value once the list is warm
+    float mn = acc[0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) mn = acc[i] < mn ? acc[i] : mn;
+    if (mn < thr) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float v = acc[i];
+        if (v < thr) {
+          list_insert<R>(L, I, v, t * kTR + (i & 3) + 8 * (i >> 2) + 4 * h);
+          thr = L[R - 1];
+        }
+      }
+    }
+
+    if (more) KNN_STORE_TILE((it + 1) & 1);
+    __syncthreads();
+  }
+
+  const int NL = 2 * S;
+  const int64_t o = ((qg * NL) + split * 2 + h) * R;
+#pragma unroll
+  for (int t = 0; t < R; t += 4) {
+    *(float4*)(out_v + o + t) = make_float4(L[t], L[t + 1], L[t + 2], L[t + 3]);
+    *(int4*)(out_i + o + t) = make_int4(I[t], I[t + 1], I[t + 2], I[t + 3]);
+  }
+#undef KNN_LOAD_TILE
+#undef KNN_STORE_TILE
+#undef KNN_LD1
+#undef KNN_ST1
+}
+
+#define KNN_DP_LIST(X) X(8) X(16) X(24) X(32) X(40) X(48) X(64) X(96) X(128) X(160) X(192) X(256)
+
+bool cand_supported(int DP) {
+#define KNN_CASE(v) if (DP == v) return true;
+  KNN_DP_LIST(KNN_CASE)
+#undef KNN_CASE
+  return false;
+}
+
+template <int DP>
+static void launch_cand_dp(int metric, const float* X32, const float* xinit, const float* Q32,
+                           int n_tiles, int S, int n_qt, float* out_v, int* out_i,
+                           hipStream_t s) {
+  dim3 grid((unsigned)(n_qt * S)), block(256);
+  if (metric == 0)
+    hipLaunchKernelGGL((cand_kernel<DP, 16, 0>), grid, block, 0, s, X32, xinit, Q32, n_tiles, S,
+                       n_qt, out_v, out_i);
+  else
+    hipLaunchKernelGGL((cand_kernel<DP, 16, 1>), grid, block, 0, s, X32, xinit, Q32, n_tiles, S,
+                       n_qt, out_v, out_i);
+}
+
+void launch_cand(int metric, int DP, const float* X32, const float* xinit, const float* Q32,
+                 int n_tiles, int S, int n_qt, float* out_v, int* out_i, hipStream_t s) {
+#define KNN_CASE(v)                                                                       \
+  if (DP == v) {                                                                          \
+    launch_cand_dp<v>(metric, X32, xinit, Q32, n_tiles, S, n_qt, out_v, out_i, s);       \
+    return;                                                                               \
+  }
+  KNN_DP_LIST(KNN_CASE)
+#undef KNN_CASE
+}
+
+// ------------------------------------------------ finish: vote / outputs
+// Sorted exact neighbours (dk ascending, di local train index) are in LDS;
+// ls[t] already holds the label of entry t for t < needed.  One wave.
+//
+// Vote (cpp:324-337): scanning t = 0..k-1, label l_t's running count
+// c_t = #{s <= t : l_s == l_t}; the reference keeps the label whose count
+// first strictly exceeds the running max, i.e. l at the first t reaching
+// max_t c_t.  max_label = -1 when k == 0.
+__device__ void finish_single(int64_t q, const double* dk, const int* di, const int* ls, int cnt,
+                              int k, int64_t idx_off, int flag0, const Sink& sink) {
+  const int lane = threadIdx.x & 63;
+  int bc = 0, bt = INT_MAX;
+  for (int t = lane; t < k; t += 64) {
+    const int lt = ls[t];
+    int c = 0;
+    for (int s2 = 0; s2 <= t; ++s2) c += (ls[s2] == lt);
+    if (c > bc) { bc = c; bt = t; }
+  }
+  const int M = wave_max_i(bc);
+  const int tmin = wave_min_i(bc == M ? bt : INT_MAX);
+  int tie_vote = 0;
+  for (int t = lane; t + 1 < k; t += 64)
+    tie_vote |= (dk[t] == dk[t + 1] && ls[t] != ls[t + 1]);
+  tie_vote = wave_max_i(tie_vote);
+  if (lane == 0) {
+    sink.labels[q] = k > 0 ? ls[tmin] : -1;
+    if (sink.flags) {
+      int f = flag0;
+      if (k > 0 && k < cnt && dk[k - 1] == dk[k]) f |= 2;  // KNN_FLAG_TIE_BOUNDARY
+      if (tie_vote) f |= 4;                                // KNN_FLAG_TIE_VOTE
+      sink.flags[q] = f;
+    }
+  }
+  for (int t = lane; t < k; t += 64) {
+    if (sink.idx) sink.idx[q * k + t] = (int64_t)di[t] + idx_off;
+    if (sink.dist) sink.dist[q * k + t] = dk[t];
+  }
+}
+
+__device__ void finish_partial(int64_t q, const double* dk, const int* di, const int* ls,
+                               int cnt, int w, int64_t idx_off, const Sink& sink) {
+  const int lane = threadIdx.x & 63;
+  for (int t = lane; t < w; t += 64) {
+    const bool ok = t < cnt;
+    sink.dist[q * w + t] = ok ? dk[t] : KNN_INF_D;
+    sink.idx[q * w + t] = ok ? (int64_t)di[t] + idx_off : -1;
+    sink.plab[q * w + t] = ok ? ls[t] : -1;
+  }
+}
+
+// --------------------------------------------- merge + exact re-rank
+// One wave per query.  Dynamic LDS: dk[C2] f64 | di[C2] | ls[C2] | uk[U2] f32 | ui[U2].
+template <int METRIC>
+__global__ void __launch_bounds__(64)
+merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, int U, int U2,
+                    int R, TrainDev t, const double* __restrict__ Q64, int W, int C, int C2,
+                    double f_err, Sink sink, int* __restrict__ rescan_q,
+                    int* __restrict__ rescan_cnt) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* dk = (double*)smem;
+  int* di = (int*)(dk + C2);
+  int* ls = di + C2;
+  float* uk = (float*)(ls + C2);
+  int* ui = (int*)(uk + U2);
+  const int64_t q = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int d = t.d;
+
+  // 1. union of the 2S lists; min over lists of their worst kept entry
+  const float* lv = cv + q * U;
+  const int* li = ci + q * U;
+  float mlr = KNN_INF_F;
+  for (int e = lane; e < U2; e += 64) {
+    float v = KNN_INF_F;
+    int id = INT_MAX;
+    if (e < U) {
+      v = lv[e];
+      if (v < KNN_INF_F) id = li[e];
+      if ((e % R) == R - 1) mlr = fminf(mlr, v);
+    }
+    uk[e] = v;
+    ui[e] = id;
+  }
+  mlr = wave_min(mlr);
+  bitonic_sort_lds(uk, ui, U2, lane, 64);
+  int nv = 0;
+  for (int e = lane; e < U2; e += 64) nv += (uk[e] < KNN_INF_F);
+  nv = wave_sum_i(nv);
+
+  // 2. best C by the fp32 proxy; lower bound of every row not re-ranked
+  const int Cn = min(C, nv);
+  const float T = Cn < nv ? uk[Cn] : KNN_INF_F;
+  const float LBa = fminf(T, mlr);
+
+  // 3. exact fp64 distances for the C best, sorted by (dist, idx)
+  const double* qrow = Q64 + q * d;
+  for (int c = lane; c < C2; c += 64) {
+    double v = KNN_INF_D;
+    int id = INT_MAX;
+    if (c < Cn) {
+      id = ui[c];
+      v = exact_dist<METRIC>(qrow, t.X64 + (int64_t)id * d, d);
+    }
+    dk[c] = v;
+    di[c] = id;
+  }
+  bitonic_sort_lds(dk, di, C2, lane, 64);
+
+  // 4. certification: every excluded row has proxy >= LBa, so its exact
+  //    distance is >= the bound below (rigorous fp32 error bound f_err).
+  bool cert;
+  if (!(LBa < KNN_INF_F)) {
+    cert = true;  // every row was re-ranked exactly
+  } else if (Cn < W) {
+    cert = false;
+  } else {
+    double qa = 0.0;
+    for (int c = lane; c < d; c += 64) {
+      const double x = qrow[c];
+      qa += METRIC == 0 ? x * x : __builtin_fabs(x);
+    }
+    qa = wave_sum_d(qa) * (1.0 + 1e-12);
+    const double dw = dk[W - 1];
+    if (METRIC == 0) {
+      const double E = f_err * (t.x2max + 2.0 * __builtin_sqrt(qa) * __builtin_sqrt(t.x2max)) + 1e-30;
+      const double bound = ((double)LBa + qa * (1.0 - 2e-12) - E) * (1.0 - 1e-12);
+      cert = bound > dw * dw * (1.0 + 1e-12);
+    } else {
+      const double E = f_err * (qa + t.x1max) + 1e-30;
+      const double bound = ((double)LBa - E) * (1.0 - 1e-12);
+      cert = bound > dw * (1.0 + 1e-12);
+    }
+  }
+  if (!cert) {
+    if (lane == 0) {
+      const int s = atomicAdd(rescan_cnt, 1);
+      rescan_q[s] = (int)q;
+    }
+    return;
+  }
+
+  // 5. outputs
+  const int need = sink.mode == MODE_SINGLE ? sink.k : sink.w;
+  for (int c = lane; c < need && c < Cn; c += 64) ls[c] = t.lab[di[c]];
+  __syncthreads();
+  if (sink.mode == MODE_SINGLE)
+    finish_single(q, dk, di, ls, Cn, sink.k, sink.idx_off, 0, sink);
+  else
+    finish_partial(q, dk, di, ls, Cn, sink.w, sink.idx_off, sink);
+}
+
+void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, const TrainDev& t,
+                         const double* Q64, int64_t m, int W, int C, double f_err,
+                         const Sink& sink, int* rescan_q, int* rescan_cnt, hipStream_t s) {
+  const int R = 16;
+  const int U = NL * R;
+  int U2 = 1;
+  while (U2 < U) U2 <<= 1;
+  int C2 = 1;
+  while (C2 < C) C2 <<= 1;
+  const size_t lds = (size_t)C2 * (8 + 4 + 4) + (size_t)U2 * 8;
+  if (metric == 0)
+    hipLaunchKernelGGL((merge_rerank_kernel<0>), dim3((unsigned)m), dim3(64), lds, s, cv, ci, U,
+                       U2, R, t, Q64, W, C, C2, f_err, sink, rescan_q, rescan_cnt);
+  else
+    hipLaunchKernelGGL((merge_rerank_kernel<1>), dim3((unsigned)m), dim3(64), lds, s, cv, ci, U,
+                       U2, R, t, Q64, W, C, C2, f_err, sink, rescan_q, rescan_cnt);
+}
+
+// ------------------------------------------------------ exact rescan path
+// Queries whose candidate set is not certified (near-duplicate clusters,
+// large exact-tie groups, adversarial row orders) are re-done exactly:
+// every row's fp64 reference distance, kSortN rows per block sorted in LDS,
+// the best W per block kept, then lists reduced by the same sort until one
+// remains.  Rare by construction; correctness path, not the fast path.
+template <int METRIC>
+__global__ void __launch_bounds__(256)
+rescan_chunk_kernel(TrainDev t, const double* __restrict__ Q64, const int* __restrict__ rescan_q,
+                    int f0, int W, int n_chunks, double* __restrict__ pk, int* __restrict__ pi) {
+  __shared__ double sk[kSortN];
+  __shared__ int si[kSortN];
+  const int chunk = blockIdx.x;
+  const int64_t q = rescan_q[f0 + blockIdx.y];
+  const double* qrow = Q64 + q * t.d;
+  for (int e = threadIdx.x; e < kSortN; e += 256) {
+    const int64_t row = (int64_t)chunk * kSortN + e;
+    double v = KNN_INF_D;
+    int id = INT_MAX;
+    if (row < t.n) {
+      v = exact_dist<METRIC>(qrow, t.X64 + row * t.d, t.d);
+      id = (int)row;
+    }
+    sk[e] = v;
+    si[e] = id;
+  }
+  bitonic_sort_lds(sk, si, kSortN, threadIdx.x, 256);
+  const int64_t o = ((int64_t)blockIdx.y * n_chunks + chunk) * W;
+  for (int e = threadIdx.x; e < W; e += 256) {
+    pk[o + e] = sk[e];
+    pi[o + e] = si[e];
+  }
+}
+
+__global__ void __launch_bounds__(256)
+rescan_reduce_kernel(const double* __restrict__ ik, const int* __restrict__ ii, int P, int W,
+                     int G, double* __restrict__ ok, int* __restrict__ oi, int P2) {
+  __shared__ double sk[kSortN];
+  __shared__ int si[kSortN];
+  const int b = blockIdx.x, f = blockIdx.y;
+  const int l0 = b * G, l1 = min(P, l0 + G);
+  const int ne = (l1 - l0) * W;
+  const int64_t src = ((int64_t)f * P + l0) * W;
+  for (int e = threadIdx.x; e < kSortN; e += 256) {
+    sk[e] = e < ne ? ik[src + e] : KNN_INF_D;
+    si[e] = e < ne ? ii[src + e] : INT_MAX;
+  }
+  bitonic_sort_lds(sk, si, kSortN, threadIdx.x, 256);
+  const int64_t o = ((int64_t)f * P2 + b) * W;
+  for (int e = threadIdx.x; e < W; e += 256) {
+    ok[o + e] = sk[e];
+    oi[o + e] = si[e];
+  }
+}
+
+__global__ void __launch_bounds__(64)
+rescan_finish_kernel(TrainDev t, const double* __restrict__ pk, const int* __restrict__ pi,
+                     const int* __restrict__ rescan_q, int f0, int W, Sink sink) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* dk = (double*)smem;
+  int* di = (int*)(dk + W);
+  int* ls = di + W;
+  const int f = blockIdx.x;
+  const int64_t q = rescan_q[f0 + f];
+  const int lane = threadIdx.x;
+  const int cnt = (int)(t.n < W ? t.n : W);
+  for (int e = lane; e < W; e += 64) {
+    dk[e] = pk[(int64_t)f * W + e];
+    di[e] = pi[(int64_t)f * W + e];
+    ls[e] = e < cnt ? t.lab[di[e]] : -1;
+  }
+  __syncthreads();
+  if (sink.mode == MODE_SINGLE)
+    finish_single(q, dk, di, ls, cnt, sink.k, sink.idx_off, 1 /*KNN_FLAG_EXACT_RESCAN*/, sink);
+  else
+    finish_partial(q, dk, di, ls, cnt, sink.w, sink.idx_off, sink);
+}
+
+size_t rescan_scratch_entries(int64_t n, int W) {
+  const int64_t n_chunks = (n + kSortN - 1) / kSortN;
+  return (size_t)n_chunks * W;
+}
+
+void launch_rescan(int metric, const TrainDev& t, const double* Q64, const int* rescan_q,
+                   int f0, int nf, int W, double* pa_k, int* pa_i, double* pb_k, int* pb_i,
+                   const Sink& sink, hipStream_t s) {
+  const int n_chunks = (int)((t.n + kSortN - 1) / kSortN);
+  if (metric == 0)
+    hipLaunchKernelGGL((rescan_chunk_kernel<0>), dim3(n_chunks, nf), dim3(256), 0, s, t, Q64,
+                       rescan_q, f0, W, n_chunks, pa_k, pa_i);
+  else
+    hipLaunchKernelGGL((rescan_chunk_kernel<1>), dim3(n_chunks, nf), dim3(256), 0, s, t, Q64,
+                       rescan_q, f0, W, n_chunks, pa_k, pa_i);
+  int P = n_chunks;
+  double* ik = pa_k; int* ii = pa_i;
+  double* ok = pb_k; int* oi = pb_i;
+  const int G = kSortN / W;  // W <= kMaxK + 1 <= kSortN / 2
+  while (P > 1) {
+    const int P2 = (P + G - 1) / G;
+    hipLaunchKernelGGL(rescan_reduce_kernel, dim3(P2, nf), dim3(256), 0, s, ik, ii, P, W, G, ok,
+                       oi, P2);
+    double* tk = ik; ik = ok; ok = tk;
+    int* ti = ii; ii = oi; oi = ti;
+    P = P2;
+  }
+  const size_t lds = (size_t)W * 16;
+  hipLaunchKernelGGL(rescan_finish_kernel, dim3(nf), dim3(64), lds, s, t, ik, ii, rescan_q, f0,
+                     W, sink);
+}
+
+// ------------------------------------------ train-sharded k-way merge + vote
+// lists [parts][m][w] sorted by (dist, global idx); one wave per query merges
+// them (bitonic in LDS) and runs the reference vote on the first k.
+__global__ void __launch_bounds__(64)
+merge_vote_partials_kernel(const double* __restrict__ dist, const int64_t* __restrict__ idx,
+                           const int32_t* __restrict__ lab, int parts, int64_t m, int w, int k,
+                           int P2, int64_t q0, Sink sink) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* dk = (double*)smem;
+  int64_t* gi = (int64_t*)(dk + P2);
+  int* ls = (int*)(gi + P2);
+  const int64_t q = q0 + blockIdx.x;  // query in the [parts][m][w] lists
+  const int64_t qo = blockIdx.x;      // row in the outputs
+  const int lane = threadIdx.x;
+  const int ne = parts * w;
+  for (int e = lane; e < P2; e += 64) {
+    double v = KNN_INF_D;
+    int64_t id = LLONG_MAX;
+    if (e < ne) {
+      const int p = e / w, c = e - p * w;
+      const int64_t src = ((int64_t)p * m + q) * w + c;
+      if (idx[src] >= 0) { v = dist[src]; id = idx[src]; }
+    }
+    dk[e] = v;
+    gi[e] = id;
+  }
+  bitonic_sort_lds(dk, gi, P2, lane, 64);
+  // labels travel with the lists: place each one at its entry's sorted slot
+  for (int e = lane; e < ne; e += 64) {
+    const int p = e / w, c = e - p * w;
+    const int64_t src = ((int64_t)p * m + q) * w + c;
+    if (idx[src] < 0) continue;
+    // position of (dist, idx) in the sorted array: binary search
+    const double v = dist[src];
+    const int64_t id = idx[src];
+    int lo = 0, hi = P2;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (pair_less(dk[mid], gi[mid], v, id)) lo = mid + 1; else hi = mid;
+    }
+    if (lo < k + 1) ls[lo] = lab[src];
+  }
+  __syncthreads();
+  int cnt = 0;
+  for (int e = lane; e < P2; e += 64) cnt += (gi[e] != LLONG_MAX);
+  cnt = wave_sum_i(cnt);
+  int bc = 0, bt = INT_MAX;
+  for (int t = lane; t < k; t += 64) {
+    const int lt = ls[t];
+    int c = 0;
+    for (int s2 = 0; s2 <= t; ++s2) c += (ls[s2] == lt);
+    if (c > bc) { bc = c; bt = t; }
+  }
+  const int M = wave_max_i(bc);
+  const int tmin = wave_min_i(bc == M ? bt : INT_MAX);
+  int tie_vote = 0;
+  for (int t = lane; t + 1 < k; t += 64) tie_vote |= (dk[t] == dk[t + 1] && ls[t] != ls[t + 1]);
+  tie_vote = wave_max_i(tie_vote);
+  if (lane == 0) {
+    sink.labels[qo] = k > 0 ? ls[tmin] : -1;
+    if (sink.flags) {
+      int f = 0;
+      if (k > 0 && k < cnt && dk[k - 1] == dk[k]) f |= 2;
+      if (tie_vote) f |= 4;
+      sink.flags[qo] = f;
+    }
+  }
+  for (int t = lane; t < k; t += 64) {
+    if (sink.idx) sink.idx[qo * k + t] = gi[t];
+    if (sink.dist) sink.dist[qo * k + t] = dk[t];
+  }
+}
+
+void launch_merge_vote_partials(const double* dist, const int64_t* idx, const int32_t* lab,
+                                int parts, int64_t m, int w, int k, int32_t* out_lab,
+                                int64_t* out_idx, double* out_dist, int32_t* out_flags,
+                                hipStream_t s, int64_t q0, int64_t mq) {
+  if (mq < 0) mq = m - q0;
+  if (mq <= 0) return;
+  int P2 = 1;
+  while (P2 < parts * w) P2 <<= 1;
+  Sink sink{};
+  sink.mode = MODE_SINGLE;
+  sink.k = k;
+  sink.labels = out_lab;
+  sink.idx = out_idx;
+  sink.dist = out_dist;
+  sink.flags = out_flags;
+  const size_t lds = (size_t)P2 * (8 + 8 + 4);
+  hipLaunchKernelGGL(merge_vote_partials_kernel, dim3((unsigned)mq), dim3(64), lds, s, dist, idx,
+                     lab, parts, m, w, k, P2, q0, sink);
+}
+
+}  // namespace knnk

@@ -1,0 +1,264 @@
+"""Python mirror of the MI355X KNN classifier (ctypes over lib/libknn_amd.so).
+
+The reference (Jason-Woo/-MPI-KNN-, knn_mpi.cpp) has no library API: its
+interface is the constant block (cpp:108-119), the CSV formats and the
+outputs.  `KnnConfig` carries those constants under the same names;
+`Classifier` is the per-GPU hot path (set_train / classify); `run_reference_
+program` reproduces main() end to end through the native host driver.
+
+There is no CPU compute path: every call goes through the HIP library and
+fails loudly (KnnError) when the library or the GPU is missing.
+"""
+import ctypes
+import dataclasses
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libknn_amd.so")
+DRIVER_PATH = os.path.join(HERE, "bin", "knn_mpi_amd")
+
+L2, L1 = 0, 1
+FLAG_EXACT_RESCAN, FLAG_TIE_BOUNDARY, FLAG_TIE_VOTE = 1, 2, 4
+EXPORTED = (
+    "knn_version", "knn_last_error", "knn_device_count", "knn_create", "knn_destroy",
+    "knn_set_train", "knn_set_train_device", "knn_classify", "knn_classify_device",
+    "knn_search_partial_device", "knn_merge_vote_device", "knn_sync", "knn_last_rescan_count",
+    "knn_group_create", "knn_group_destroy", "knn_group_set_train", "knn_group_classify",
+    "knn_group_last_compute_seconds", "knn_set_timing", "knn_last_phase_ms",
+    "knn_last_geometry",
+)
+PHASE_PREP, PHASE_CANDIDATE, PHASE_RERANK, PHASE_RESCAN = 0, 1, 2, 3
+
+
+class KnnError(RuntimeError):
+    pass
+
+
+@dataclasses.dataclass
+class KnnConfig:
+    """The reference's configuration constants (cpp:108-119), same defaults."""
+    dim: int = 784
+    K: int = 50
+    N_train: int = 60000
+    N_test: int = 10000
+    N_val: int = 10000
+    class_cnt: int = 10
+    Euclidean_distance: bool = True
+    Normalize: bool = True
+    Validation: bool = True
+    train_file_name: str = "mnist_train.csv"
+    validation_file_name: str = "mnist_validation.csv"
+    test_file_name: str = "mnist_test.csv"
+
+
+def build(jobs=8):
+    subprocess.run(["make", "-s", "-j%d" % jobs, "-C", HERE], check=True)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise KnnError("HIP library not built: %s (run build())" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    P, i32, i64, f64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
+    sig = {
+        "knn_version": ([], ctypes.c_char_p),
+        "knn_last_error": ([], ctypes.c_char_p),
+        "knn_device_count": ([], ctypes.c_int),
+        "knn_create": ([ctypes.POINTER(P), ctypes.c_int], ctypes.c_int),
+        "knn_destroy": ([P], ctypes.c_int),
+        "knn_set_train": ([P, P, P, i64, i32, i32], ctypes.c_int),
+        "knn_set_train_device": ([P, P, P, i64, i32, i32, i64], ctypes.c_int),
+        "knn_classify": ([P, P, i64, i32, i32, P, P, P, P], ctypes.c_int),
+        "knn_classify_device": ([P, P, i64, i32, i32, P, P, P, P, P], ctypes.c_int),
+        "knn_search_partial_device": ([P, P, i64, i32, i32, P, P, P, P], ctypes.c_int),
+        "knn_merge_vote_device": ([P, P, P, P, i32, i64, i32, i32, P, P, P, P, P], ctypes.c_int),
+        "knn_sync": ([P], ctypes.c_int),
+        "knn_last_rescan_count": ([P], i64),
+        "knn_group_create": ([ctypes.POINTER(P), ctypes.c_int, P, ctypes.c_int], ctypes.c_int),
+        "knn_group_destroy": ([P], ctypes.c_int),
+        "knn_group_set_train": ([P, P, P, i64, i32, i32], ctypes.c_int),
+        "knn_group_classify": ([P, P, i64, i32, i32, P, P, P, P], ctypes.c_int),
+        "knn_group_last_compute_seconds": ([P], f64),
+        "knn_set_timing": ([P, ctypes.c_int], ctypes.c_int),
+        "knn_last_phase_ms": ([P, ctypes.c_int], f64),
+        "knn_last_geometry": ([P, ctypes.POINTER(i64)], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc != 0:
+        raise KnnError("knn error %d: %s" % (rc, lib().knn_last_error().decode()))
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+def _f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+class Classifier:
+    """One GPU (≙ one MPI rank).  set_train ≙ MPI_Bcast of Data_train
+    (cpp:224-225); classify ≙ the query loop cpp:358-381."""
+
+    def __init__(self, device=0):
+        self._h = ctypes.c_void_p()
+        _check(lib().knn_create(ctypes.byref(self._h), device))
+        self.device = device
+        self.n_train = 0
+        self.dim = 0
+
+    def close(self):
+        if self._h:
+            lib().knn_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_train(self, X, labels, class_cnt):
+        X = _f64(X)
+        labels = np.ascontiguousarray(labels, dtype=np.int32)
+        n, d = X.shape
+        _check(lib().knn_set_train(self._h, _ptr(X), _ptr(labels), n, d, int(class_cnt)))
+        self.n_train, self.dim = n, d
+        self._keep = None
+
+    def set_train_device(self, dX_ptr, dlab_ptr, n, d, class_cnt, idx_offset=0, keep=None):
+        """Device pointers (e.g. torch tensors' data_ptr()); `keep` holds the
+        owning objects alive for the library (the pointers are borrowed)."""
+        _check(lib().knn_set_train_device(self._h, dX_ptr, dlab_ptr, n, d, int(class_cnt),
+                                          int(idx_offset)))
+        self.n_train, self.dim = n, d
+        self._keep = keep
+
+    def classify(self, Q, k, metric=L2, return_neighbors=False):
+        """Returns labels (int32[m]) and, if requested, (idx[m,k], dist[m,k], flags[m])."""
+        Q = _f64(Q)
+        m = Q.shape[0]
+        labels = np.empty(m, np.int32)
+        flags = np.empty(m, np.int32)
+        idx = np.empty((m, max(k, 1)), np.int64) if return_neighbors else None
+        dist = np.empty((m, max(k, 1)), np.float64) if return_neighbors else None
+        _check(lib().knn_classify(self._h, _ptr(Q), m, int(k), int(metric), _ptr(labels),
+                                  _ptr(idx), _ptr(dist), _ptr(flags)))
+        if return_neighbors:
+            return labels, idx[:, :k], dist[:, :k], flags
+        return labels
+
+    def classify_device(self, dQ_ptr, m, k, metric, d_labels, d_idx=None, d_dist=None,
+                        d_flags=None, stream=None):
+        _check(lib().knn_classify_device(self._h, dQ_ptr, m, int(k), int(metric), d_labels, d_idx,
+                                         d_dist, d_flags, stream))
+
+    def search_partial_device(self, dQ_ptr, m, w, metric, d_dist, d_idx, d_lab, stream=None):
+        _check(lib().knn_search_partial_device(self._h, dQ_ptr, m, int(w), int(metric), d_dist,
+                                               d_idx, d_lab, stream))
+
+    def merge_vote_device(self, d_dist, d_idx, d_lab, parts, m, w, k, d_labels, d_out_idx=None,
+                          d_out_dist=None, d_flags=None, stream=None):
+        _check(lib().knn_merge_vote_device(self._h, d_dist, d_idx, d_lab, int(parts), m, int(w),
+                                           int(k), d_labels, d_out_idx, d_out_dist, d_flags,
+                                           stream))
+
+    def sync(self):
+        _check(lib().knn_sync(self._h))
+
+    def last_rescan_count(self):
+        return int(lib().knn_last_rescan_count(self._h))
+
+    def set_timing(self, enable=True):
+        _check(lib().knn_set_timing(self._h, int(bool(enable))))
+
+    def last_phase_ms(self, phase):
+        return float(lib().knn_last_phase_ms(self._h, int(phase)))
+
+    def last_geometry(self):
+        out = (ctypes.c_int64 * 4)()
+        _check(lib().knn_last_geometry(self._h, out))
+        return dict(workgroups=out[0], splits=out[1], lists=out[2], rerank=out[3])
+
+
+class Group:
+    """Single-process multi-GPU classifier over RCCL (mode 0 query-sharded,
+    1 train-sharded); see include/knn_amd.h."""
+
+    def __init__(self, devices, mode=0):
+        self._h = ctypes.c_void_p()
+        arr = (ctypes.c_int * len(devices))(*devices)
+        _check(lib().knn_group_create(ctypes.byref(self._h), len(devices), arr, int(mode)))
+
+    def close(self):
+        if self._h:
+            lib().knn_group_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_train(self, X, labels, class_cnt):
+        X = _f64(X)
+        labels = np.ascontiguousarray(labels, dtype=np.int32)
+        n, d = X.shape
+        _check(lib().knn_group_set_train(self._h, _ptr(X), _ptr(labels), n, d, int(class_cnt)))
+
+    def classify(self, Q, k, metric=L2, return_neighbors=False):
+        Q = _f64(Q)
+        m = Q.shape[0]
+        labels = np.empty(m, np.int32)
+        flags = np.empty(m, np.int32)
+        idx = np.empty((m, max(k, 1)), np.int64) if return_neighbors else None
+        dist = np.empty((m, max(k, 1)), np.float64) if return_neighbors else None
+        _check(lib().knn_group_classify(self._h, _ptr(Q), m, int(k), int(metric), _ptr(labels),
+                                        _ptr(idx), _ptr(dist), _ptr(flags)))
+        if return_neighbors:
+            return labels, idx[:, :k], dist[:, :k], flags
+        return labels
+
+    def last_compute_seconds(self):
+        return float(lib().knn_group_last_compute_seconds(self._h))
+
+
+def run_reference_program(cfg: KnnConfig, workdir, gpus=1, mode="query", extra=()):
+    """Runs the native drop-in driver (bin/knn_mpi_amd) like `mpiexec knn_mpi`
+    in `workdir`; returns its stdout."""
+    if not os.path.exists(DRIVER_PATH):
+        raise KnnError("driver not built: " + DRIVER_PATH)
+    args = [DRIVER_PATH]
+    for f in ("dim", "K", "N_train", "N_test", "N_val", "class_cnt"):
+        args += ["--" + f, str(getattr(cfg, f))]
+    for f in ("Euclidean_distance", "Normalize", "Validation"):
+        args += ["--" + f, "true" if getattr(cfg, f) else "false"]
+    args += ["--train_file", cfg.train_file_name, "--validation_file", cfg.validation_file_name,
+             "--test_file", cfg.test_file_name, "--gpus", str(gpus), "--mode", mode]
+    args += list(extra)
+    r = subprocess.run(args, cwd=workdir, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise KnnError("driver failed (%d): %s" % (r.returncode, r.stderr.strip()))
+    return r.stdout

@@ -1,0 +1,166 @@
+/* knn_amd.h -- C ABI of the MI355X-native brute-force KNN classifier.
+ *
+ * This is the drop-in boundary for the hot path of Jason-Woo/-MPI-KNN-
+ * (/root/reference/knn_mpi.cpp, cited "cpp:N").  The reference has no
+ * library interface: its hot path is inlined in main() (cpp:308-381), fed by
+ * the constant block (cpp:108-119) and the MPI collectives (cpp:224-227,
+ * 340, 383).  Each entry point below replaces one piece of that:
+ *
+ *   knn_set_train*      MPI_Bcast of Data_train/Train_label (cpp:224-225) and
+ *                       the train side of the config block (N_train, dim,
+ *                       class_cnt: cpp:108-113)
+ *   knn_classify*       the query loop: per-pair Euclidean_D/Manhattan_D
+ *                       (cpp:33-67) -> std::sort of all N_train records
+ *                       (cpp:323/366) -> first-to-max vote over K
+ *                       (cpp:324-337/367-380) -> Val/Test_label_buffer
+ *   knn_search_partial  train-sharded variant (new; north_star mode b):
+ *                       exact local top-w per query with global indices
+ *   knn_merge_vote      k-way merge of per-shard lists + the vote (cpp:324-337)
+ *   knn_group_*         single-process multi-GPU driver over RCCL/xGMI that
+ *                       replaces MPI_Bcast/Scatter/Gather (cpp:224-227, 383)
+ *
+ * Semantics (identical to the reference on the same fp64 inputs):
+ *   - distances are the reference's fp64 values: sqrt of the sequential
+ *     sum of (q_i - x_i)^2 (no FMA) for metric 0, sum of |q_i - x_i| for
+ *     metric 1;
+ *   - neighbours are ordered by ascending distance; exact distance ties are
+ *     ordered by train index (the reference's std::sort leaves tie order
+ *     unspecified -- such queries are reported in out_flags);
+ *   - label = first label whose running count strictly exceeds the running
+ *     maximum while scanning the k nearest in order; -1 when k == 0.
+ *   - the GPU computes a certified candidate set with fp32 MFMA and re-ranks
+ *     it in fp64; queries whose candidate set cannot be certified are
+ *     re-run exactly (fp64 over all rows).  No CPU fallback exists: without
+ *     a usable HIP device every call fails with KNN_ERR_DEVICE.
+ *
+ * Conventions: plain pointers and sizes; return 0 on success, a negative
+ * KNN_ERR_* code on failure (message via knn_last_error(), thread-local).
+ * A host driver maps non-zero to exit(1), like MPI_Abort(..., 1)
+ * (cpp:127-129).  One host thread per context; contexts are independent.
+ * "Host" pointers are ordinary CPU memory; "_device" variants take device
+ * pointers on the context's GPU and an optional hipStream_t (NULL = the
+ * context's own stream).
+ */
+#ifndef KNN_AMD_H
+#define KNN_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KNN_OK 0
+#define KNN_ERR_ARG -1     /* bad argument (sizes, k > n_train, label range) */
+#define KNN_ERR_DEVICE -2  /* no HIP device / HIP runtime error */
+#define KNN_ERR_STATE -3   /* e.g. classify before set_train */
+#define KNN_ERR_NOMEM -4   /* device allocation failed */
+#define KNN_ERR_COMM -5    /* RCCL failure */
+
+#define KNN_METRIC_L2 0 /* Euclidean_distance = true  (cpp:114, 320, 363) */
+#define KNN_METRIC_L1 1 /* Euclidean_distance = false (cpp:114, 321, 364) */
+
+/* out_flags bits (per query) */
+#define KNN_FLAG_EXACT_RESCAN 1 /* candidate set not certified; exact fp64 rescan used */
+#define KNN_FLAG_TIE_BOUNDARY 2 /* dist[k-1] == dist[k]: membership tie at the k-th */
+#define KNN_FLAG_TIE_VOTE 4     /* equal distances with different labels inside top-k */
+
+typedef struct knn_ctx knn_ctx;
+typedef struct knn_group knn_group;
+
+/* Version string of the library build. */
+const char* knn_version(void);
+/* Last error message of the calling thread ("" if none). */
+const char* knn_last_error(void);
+/* Number of visible HIP devices (0 if none). */
+int knn_device_count(void);
+
+/* Context on HIP device `device` (replaces MPI_Init + per-rank state, cpp:123-125). */
+int knn_create(knn_ctx** out, int device);
+int knn_destroy(knn_ctx* ctx);
+
+/* Train set from host memory: X row-major n x d fp64 (Data_train, cpp:140),
+ * labels (Train_label, cpp:141) with 0 <= label < class_cnt.  The library
+ * copies both to HBM (≙ MPI_Bcast cpp:224-225). */
+int knn_set_train(knn_ctx* ctx, const double* X, const int32_t* labels, int64_t n,
+                  int32_t d, int32_t class_cnt);
+/* Same from device memory on ctx's GPU (e.g. after an RCCL broadcast).
+ * dX/dlabels are borrowed and must stay valid until the next set_train or
+ * destroy.  idx_offset is added to every reported neighbour index (train
+ * sharding: global index of this shard's first row). */
+int knn_set_train_device(knn_ctx* ctx, const double* dX, const int32_t* dlabels, int64_t n,
+                         int32_t d, int32_t class_cnt, int64_t idx_offset);
+
+/* Classify m queries Q (row-major m x d fp64, same d as the train set).
+ * out_labels[m] (Test_label_buffer, cpp:380) required; out_idx[m*k]
+ * (global train indices) and out_dist[m*k] (fp64 reference distances) and
+ * out_flags[m] nullable.  Host pointers. */
+int knn_classify(knn_ctx* ctx, const double* Q, int64_t m, int32_t k, int32_t metric,
+                 int32_t* out_labels, int64_t* out_idx, double* out_dist,
+                 int32_t* out_flags);
+/* Device-pointer variant; enqueued on `stream` (hipStream_t, NULL = ctx
+ * stream).  Returns after enqueueing when no exact rescan is needed; may
+ * synchronise the stream once to size the rescan. */
+int knn_classify_device(knn_ctx* ctx, const double* dQ, int64_t m, int32_t k, int32_t metric,
+                        int32_t* d_labels, int64_t* d_idx, double* d_dist, int32_t* d_flags,
+                        void* stream);
+
+/* Train-sharded building block: exact top-w of THIS context's shard for
+ * each query, sorted by (dist, global idx), with each neighbour's label.
+ * Rows beyond the shard size are padded with dist=+inf, idx=-1, label=-1.
+ * Device pointers: d_dist[m*w], d_idx[m*w], d_lab[m*w]. */
+int knn_search_partial_device(knn_ctx* ctx, const double* dQ, int64_t m, int32_t w,
+                              int32_t metric, double* d_dist, int64_t* d_idx,
+                              int32_t* d_lab, void* stream);
+/* k-way merge of `parts` sorted lists per query, laid out [parts][m][w]
+ * (the layout an all-gather of knn_search_partial outputs produces), then
+ * the reference vote over the first k of the merged order.  Device pointers;
+ * d_out_idx/d_out_dist/d_flags nullable. */
+int knn_merge_vote_device(knn_ctx* ctx, const double* d_dist, const int64_t* d_idx,
+                          const int32_t* d_lab, int32_t parts, int64_t m, int32_t w, int32_t k,
+                          int32_t* d_labels, int64_t* d_out_idx, double* d_out_dist,
+                          int32_t* d_flags, void* stream);
+
+/* Per-phase device timing with HIP events recorded on the stream the
+ * kernels run on (off by default).  Phases: 0 = query prep, 1 = candidate
+ * kernel (fused MFMA distance + top-R), 2 = merge/re-rank/vote, 3 = exact
+ * rescan.  Values refer to the last classify/search call (0 if not run). */
+#define KNN_PHASE_PREP 0
+#define KNN_PHASE_CANDIDATE 1
+#define KNN_PHASE_RERANK 2
+#define KNN_PHASE_RESCAN 3
+int knn_set_timing(knn_ctx* ctx, int enable);
+double knn_last_phase_ms(knn_ctx* ctx, int phase);
+/* Geometry of the last candidate launch: out[0]=workgroups, out[1]=splits
+ * per query tile, out[2]=lists per query, out[3]=re-rank count C. */
+int knn_last_geometry(knn_ctx* ctx, int64_t out[4]);
+
+/* Synchronise the context's stream. */
+int knn_sync(knn_ctx* ctx);
+/* Last classify's count of queries that needed the exact rescan. */
+int64_t knn_last_rescan_count(knn_ctx* ctx);
+
+/* ---- single-process multi-GPU group over RCCL (xGMI) ---------------------
+ * mode 0 = query-sharded: the train set is RCCL-broadcast from device
+ *          devs[0] to every GPU (≙ MPI_Bcast cpp:224-225); queries are
+ *          split into contiguous shards (≙ MPI_Scatter cpp:226-227, ragged
+ *          shards allowed); labels land in one host array (≙ MPI_Gather
+ *          cpp:340/383).
+ * mode 1 = train-sharded: every GPU holds n/G rows; each computes the exact
+ *          local top-(k+1) for all queries; ncclAllGather exchanges the lists;
+ *          each GPU k-way merges and votes its slice of the queries. */
+int knn_group_create(knn_group** out, int ndev, const int* devs, int mode);
+int knn_group_destroy(knn_group* g);
+int knn_group_set_train(knn_group* g, const double* X, const int32_t* labels, int64_t n,
+                        int32_t d, int32_t class_cnt);
+int knn_group_classify(knn_group* g, const double* Q, int64_t m, int32_t k, int32_t metric,
+                       int32_t* out_labels, int64_t* out_idx, double* out_dist,
+                       int32_t* out_flags);
+/* Seconds of the last group classify spent between the first enqueue and
+ * the last device completion (device-resident inputs, excludes H2D/D2H). */
+double knn_group_last_compute_seconds(knn_group* g);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KNN_AMD_H */

@@ -1,0 +1,251 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference.
+
+Two anchors:
+  * golden fixtures produced by the reference binary itself (tests/golden);
+  * the CPU oracle (oracle/knn_oracle.cpp, itself pinned to those fixtures)
+    on seeded inputs at sizes the oracle finishes in seconds, including the
+    edge cases the reference's structure implies (ragged sizes, k=1, k=n,
+    tiny n, duplicated rows / exact ties, adversarial row order, L1).
+Bar: labels identical; neighbour indices and fp64 distances bit-identical,
+except that among EXACTLY equal distances the reference's std::sort order
+is unspecified -- there we require the same distance multiset and accept
+any order (such queries carry KNN_FLAG_TIE_* in out_flags).
+"""
+import numpy as np
+import pytest
+
+import golden_io
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def knn():
+    import importlib.util
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location(
+        "knn_amd", os.path.join(root, "-mpi-knn-_amd", "knn_amd.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    if mod.lib().knn_device_count() < 1:
+        pytest.fail("no HIP device visible: the KNN path has no CPU fallback")
+    return mod
+
+
+@pytest.fixture(scope="module")
+def clf(knn):
+    c = knn.Classifier(0)
+    yield c
+    c.close()
+
+
+def assert_neighbors_match(idx, dist, widx, wdist, flags=None, labels_msg=""):
+    """Bit-exact distances; indices exact except inside groups of equal distance."""
+    assert idx.shape == widx.shape
+    dbits, wbits = dist.view(np.int64), wdist.view(np.int64)
+    bad = np.nonzero((dbits != wbits).any(1))[0]
+    assert bad.size == 0, "distance mismatch at queries %s" % bad[:10]
+    diff = np.nonzero((idx != widx).any(1))[0]
+    for q in diff:
+        # differing indices are only allowed inside runs of equal distances
+        d = dist[q]
+        for t in np.nonzero(idx[q] != widx[q])[0]:
+            run = np.nonzero(d == d[t])[0]
+            assert len(run) > 1, "query %d pos %d: index differs without a tie" % (q, t)
+            # same set of indices over the full tie run is required unless the run
+            # crosses the k boundary (then membership itself is tie-ambiguous)
+            if run[-1] < len(d) - 1:
+                assert set(idx[q][run]) == set(widx[q][run]), "query %d tie group differs" % q
+        if flags is not None:
+            assert flags[q] & 6, "query %d differs but is not flagged as a tie" % q
+
+
+def run_case(clf, knn, train, lab, queries, k, metric, classes):
+    clf.set_train(train, lab, classes)
+    got, idx, dist, flags = clf.classify(queries, k, metric, return_neighbors=True)
+    want, widx, wdist = oracle.knn(train, lab, queries, k, metric == 0, classes, n_out=k)
+    tie_vote = (flags & knn.FLAG_TIE_VOTE) != 0
+    assert (got[~tie_vote] == want[~tie_vote]).all(), "labels differ on untied queries"
+    assert_neighbors_match(idx, dist, widx, wdist, flags)
+    return got, want, flags
+
+
+@pytest.mark.parametrize("name", golden_io.names())
+def test_golden_fixture(name, clf, knn, fmt_cout):
+    fx = golden_io.Fixture(name)
+    s = fx.spec
+    tr, trl, te, tel, va, val_ = fx.normalized()
+    metric = 0 if s["Euclidean_distance"] else 1
+    K = s["K"]
+    clf.set_train(tr, trl, s["class_cnt"])
+    got, idx, dist, flags = clf.classify(te, K, metric, return_neighbors=True)
+    np.testing.assert_array_equal(got, fx.test_labels)
+    nq = fx.test_nbr_idx.shape[0]
+    assert_neighbors_match(idx[:nq], dist[:nq], fx.test_nbr_idx[:nq, :K],
+                           fx.test_nbr_dist[:nq, :K], flags[:nq])
+    if s["Validation"]:
+        vl, vidx, vdist, vflags = clf.classify(va, K, metric, return_neighbors=True)
+        acc = float((vl == val_).sum()) / len(val_)  # acc_calc, cpp:69-84
+        assert "accuracy = " + fmt_cout(acc) == str(fx.accuracy_line)
+        nv = fx.val_nbr_idx.shape[0]
+        assert_neighbors_match(vidx[:nv], vdist[:nv], fx.val_nbr_idx[:nv, :K],
+                               fx.val_nbr_dist[:nv, :K], vflags[:nv])
+
+
+def _mix(rng, n, m, d, classes, spread=2.0, grid=1024.0):
+    centres = rng.uniform(-spread, spread, (classes, d))
+    lab = rng.integers(0, classes, n + m).astype(np.int32)
+    X = centres[lab] + rng.standard_normal((n + m, d))
+    if grid:
+        X = np.round(X * grid) / grid
+    tr, te = X[:n].copy(), X[n:].copy()
+    oracle.normalize(tr, te, None)
+    return tr, lab[:n].copy(), te
+
+
+CASES = [
+    # n, m, d, k, metric, classes
+    (5000, 300, 128, 10, 0, 10),
+    (4099, 257, 96, 10, 0, 7),      # ragged n (not /32), ragged m (not /128)
+    (3000, 130, 13, 5, 0, 3),       # odd dim -> zero padding
+    (2000, 64, 1, 3, 0, 2),         # d = 1
+    (1000, 100, 64, 1, 0, 4),       # k = 1
+    (20, 50, 16, 20, 0, 3),         # k = n, n < one tile
+    (31, 40, 8, 30, 1, 3),          # L1, n just under a tile, k = n-1
+    (6000, 200, 40, 7, 1, 5),       # L1
+    (3000, 150, 256, 50, 0, 10),    # largest register-resident dim, K=50
+    (4000, 100, 64, 100, 0, 10),    # K=100 (cfg5's k)
+    (8000, 128, 24, 16, 0, 6),
+]
+
+
+@pytest.mark.parametrize("n,m,d,k,metric,classes", CASES)
+def test_vs_oracle(n, m, d, k, metric, classes, clf, knn):
+    rng = np.random.default_rng(n * 7 + m * 3 + d + k)
+    tr, lab, te = _mix(rng, n, m, d, classes)
+    run_case(clf, knn, tr, lab, te, k, metric, classes)
+
+
+def test_duplicates_force_rescan(clf, knn):
+    """Many exact duplicates of the nearest rows: the candidate set cannot be
+    certified from the fp32 pass, so the exact fp64 rescan must run."""
+    rng = np.random.default_rng(7)
+    tr, lab, te = _mix(rng, 3000, 64, 32, 4)
+    tr[1000:1400] = tr[5]           # 400 identical rows
+    lab[1000:1400] = rng.integers(0, 4, 400)
+    te[:32] = tr[5]                  # queries sitting exactly on them
+    got, want, flags = run_case(clf, knn, tr, lab, te, 9, 0, 4)
+    assert clf.last_rescan_count() > 0
+    assert (flags[:32] & knn.FLAG_EXACT_RESCAN).all()
+
+
+def test_integer_ties(clf, knn):
+    """SIFT-like integer data: many exact distance ties."""
+    rng = np.random.default_rng(11)
+    centres = rng.integers(0, 256, (5, 16))
+    lab = rng.integers(0, 5, 4200).astype(np.int32)
+    X = np.clip(centres[lab] + rng.integers(-6, 7, (4200, 16)), 0, 255).astype(np.float64)
+    tr, te = X[:4000].copy(), X[4000:].copy()
+    run_case(clf, knn, tr, lab[:4000].copy(), te, 10, 0, 5)
+    run_case(clf, knn, tr, lab[:4000].copy(), te, 10, 1, 5)
+
+
+def test_sorted_train_rows(clf, knn):
+    """Train rows sorted by class (all near neighbours in one contiguous run)."""
+    rng = np.random.default_rng(5)
+    tr, lab, te = _mix(rng, 12000, 256, 32, 3, spread=3.0)
+    order = np.argsort(lab, kind="stable")
+    run_case(clf, knn, np.ascontiguousarray(tr[order]), lab[order].copy(), te, 20, 0, 3)
+
+
+def test_k_zero_and_errors(clf, knn):
+    rng = np.random.default_rng(3)
+    tr, lab, te = _mix(rng, 500, 10, 8, 2)
+    clf.set_train(tr, lab, 2)
+    assert (clf.classify(te, 0) == -1).all()   # cpp:324: max_label = -1
+    with pytest.raises(knn.KnnError):
+        clf.classify(te, 501)                  # k > n_train (reference UB)
+    with pytest.raises(knn.KnnError):
+        clf.set_train(tr, np.full(500, 2, np.int32), 2)  # label out of range
+
+
+def test_device_api_and_partial_merge(clf, knn):
+    """knn_classify_device + search_partial/merge_vote (train-sharded building
+    blocks) on one GPU: shard the train set in two contexts, merge, compare."""
+    import torch
+    rng = np.random.default_rng(9)
+    tr, lab, te = _mix(rng, 6000, 300, 48, 5)
+    k = 10
+    want, widx, wdist = oracle.knn(tr, lab, te, k, True, 5, n_out=k)
+    dev = torch.device("cuda", 0)
+    parts, half = 2, 3000
+    w = k + 1
+    c2 = knn.Classifier(0)
+    Xs = [torch.from_numpy(tr[:half]).to(dev), torch.from_numpy(tr[half:]).to(dev)]
+    Ls = [torch.from_numpy(lab[:half]).to(dev), torch.from_numpy(lab[half:]).to(dev)]
+    Q = torch.from_numpy(te).to(dev)
+    m = te.shape[0]
+    gd = torch.empty((parts, m, w), dtype=torch.float64, device=dev)
+    gi = torch.empty((parts, m, w), dtype=torch.int64, device=dev)
+    gl = torch.empty((parts, m, w), dtype=torch.int32, device=dev)
+    for p, c in enumerate((clf, c2)):
+        c.set_train_device(Xs[p].data_ptr(), Ls[p].data_ptr(), half, 48, 5, idx_offset=p * half,
+                           keep=(Xs[p], Ls[p]))
+        c.search_partial_device(Q.data_ptr(), m, w, knn.L2, gd[p].data_ptr(), gi[p].data_ptr(),
+                                gl[p].data_ptr())
+        c.sync()
+    ol = torch.empty(m, dtype=torch.int32, device=dev)
+    oi = torch.empty((m, k), dtype=torch.int64, device=dev)
+    od = torch.empty((m, k), dtype=torch.float64, device=dev)
+    of = torch.empty(m, dtype=torch.int32, device=dev)
+    clf.merge_vote_device(gd.data_ptr(), gi.data_ptr(), gl.data_ptr(), parts, m, w, k,
+                          ol.data_ptr(), oi.data_ptr(), od.data_ptr(), of.data_ptr())
+    clf.sync()
+    np.testing.assert_array_equal(ol.cpu().numpy(), want)
+    assert_neighbors_match(oi.cpu().numpy(), od.cpu().numpy(), widx, wdist, of.cpu().numpy())
+    # device classify on the full set
+    Xf = torch.from_numpy(tr).to(dev)
+    Lf = torch.from_numpy(lab).to(dev)
+    clf.set_train_device(Xf.data_ptr(), Lf.data_ptr(), 6000, 48, 5, keep=(Xf, Lf))
+    clf.classify_device(Q.data_ptr(), m, k, knn.L2, ol.data_ptr(), oi.data_ptr(), od.data_ptr(),
+                        of.data_ptr())
+    clf.sync()
+    np.testing.assert_array_equal(ol.cpu().numpy(), want)
+    c2.close()
+
+
+def test_group_single_gpu_modes(knn):
+    rng = np.random.default_rng(21)
+    tr, lab, te = _mix(rng, 5000, 333, 32, 6)
+    want, widx, wdist = oracle.knn(tr, lab, te, 7, True, 6, n_out=7)
+    for mode in (0, 1):
+        g = knn.Group([0], mode)
+        g.set_train(tr, lab, 6)
+        got, idx, dist, flags = g.classify(te, 7, knn.L2, return_neighbors=True)
+        np.testing.assert_array_equal(got, want)
+        assert_neighbors_match(idx, dist, widx, wdist, flags)
+        g.close()
+
+
+def test_driver_matches_reference_outputs(tmp_path, knn):
+    """The native drop-in driver on the reference's CSV files reproduces
+    Test_label.csv and the accuracy line of the reference run."""
+    for name in ("f1_cfg1", "f3_l1", "f5_csv_crlf", "f7_nonorm_noval"):
+        fx = golden_io.Fixture(name)
+        s = fx.spec
+        d = tmp_path / name
+        d.mkdir()
+        cfg = knn.KnnConfig(dim=s["dim"], K=s["K"], N_train=s["N_train"], N_test=s["N_test"],
+                            N_val=s["N_val"], class_cnt=s["class_cnt"],
+                            Euclidean_distance=s["Euclidean_distance"], Normalize=s["Normalize"],
+                            Validation=s["Validation"])
+        fx.write_inputs(str(d), names=(cfg.train_file_name, cfg.validation_file_name,
+                                       cfg.test_file_name))
+        out = knn.run_reference_program(cfg, str(d))
+        labels = np.loadtxt(d / "Test_label.csv", dtype=np.int64, ndmin=1)
+        np.testing.assert_array_equal(labels, fx.test_labels)
+        if s["Validation"]:
+            assert str(fx.accuracy_line) in out
+        assert "Running time is " in out
