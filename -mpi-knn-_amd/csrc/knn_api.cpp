@@ -122,7 +122,7 @@ static int build_train(knn_ctx* ctx, const double* dX, const int32_t* dlab, int6
   const int DP = pad_dim(d);
   if (!cand_supported(DP))
     return knn_fail(KNN_ERR_ARG, "dimension " + std::to_string(d) + " not supported by this build");
-  const int64_t n_pad = (n + kTR - 1) / kTR * kTR;
+  const int64_t n_pad = (n + kRowAlign - 1) / kRowAlign * kRowAlign;
   int rc;
   if ((rc = ctx->X32.ensure((size_t)n_pad * DP * sizeof(float)))) return rc;
   if ((rc = ctx->xl2.ensure((size_t)n_pad * sizeof(float)))) return rc;
@@ -198,14 +198,40 @@ int knn_set_train_device(knn_ctx* ctx, const double* dX, const int32_t* dlabels,
 
 }  // extern "C"
 
-// Splits per query tile: enough workgroups to fill 256 CUs a few times over,
-// enough lists to hold C candidates, at least 2 tiles per split.
-static int choose_splits(int n_qt, int64_t n_tiles, int C, int R) {
-  int S = (2048 + n_qt - 1) / n_qt;
-  S = std::max(S, (C + 2 * R - 1) / (2 * R));
-  S = std::min(S, 32);
-  S = (int)std::min<int64_t>(S, std::max<int64_t>(1, n_tiles / 2));
-  return std::max(S, 1);
+// Work decomposition of the candidate kernel: S train splits per 128-query
+// tile, R list entries per lane.  The grid (n_qt * S workgroups) is sized so
+// its last wave of workgroups is nearly full on the resident slots of this
+// kernel (occupancy x CUs): a mostly-empty final round costs up to a whole
+// workgroup duration.  The union of the 2S lists must hold the C re-rank
+// candidates; R grows to 16 when the expected per-list share of C is large.
+static void choose_geometry(knn_ctx* ctx, int metric, int DP, int n_qt, int64_t n_tiles, int C,
+                            int& S_out, int& R_out) {
+  if (ctx->cu_count <= 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    ctx->cu_count = cus;
+  }
+  const int S_hi = (int)std::max<int64_t>(1, std::min<int64_t>(64, n_tiles));
+  int bestS = 1, bestR = 8;
+  for (int R : {8, 16}) {
+    const int64_t slots = (int64_t)cand_blocks_per_cu(metric, DP, R) * ctx->cu_count;
+    const int S_lo = std::min(S_hi, std::max(1, (C + 2 * R - 1) / (2 * R)));
+    double best = -1.0;
+    int bS = S_lo;
+    for (int S = S_lo; S <= S_hi; S++) {
+      const int64_t wg = (int64_t)n_qt * S;
+      const int64_t rounds = (wg + slots - 1) / slots;
+      const double eff = (double)wg / (double)(rounds * slots);
+      if (eff > best + 1e-3) { best = eff; bS = S; }
+    }
+    bestS = bS;
+    bestR = R;
+    if (C <= 4 * bS) break;  // expected per-list share of the C candidates <= 2: R = 8 is ample
+  }
+  S_out = bestS;
+  R_out = bestR;
 }
 
 static double err_factor(int metric, int DP) {
@@ -220,13 +246,13 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
                    hipStream_t s) {
   const TrainDev& t = ctx->train;
   const int DP = t.DP;
-  const int R = 16;
   const int n_qt = (int)((m + kQPB - 1) / kQPB);
   const int64_t m_pad = (int64_t)n_qt * kQPB;
-  const int64_t n_tiles = t.n_pad / kTR;
+  const int64_t n_tiles = t.n_pad / cand_tile_rows(DP);
   int C = (int)std::min<int64_t>(t.n, std::max(2 * W, W + 16));
   C = std::min(C, kMaxUnion);
-  const int S = choose_splits(n_qt, n_tiles, C, R);
+  int S = 1, R = 8;
+  choose_geometry(ctx, metric, DP, n_qt, n_tiles, C, S, R);
   const int NL = 2 * S;
   C = std::min(C, NL * R);
   int rc;
@@ -238,19 +264,30 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
 
   ctx->geom[0] = (int64_t)n_qt * S;
   ctx->geom[1] = S;
-  ctx->geom[2] = NL;
+  ctx->geom[2] = R;
   ctx->geom[3] = C;
   const bool tm = ctx->timing;
   if (tm) HIP_TRY(hipEventRecord(ctx->ev[0], s));
   launch_prep_queries(dQ, m, t.d, DP, m_pad, metric == 0 ? -2.0f : 1.0f, (float*)ctx->Q32.p, s);
   if (tm) HIP_TRY(hipEventRecord(ctx->ev[1], s));
-  launch_cand(metric, DP, t.X32, metric == 0 ? t.xinit_l2 : t.xinit_l1, (const float*)ctx->Q32.p,
-              (int)n_tiles, S, n_qt, (float*)ctx->cand_v.p, (int*)ctx->cand_i.p, s);
+  CandLaunch cl{};
+  cl.metric = metric;
+  cl.DP = DP;
+  cl.R = R;
+  cl.S = S;
+  cl.n_qt = n_qt;
+  cl.n_pad = t.n_pad;
+  cl.X32 = t.X32;
+  cl.xinit = metric == 0 ? t.xinit_l2 : t.xinit_l1;
+  cl.Q32 = (const float*)ctx->Q32.p;
+  cl.out_v = (float*)ctx->cand_v.p;
+  cl.out_i = (int*)ctx->cand_i.p;
+  launch_cand(cl, s);
   HIP_TRY(hipGetLastError());
   if (tm) HIP_TRY(hipEventRecord(ctx->ev[2], s));
   HIP_TRY(hipMemsetAsync(ctx->rescan_cnt.p, 0, sizeof(int), s));
-  launch_merge_rerank(metric, (const float*)ctx->cand_v.p, (const int*)ctx->cand_i.p, NL, t, dQ, m,
-                      W, C, err_factor(metric, DP), sink, (int*)ctx->rescan_q.p,
+  launch_merge_rerank(metric, (const float*)ctx->cand_v.p, (const int*)ctx->cand_i.p, NL, R, t, dQ,
+                      m, W, C, err_factor(metric, DP), sink, (int*)ctx->rescan_q.p,
                       (int*)ctx->rescan_cnt.p, s);
   HIP_TRY(hipGetLastError());
   if (tm) HIP_TRY(hipEventRecord(ctx->ev[3], s));

@@ -22,6 +22,7 @@ struct knn_ctx {
   int class_cnt = 0;
   int64_t idx_off = 0;
   int64_t last_rescan = 0;
+  int cu_count = 0;
   knnk::TrainDev train{};
   bool timing = false;
   hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};

@@ -11,6 +11,8 @@ constexpr int kTR = 32;          // train rows per LDS tile
 constexpr int kMaxUnion = 1024;  // max candidates kept per query across all lists
 constexpr int kSortN = 2048;     // rows per exact-rescan chunk / reduce block
 constexpr int kMaxK = 1000;      // largest k served (k+1 <= kMaxUnion)
+constexpr int kStreamDC = 32;    // dims per LDS chunk in the large-d kernel
+constexpr int kRowAlign = 128;   // train rows are padded to a multiple of this
 
 enum { MODE_SINGLE = 0, MODE_PARTIAL = 1 };
 
@@ -40,18 +42,30 @@ struct TrainDev {
   double x2max, x1max;   // max ||x||_2^2, max ||x||_1 over the train rows
 };
 
-int pad_dim(int d);                 // DP for a given d (multiple of 8)
+int pad_dim(int d);                 // padded dim the candidate kernels run at
 bool cand_supported(int DP);
+int cand_tile_rows(int DP);         // train rows per tile of the kernel serving DP
+int cand_blocks_per_cu(int metric, int DP, int R);  // resident workgroups per CU
+
+struct CandLaunch {
+  int metric, DP, R, S, n_qt;
+  int64_t n_pad;
+  const float* X32;
+  const float* xinit;
+  const float* Q32;
+  float* out_v;
+  int* out_i;
+};
 
 void launch_prep_train(const double* X64, int64_t n, int d, int DP, int64_t n_pad, float* X32,
                        float* xl2, float* xl1, unsigned long long* stats, hipStream_t s);
 void launch_prep_queries(const double* Q64, int64_t m, int d, int DP, int64_t m_pad,
                          float scale, float* Q32, hipStream_t s);
-void launch_cand(int metric, int DP, const float* X32, const float* xinit, const float* Q32,
-                 int n_tiles, int S, int n_qt, float* out_v, int* out_i, hipStream_t s);
-void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, const TrainDev& t,
-                         const double* Q64, int64_t m, int W, int C, double f_err,
-                         const Sink& sink, int* rescan_q, int* rescan_cnt, hipStream_t s);
+void launch_cand(const CandLaunch& c, hipStream_t s);
+void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int R,
+                         const TrainDev& t, const double* Q64, int64_t m, int W, int C,
+                         double f_err, const Sink& sink, int* rescan_q, int* rescan_cnt,
+                         hipStream_t s);
 void launch_rescan(int metric, const TrainDev& t, const double* Q64, const int* rescan_q,
                    int f0, int nf, int W, double* pa_k, int* pa_i, double* pb_k, int* pb_i,
                    const Sink& sink, hipStream_t s);

@@ -31,7 +31,6 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #define KNN_INF_F __builtin_inff()
 #define KNN_INF_D __builtin_inf()
 
-int pad_dim(int d) { return (d + 7) & ~7; }
 
 // ---------------------------------------------------------------- helpers
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
@@ -56,6 +55,11 @@ __device__ __forceinline__ int wave_max_i(int v) {
 __device__ __forceinline__ int wave_min_i(int v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_or_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);
   return v;
 }
 __device__ __forceinline__ int wave_sum_i(int v) {
@@ -227,6 +231,40 @@ __device__ __forceinline__ void list_insert(float (&L)[R], int (&I)[R], float v,
   L[0] = c0 ? v : L[0];
 }
 
+// Fused top-R selection over one 32x32 accumulator block: lane (j, h) holds
+// the values of query j against rows row0 + rho(i, h), i = 0..15.  Once the
+// list is warm this is one min-reduction and one compare per block.
+template <int R>
+__device__ __forceinline__ void select_block(const f32x16& acc, int row0, int h, float (&L)[R],
+                                             int (&I)[R], float& thr) {
+  float mn = acc[0];
+#pragma unroll
+  for (int i = 1; i < 16; ++i) mn = acc[i] < mn ? acc[i] : mn;
+  if (mn < thr) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float v = acc[i];
+      if (v < thr) {
+        list_insert<R>(L, I, v, row0 + (i & 3) + 8 * (i >> 2) + 4 * h);
+        thr = L[R - 1];
+      }
+    }
+  }
+}
+
+// Lists are stored [query][split][half][R] so a query's 2S lists are contiguous.
+template <int R>
+__device__ __forceinline__ void write_lists(float* __restrict__ out_v, int* __restrict__ out_i,
+                                            int64_t qg, int S, int split, int h,
+                                            const float (&L)[R], const int (&I)[R]) {
+  const int64_t o = ((qg * (2 * S)) + split * 2 + h) * R;
+#pragma unroll
+  for (int t = 0; t < R; t += 4) {
+    *(float4*)(out_v + o + t) = make_float4(L[t], L[t + 1], L[t + 2], L[t + 3]);
+    *(int4*)(out_i + o + t) = make_int4(I[t], I[t + 1], I[t + 2], I[t + 3]);
+  }
+}
+
 // Workgroup = 4 waves = 128 queries; it streams the 32-row train tiles
 // split, split+S, split+2S, ... (round-robin so a run of similar rows is
 // spread over all splits).  Lane (j = lane&31, h = lane>>5) of wave w owns
@@ -359,69 +397,254 @@ cand_kernel(const float* __restrict__ X32, const float* __restrict__ xinit,
       }
     }
 
-    // fused top-R selection: one compare per value once the list is warm
-    float mn = acc[0];
-#pragma unroll
-    for (int i = 1; i < 16; ++i) mn = acc[i] < mn ? acc[i] : mn;
-    if (mn < thr) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float v = acc[i];
-        if (v < thr) {
-          list_insert<R>(L, I, v, t * kTR + (i & 3) + 8 * (i >> 2) + 4 * h);
-          thr = L[R - 1];
-        }
-      }
-    }
+    select_block<R>(acc, t * kTR, h, L, I, thr);
 
     if (more) KNN_STORE_TILE((it + 1) & 1);
     __syncthreads();
   }
 
-  const int NL = 2 * S;
-  const int64_t o = ((qg * NL) + split * 2 + h) * R;
-#pragma unroll
-  for (int t = 0; t < R; t += 4) {
-    *(float4*)(out_v + o + t) = make_float4(L[t], L[t + 1], L[t + 2], L[t + 3]);
-    *(int4*)(out_i + o + t) = make_int4(I[t], I[t + 1], I[t + 2], I[t + 3]);
-  }
+  write_lists<R>(out_v, out_i, qg, S, split, h, L, I);
 #undef KNN_LOAD_TILE
 #undef KNN_STORE_TILE
 #undef KNN_LD1
 #undef KNN_ST1
 }
 
-#define KNN_DP_LIST(X) X(8) X(16) X(24) X(32) X(40) X(48) X(64) X(96) X(128) X(160) X(192) X(256)
+// Large-dimension variant (DP > 256, e.g. the reference's MNIST default
+// d=784): the query tile no longer fits in VGPRs, so both operands are staged
+// through LDS in chunks of DC dims.  Workgroup tile = 128 queries x 128 train
+// rows (4 waves x (32 queries x 4 row blocks)); per chunk each wave issues
+// 4 x DC/2 MFMAs reading its B fragment once per 8 dims and reusing it over
+// the 4 row blocks.  LDS: 2 buffers x (A 128xDC + B 128xDC), rows padded by
+// 16 B (DC/4 + 1 odd -> conflict-free ds_read_b128).  Same selection epilogue
+// after the last chunk of a tile.
+template <int DC, int R, int METRIC>
+__global__ void __launch_bounds__(256)
+cand_stream_kernel(const float* __restrict__ X32, const float* __restrict__ xinit,
+                   const float* __restrict__ Q32, int DP, int n_tiles, int S, int n_qt,
+                   float* __restrict__ out_v, int* __restrict__ out_i) {
+  constexpr int TRS = 128;          // train rows per tile
+  constexpr int LS = DC + 4;        // LDS row stride (floats)
+  constexpr int OP = TRS * LS;      // floats per operand image
+  constexpr int CPR = DC / 4;       // float4 per row chunk
+  constexpr int NCH = TRS * CPR;    // float4 per operand chunk
+  constexpr int CPT = NCH / 256;    // per thread
+  static_assert(CPT == 4, "staging below is written for 4 float4 per operand");
+  __shared__ __attribute__((aligned(16))) float lds[2 * 2 * OP + 2 * TRS];
+  float* ldsn = lds + 4 * OP;
 
-bool cand_supported(int DP) {
-#define KNN_CASE(v) if (DP == v) return true;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / n_qt;
+  const int qt = bid - split * n_qt;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int j = lane & 31, h = lane >> 5;
+  const int64_t qg = (int64_t)qt * kQPB + wv * 32 + j;
+  const int nch = DP / DC;
+
+  float L[R];
+  int I[R];
+#pragma unroll
+  for (int t = 0; t < R; ++t) { L[t] = KNN_INF_F; I[t] = -1; }
+  float thr = KNN_INF_F;
+
+  const int my_nt = split < n_tiles ? (n_tiles - split + S - 1) / S : 0;
+  const int total = my_nt * nch;
+
+  float4 a0, a1, a2, a3, b0, b1, b2, b3;
+  float4 stn = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float* qbase = Q32 + (int64_t)qt * kQPB * DP;
+#define KNN_SLOAD(st_)                                                                  \
+  do {                                                                                  \
+    const int it_ = (st_) / nch, c_ = (st_) - it_ * nch;                                \
+    const int t_ = split + it_ * S;                                                     \
+    const float* xs_ = X32 + (int64_t)t_ * TRS * DP + c_ * DC;                          \
+    const float* qs_ = qbase + c_ * DC;                                                 \
+    int e_ = tid;                                                                       \
+    a0 = *(const float4*)(xs_ + (e_ / CPR) * DP + (e_ % CPR) * 4);                      \
+    b0 = *(const float4*)(qs_ + (e_ / CPR) * DP + (e_ % CPR) * 4);                      \
+    e_ += 256;                                                                          \
+    a1 = *(const float4*)(xs_ + (e_ / CPR) * DP + (e_ % CPR) * 4);                      \
+    b1 = *(const float4*)(qs_ + (e_ / CPR) * DP + (e_ % CPR) * 4);                      \
+    e_ += 256;                                                                          \
+    a2 = *(const float4*)(xs_ + (e_ / CPR) * DP + (e_ % CPR) * 4);                      \
+    b2 = *(const float4*)(qs_ + (e_ / CPR) * DP + (e_ % CPR) * 4);                      \
+    e_ += 256;                                                                          \
+    a3 = *(const float4*)(xs_ + (e_ / CPR) * DP + (e_ % CPR) * 4);                      \
+    b3 = *(const float4*)(qs_ + (e_ / CPR) * DP + (e_ % CPR) * 4);                      \
+    if (c_ == 0 && tid < TRS / 4) stn = ((const float4*)(xinit + (int64_t)t_ * TRS))[tid]; \
+  } while (0)
+#define KNN_SSTORE(st_, buf_)                                                           \
+  do {                                                                                  \
+    float* A_ = lds + (buf_) * 2 * OP;                                                  \
+    float* B_ = A_ + OP;                                                                \
+    int e_ = tid;                                                                       \
+    *(float4*)(A_ + (e_ / CPR) * LS + (e_ % CPR) * 4) = a0;                             \
+    *(float4*)(B_ + (e_ / CPR) * LS + (e_ % CPR) * 4) = b0;                             \
+    e_ += 256;                                                                          \
+    *(float4*)(A_ + (e_ / CPR) * LS + (e_ % CPR) * 4) = a1;                             \
+    *(float4*)(B_ + (e_ / CPR) * LS + (e_ % CPR) * 4) = b1;                             \
+    e_ += 256;                                                                          \
+    *(float4*)(A_ + (e_ / CPR) * LS + (e_ % CPR) * 4) = a2;                             \
+    *(float4*)(B_ + (e_ / CPR) * LS + (e_ % CPR) * 4) = b2;                             \
+    e_ += 256;                                                                          \
+    *(float4*)(A_ + (e_ / CPR) * LS + (e_ % CPR) * 4) = a3;                             \
+    *(float4*)(B_ + (e_ / CPR) * LS + (e_ % CPR) * 4) = b3;                             \
+    const int c_ = (st_) % nch;                                                         \
+    if (c_ == 0 && tid < TRS / 4) *(float4*)(ldsn + (buf_) * TRS + 4 * tid) = stn;      \
+  } while (0)
+
+  if (total > 0) {
+    KNN_SLOAD(0);
+    KNN_SSTORE(0, 0);
+  }
+  __syncthreads();
+
+  f32x16 acc0, acc1, acc2, acc3;
+  for (int st = 0; st < total; ++st) {
+    const int it = st / nch, c = st - it * nch;
+    const int t = split + it * S;
+    const bool more = st + 1 < total;
+    if (more) KNN_SLOAD(st + 1);
+    const float* A = lds + (st & 1) * 2 * OP;
+    const float* B = A + OP;
+    if (c == 0) {
+      // the norms were staged with chunk 0 of this tile into buffer (st & 1)
+      const float* nb = ldsn + (st & 1) * TRS;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 n0 = *(const float4*)(nb + 0 * 32 + 8 * g + 4 * h);
+        const float4 n1 = *(const float4*)(nb + 1 * 32 + 8 * g + 4 * h);
+        const float4 n2 = *(const float4*)(nb + 2 * 32 + 8 * g + 4 * h);
+        const float4 n3 = *(const float4*)(nb + 3 * 32 + 8 * g + 4 * h);
+        acc0[4 * g] = n0.x; acc0[4 * g + 1] = n0.y; acc0[4 * g + 2] = n0.z; acc0[4 * g + 3] = n0.w;
+        acc1[4 * g] = n1.x; acc1[4 * g + 1] = n1.y; acc1[4 * g + 2] = n1.z; acc1[4 * g + 3] = n1.w;
+        acc2[4 * g] = n2.x; acc2[4 * g + 1] = n2.y; acc2[4 * g + 2] = n2.z; acc2[4 * g + 3] = n2.w;
+        acc3[4 * g] = n3.x; acc3[4 * g + 1] = n3.y; acc3[4 * g + 2] = n3.z; acc3[4 * g + 3] = n3.w;
+      }
+    }
+    if constexpr (METRIC == 0) {
+      const float* brow = B + (wv * 32 + j) * LS + 4 * h;
+      const float* arow = A + j * LS + 4 * h;
+#pragma unroll
+      for (int g = 0; g < DC / 8; ++g) {
+        const float4 b = *(const float4*)(brow + 8 * g);
+        const float4 x0 = *(const float4*)(arow + 0 * 32 * LS + 8 * g);
+        const float4 x1 = *(const float4*)(arow + 1 * 32 * LS + 8 * g);
+        const float4 x2 = *(const float4*)(arow + 2 * 32 * LS + 8 * g);
+        const float4 x3 = *(const float4*)(arow + 3 * 32 * LS + 8 * g);
+#define KNN_MF4(acc_, x_)                                                               \
+  acc_ = __builtin_amdgcn_mfma_f32_32x32x2f32(x_.x, b.x, acc_, 0, 0, 0);                \
+  acc_ = __builtin_amdgcn_mfma_f32_32x32x2f32(x_.y, b.y, acc_, 0, 0, 0);                \
+  acc_ = __builtin_amdgcn_mfma_f32_32x32x2f32(x_.z, b.z, acc_, 0, 0, 0);                \
+  acc_ = __builtin_amdgcn_mfma_f32_32x32x2f32(x_.w, b.w, acc_, 0, 0, 0);
+        KNN_MF4(acc0, x0) KNN_MF4(acc1, x1) KNN_MF4(acc2, x2) KNN_MF4(acc3, x3)
+#undef KNN_MF4
+      }
+    } else {
+      const float* brow = B + (wv * 32 + j) * LS;
+#pragma unroll 2
+      for (int g = 0; g < DC / 4; ++g) {
+        const float4 qv = *(const float4*)(brow + 4 * g);
+#define KNN_L1B(acc_, blk_)                                                             \
+  _Pragma("unroll") for (int i = 0; i < 16; ++i) {                                      \
+    const int r = (blk_) * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;                         \
+    const float4 xv = *(const float4*)(A + r * LS + 4 * g);                             \
+    float a = acc_[i];                                                                  \
+    a = a + __builtin_fabsf(qv.x - xv.x);                                               \
+    a = a + __builtin_fabsf(qv.y - xv.y);                                               \
+    a = a + __builtin_fabsf(qv.z - xv.z);                                               \
+    a = a + __builtin_fabsf(qv.w - xv.w);                                               \
+    acc_[i] = a;                                                                        \
+  }
+        KNN_L1B(acc0, 0) KNN_L1B(acc1, 1) KNN_L1B(acc2, 2) KNN_L1B(acc3, 3)
+#undef KNN_L1B
+      }
+    }
+    if (c == nch - 1) {
+      select_block<R>(acc0, t * TRS + 0, h, L, I, thr);
+      select_block<R>(acc1, t * TRS + 32, h, L, I, thr);
+      select_block<R>(acc2, t * TRS + 64, h, L, I, thr);
+      select_block<R>(acc3, t * TRS + 96, h, L, I, thr);
+    }
+    if (more) KNN_SSTORE(st + 1, (st + 1) & 1);
+    __syncthreads();
+  }
+  write_lists<R>(out_v, out_i, qg, S, split, h, L, I);
+#undef KNN_SLOAD
+#undef KNN_SSTORE
+}
+
+#define KNN_DP_LIST(X) X(8) X(16) X(24) X(32) X(48) X(64) X(96) X(128) X(160) X(192) X(256)
+
+int pad_dim(int d) {
+#define KNN_CASE(v) if (d <= v) return v;
   KNN_DP_LIST(KNN_CASE)
 #undef KNN_CASE
-  return false;
+  return (d + kStreamDC - 1) / kStreamDC * kStreamDC;  // streamed kernel
+}
+
+bool cand_supported(int DP) { return DP > 0 && pad_dim(DP) == DP; }
+
+template <class KernelT>
+static int occupancy_of(KernelT k) {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 256, 0) != hipSuccess) return 1;
+  return nb > 0 ? nb : 1;
+}
+
+template <int DP, int R, int METRIC>
+static void launch_res(const CandLaunch& c, hipStream_t s) {
+  hipLaunchKernelGGL((cand_kernel<DP, R, METRIC>), dim3((unsigned)(c.n_qt * c.S)), dim3(256), 0, s,
+                     c.X32, c.xinit, c.Q32, (int)(c.n_pad / kTR), c.S, c.n_qt, c.out_v, c.out_i);
+}
+template <int R, int METRIC>
+static void launch_str(const CandLaunch& c, hipStream_t s) {
+  hipLaunchKernelGGL((cand_stream_kernel<kStreamDC, R, METRIC>), dim3((unsigned)(c.n_qt * c.S)),
+                     dim3(256), 0, s, c.X32, c.xinit, c.Q32, c.DP, (int)(c.n_pad / 128), c.S,
+                     c.n_qt, c.out_v, c.out_i);
 }
 
 template <int DP>
-static void launch_cand_dp(int metric, const float* X32, const float* xinit, const float* Q32,
-                           int n_tiles, int S, int n_qt, float* out_v, int* out_i,
-                           hipStream_t s) {
-  dim3 grid((unsigned)(n_qt * S)), block(256);
-  if (metric == 0)
-    hipLaunchKernelGGL((cand_kernel<DP, 16, 0>), grid, block, 0, s, X32, xinit, Q32, n_tiles, S,
-                       n_qt, out_v, out_i);
-  else
-    hipLaunchKernelGGL((cand_kernel<DP, 16, 1>), grid, block, 0, s, X32, xinit, Q32, n_tiles, S,
-                       n_qt, out_v, out_i);
+static int blocks_per_cu_res(int R, int metric) {
+  if (metric == 0) return R == 8 ? occupancy_of(cand_kernel<DP, 8, 0>) : occupancy_of(cand_kernel<DP, 16, 0>);
+  return R == 8 ? occupancy_of(cand_kernel<DP, 8, 1>) : occupancy_of(cand_kernel<DP, 16, 1>);
 }
 
-void launch_cand(int metric, int DP, const float* X32, const float* xinit, const float* Q32,
-                 int n_tiles, int S, int n_qt, float* out_v, int* out_i, hipStream_t s) {
-#define KNN_CASE(v)                                                                       \
-  if (DP == v) {                                                                          \
-    launch_cand_dp<v>(metric, X32, xinit, Q32, n_tiles, S, n_qt, out_v, out_i, s);       \
-    return;                                                                               \
+int cand_blocks_per_cu(int metric, int DP, int R) {
+#define KNN_CASE(v) if (DP == v) return blocks_per_cu_res<v>(R, metric);
+  KNN_DP_LIST(KNN_CASE)
+#undef KNN_CASE
+  if (metric == 0)
+    return R == 8 ? occupancy_of(cand_stream_kernel<kStreamDC, 8, 0>)
+                  : occupancy_of(cand_stream_kernel<kStreamDC, 16, 0>);
+  return R == 8 ? occupancy_of(cand_stream_kernel<kStreamDC, 8, 1>)
+                : occupancy_of(cand_stream_kernel<kStreamDC, 16, 1>);
+}
+
+int cand_tile_rows(int DP) { return DP <= 256 ? kTR : 128; }
+
+template <int DP>
+static void launch_res_dp(const CandLaunch& c, hipStream_t s) {
+  if (c.metric == 0) {
+    if (c.R == 8) launch_res<DP, 8, 0>(c, s); else launch_res<DP, 16, 0>(c, s);
+  } else {
+    if (c.R == 8) launch_res<DP, 8, 1>(c, s); else launch_res<DP, 16, 1>(c, s);
+  }
+}
+
+void launch_cand(const CandLaunch& c, hipStream_t s) {
+#define KNN_CASE(v)                \
+  if (c.DP == v) {                 \
+    launch_res_dp<v>(c, s);        \
+    return;                        \
   }
   KNN_DP_LIST(KNN_CASE)
 #undef KNN_CASE
+  if (c.metric == 0) {
+    if (c.R == 8) launch_str<8, 0>(c, s); else launch_str<16, 0>(c, s);
+  } else {
+    if (c.R == 8) launch_str<8, 1>(c, s); else launch_str<16, 1>(c, s);
+  }
 }
 
 // ------------------------------------------------ finish: vote / outputs
@@ -444,16 +667,15 @@ __device__ void finish_single(int64_t q, const double* dk, const int* di, const 
   }
   const int M = wave_max_i(bc);
   const int tmin = wave_min_i(bc == M ? bt : INT_MAX);
-  int tie_vote = 0;
+  int tie = 0;
   for (int t = lane; t + 1 < k; t += 64)
-    tie_vote |= (dk[t] == dk[t + 1] && ls[t] != ls[t + 1]);
-  tie_vote = wave_max_i(tie_vote);
+    if (dk[t] == dk[t + 1]) tie |= ls[t] != ls[t + 1] ? 4 : 8;  // TIE_VOTE / TIE_ORDER
+  tie = wave_or_i(tie);
   if (lane == 0) {
     sink.labels[q] = k > 0 ? ls[tmin] : -1;
     if (sink.flags) {
-      int f = flag0;
+      int f = flag0 | tie;
       if (k > 0 && k < cnt && dk[k - 1] == dk[k]) f |= 2;  // KNN_FLAG_TIE_BOUNDARY
-      if (tie_vote) f |= 4;                                // KNN_FLAG_TIE_VOTE
       sink.flags[q] = f;
     }
   }
@@ -575,10 +797,10 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
     finish_partial(q, dk, di, ls, Cn, sink.w, sink.idx_off, sink);
 }
 
-void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, const TrainDev& t,
-                         const double* Q64, int64_t m, int W, int C, double f_err,
-                         const Sink& sink, int* rescan_q, int* rescan_cnt, hipStream_t s) {
-  const int R = 16;
+void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int R,
+                         const TrainDev& t, const double* Q64, int64_t m, int W, int C,
+                         double f_err, const Sink& sink, int* rescan_q, int* rescan_cnt,
+                         hipStream_t s) {
   const int U = NL * R;
   int U2 = 1;
   while (U2 < U) U2 <<= 1;
@@ -758,15 +980,15 @@ merge_vote_partials_kernel(const double* __restrict__ dist, const int64_t* __res
   }
   const int M = wave_max_i(bc);
   const int tmin = wave_min_i(bc == M ? bt : INT_MAX);
-  int tie_vote = 0;
-  for (int t = lane; t + 1 < k; t += 64) tie_vote |= (dk[t] == dk[t + 1] && ls[t] != ls[t + 1]);
-  tie_vote = wave_max_i(tie_vote);
+  int tie = 0;
+  for (int t = lane; t + 1 < k; t += 64)
+    if (dk[t] == dk[t + 1]) tie |= ls[t] != ls[t + 1] ? 4 : 8;
+  tie = wave_or_i(tie);
   if (lane == 0) {
     sink.labels[qo] = k > 0 ? ls[tmin] : -1;
     if (sink.flags) {
-      int f = 0;
+      int f = tie;
       if (k > 0 && k < cnt && dk[k - 1] == dk[k]) f |= 2;
-      if (tie_vote) f |= 4;
       sink.flags[qo] = f;
     }
   }

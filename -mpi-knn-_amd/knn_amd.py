@@ -13,6 +13,7 @@ import ctypes
 import dataclasses
 import os
 import subprocess
+import sys
 
 import numpy as np
 
@@ -21,7 +22,7 @@ LIB_PATH = os.path.join(HERE, "lib", "libknn_amd.so")
 DRIVER_PATH = os.path.join(HERE, "bin", "knn_mpi_amd")
 
 L2, L1 = 0, 1
-FLAG_EXACT_RESCAN, FLAG_TIE_BOUNDARY, FLAG_TIE_VOTE = 1, 2, 4
+FLAG_EXACT_RESCAN, FLAG_TIE_BOUNDARY, FLAG_TIE_VOTE, FLAG_TIE_ORDER = 1, 2, 4, 8
 EXPORTED = (
     "knn_version", "knn_last_error", "knn_device_count", "knn_create", "knn_destroy",
     "knn_set_train", "knn_set_train_device", "knn_classify", "knn_classify_device",
@@ -67,6 +68,15 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise KnnError("HIP library not built: %s (run build())" % LIB_PATH)
+    # PyTorch-ROCm bundles its own HIP/HSA runtime with the same sonames as
+    # /opt/rocm's.  If torch is in the process, let it bring up its runtime
+    # first so this library binds to the already-loaded one (two runtimes in
+    # one process leave torch without devices).
+    if "torch" in sys.modules:
+        try:
+            sys.modules["torch"].cuda.init()
+        except Exception:
+            pass
     L = ctypes.CDLL(LIB_PATH)
     P, i32, i64, f64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
     sig = {

@@ -64,6 +64,8 @@ extern "C" {
 #define KNN_FLAG_EXACT_RESCAN 1 /* candidate set not certified; exact fp64 rescan used */
 #define KNN_FLAG_TIE_BOUNDARY 2 /* dist[k-1] == dist[k]: membership tie at the k-th */
 #define KNN_FLAG_TIE_VOTE 4     /* equal distances with different labels inside top-k */
+#define KNN_FLAG_TIE_ORDER 8    /* equal distances inside top-k (order unspecified in
+                                   the reference's std::sort; ours: by train index) */
 
 typedef struct knn_ctx knn_ctx;
 typedef struct knn_group knn_group;
@@ -132,7 +134,7 @@ int knn_merge_vote_device(knn_ctx* ctx, const double* d_dist, const int64_t* d_i
 int knn_set_timing(knn_ctx* ctx, int enable);
 double knn_last_phase_ms(knn_ctx* ctx, int phase);
 /* Geometry of the last candidate launch: out[0]=workgroups, out[1]=splits
- * per query tile, out[2]=lists per query, out[3]=re-rank count C. */
+ * per query tile, out[2]=list entries per lane (R), out[3]=re-rank count C. */
 int knn_last_geometry(knn_ctx* ctx, int64_t out[4]);
 
 /* Synchronise the context's stream. */

@@ -3,6 +3,11 @@ import sys
 
 import pytest
 
+try:  # import torch before the HIP library is loaded (see knn_amd.lib())
+    import torch  # noqa: F401
+except Exception:
+    pass
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 for p in (HERE, ROOT, os.path.join(ROOT, "oracle")):

@@ -59,7 +59,7 @@ def assert_neighbors_match(idx, dist, widx, wdist, flags=None, labels_msg=""):
             if run[-1] < len(d) - 1:
                 assert set(idx[q][run]) == set(widx[q][run]), "query %d tie group differs" % q
         if flags is not None:
-            assert flags[q] & 6, "query %d differs but is not flagged as a tie" % q
+            assert flags[q] & 14, "query %d differs but is not flagged as a tie" % q
 
 
 def run_case(clf, knn, train, lab, queries, k, metric, classes):
