@@ -48,15 +48,18 @@ def assert_neighbors_match(idx, dist, widx, wdist, flags=None, labels_msg=""):
     bad = np.nonzero((dbits != wbits).any(1))[0]
     assert bad.size == 0, "distance mismatch at queries %s" % bad[:10]
     diff = np.nonzero((idx != widx).any(1))[0]
+    k = idx.shape[1]
     for q in diff:
         # differing indices are only allowed inside runs of equal distances
         d = dist[q]
+        boundary = flags is None or bool(flags[q] & 2)  # dist[k-1] == dist[k]
         for t in np.nonzero(idx[q] != widx[q])[0]:
             run = np.nonzero(d == d[t])[0]
-            assert len(run) > 1, "query %d pos %d: index differs without a tie" % (q, t)
-            # same set of indices over the full tie run is required unless the run
-            # crosses the k boundary (then membership itself is tie-ambiguous)
-            if run[-1] < len(d) - 1:
+            at_edge = run[-1] == k - 1 and boundary
+            assert len(run) > 1 or at_edge, "query %d pos %d: index differs without a tie" % (q, t)
+            # the same set of indices over the tie run is required unless the run
+            # reaches the k-th position and ties past it (membership ambiguous)
+            if not at_edge:
                 assert set(idx[q][run]) == set(widx[q][run]), "query %d tie group differs" % q
         if flags is not None:
             assert flags[q] & 14, "query %d differs but is not flagged as a tie" % q

@@ -1,14 +1,40 @@
 #!/bin/bash
-cd "$GRAFT_REPO_ROOT"
+# GPU-box check script (run through gpurun).  Stages: smoke tests bench prof
+# pmc; each GPU step has its own time limit; a crash/timeout (rc not 0/1)
+# stops the script so nothing else touches the GPU after a fault.
+cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-(ls -la /opt/conda/bin/mpirun; nproc; rocm-smi --showproductname | head -20) > gpurun_out/probe.log 2>&1
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
-rc=$?
-echo "smoke rc=$rc"
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
-rc=$?
-echo "tests rc=$rc"
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 600 python bench.py --steps 5 --warmup 2 > gpurun_out/bench1.log 2>&1
-echo "bench rc=$?"
+TAG=${TAG:-r1}
+stages="${*:-smoke tests bench}"
+step() {  # step <name> <limit-seconds> <cmd...>
+  local name=$1 lim=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$lim" "$@" > "gpurun_out/${TAG}_${name}.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -3 "gpurun_out/${TAG}_${name}.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+  return 0
+}
+for s in $stages; do
+  case $s in
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) step tests 900 python -m pytest tests -m gpu -q -p no:cacheprovider -x ;;
+    testsall) step testsall 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    bench) step bench 600 python bench.py --steps 10 --warmup 2 ;;
+    prof)
+      export TMPDIR=/tmp
+      step prof 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG" \
+        -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 1 \
+        --no-cpu-baseline ;;
+    pmc)
+      export TMPDIR=/tmp
+      step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_fetch_$TAG" \
+        -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 2 --warmup 1 \
+        --no-cpu-baseline
+      step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_write_$TAG" \
+        -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 2 --warmup 1 \
+        --no-cpu-baseline ;;
+    *) step custom 600 bash -c "$s" ;;
+  esac
+done
