@@ -217,36 +217,43 @@ void launch_fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t s) {
 // indexing (which would go to scratch).
 template <int R>
 __device__ __forceinline__ void list_insert(float (&L)[R], int (&I)[R], float v, int id) {
+  // L'[t] = max(L[t-1], min(v, L[t])) shifts the tail and drops L[R-1];
+  // the index follows with two selects.  Branch-free: v_min/v_max/v_cndmask
+  // (the TU is built with -fno-honor-nans so fminf/fmaxf need no quieting).
+  bool cc = true;  // v < L[R-1] by precondition
 #pragma unroll
   for (int t = R - 1; t > 0; --t) {
     const bool cp = v < L[t - 1];
-    const bool cc = v < L[t];
-    const float nl = cp ? L[t - 1] : (cc ? v : L[t]);
-    const int ni = cp ? I[t - 1] : (cc ? id : I[t]);
-    L[t] = nl;
-    I[t] = ni;
+    L[t] = __builtin_fmaxf(L[t - 1], __builtin_fminf(v, L[t]));
+    I[t] = cp ? I[t - 1] : (cc ? id : I[t]);
+    cc = cp;
   }
-  const bool c0 = v < L[0];
-  I[0] = c0 ? id : I[0];
-  L[0] = c0 ? v : L[0];
+  I[0] = cc ? id : I[0];
+  L[0] = __builtin_fminf(v, L[0]);
 }
 
 // Fused top-R selection over one 32x32 accumulator block: lane (j, h) holds
 // the values of query j against rows row0 + rho(i, h), i = 0..15.  Once the
-// list is warm this is one min-reduction and one compare per block.
+// list is warm this is a 16-way min (v_min3) and one compare per block; a
+// value is inserted only under a branch that no lane of the wave skips.
 template <int R>
 __device__ __forceinline__ void select_block(const f32x16& acc, int row0, int h, float (&L)[R],
                                              int (&I)[R], float& thr) {
-  float mn = acc[0];
+  // Lanes l and l^32 hold the same query: filtering with the smaller of the
+  // two list thresholds is safe -- anything dropped is >= some list's final
+  // R-th entry, which the merge's lower bound (min over lists) accounts for.
+  float te = __builtin_fminf(thr, __shfl_xor(thr, 32, 64));
+  float mn = __builtin_fminf(acc[0], acc[1]);
 #pragma unroll
-  for (int i = 1; i < 16; ++i) mn = acc[i] < mn ? acc[i] : mn;
-  if (mn < thr) {
+  for (int i = 2; i < 16; ++i) mn = __builtin_fminf(mn, acc[i]);
+  if (mn < te) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const float v = acc[i];
-      if (v < thr) {
+      if (v < te) {
         list_insert<R>(L, I, v, row0 + (i & 3) + 8 * (i >> 2) + 4 * h);
         thr = L[R - 1];
+        te = __builtin_fminf(te, thr);
       }
     }
   }

@@ -35,6 +35,12 @@ for s in $stages; do
       step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_write_$TAG" \
         -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 2 --warmup 1 \
         --no-cpu-baseline ;;
+    pmcsq)
+      export TMPDIR=/tmp
+      step pmc_sq 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU \
+        SQ_INSTS_MFMA SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_LDS GRBM_GUI_ACTIVE --kernel-trace \
+        -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_sq_$TAG" -o run --output-format csv -- \
+        python3 "$GRAFT_REPO_ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline ;;
     *) step custom 600 bash -c "$s" ;;
   esac
 done
