@@ -96,6 +96,10 @@ int knn_create(knn_ctx** out, int device) {
     delete c;
     return knn_fail(KNN_ERR_DEVICE, "hipHostMalloc failed");
   }
+  if (const char* e = getenv("KNN_PRECISION")) {
+    if (!strcmp(e, "fp32")) c->precision = KNN_PRECISION_FP32;
+    else if (!strcmp(e, "bf16x3")) c->precision = KNN_PRECISION_BF16X3;
+  }
   *out = c;
   return KNN_OK;
 }
@@ -152,8 +156,30 @@ static int build_train(knn_ctx* ctx, const double* dX, const int32_t* dlab, int6
   t.x1max = x1;
   ctx->class_cnt = class_cnt;
   ctx->idx_off = idx_off;
+  ctx->DPb = 0;  // bf16x3 copy is rebuilt lazily for the new train set
   ctx->trained = true;
   return KNN_OK;
+}
+
+// The bf16 hi/lo copy of the train rows for the bf16x3 L2 candidate pass,
+// built on first use (same row padding as X32).
+static int ensure_bf16x3(knn_ctx* ctx, hipStream_t s) {
+  const TrainDev& t = ctx->train;
+  const int DPb = pad_dim_bf16x3(t.d);
+  if (DPb <= 0) return knn_fail(KNN_ERR_ARG, "bf16x3 path supports d <= 256");
+  if (ctx->DPb == DPb) return KNN_OK;
+  int rc;
+  if ((rc = ctx->XB.ensure((size_t)t.n_pad * DPb * sizeof(float)))) return rc;
+  launch_prep_split(t.X64, t.n, t.d, DPb, t.n_pad, 1.0, (unsigned short*)ctx->XB.p, s);
+  HIP_TRY(hipGetLastError());
+  ctx->DPb = DPb;
+  return KNN_OK;
+}
+
+static bool use_bf16x3(const knn_ctx* ctx, int metric) {
+  if (metric != KNN_METRIC_L2) return false;
+  if (ctx->precision == KNN_PRECISION_FP32) return false;
+  return pad_dim_bf16x3(ctx->train.d) > 0;  // AUTO and BF16X3 (where supported)
 }
 
 static int check_train_args(int64_t n, int d, int class_cnt) {
@@ -234,50 +260,75 @@ static void choose_geometry(knn_ctx* ctx, int metric, int DP, int n_qt, int64_t 
   R_out = bestR;
 }
 
-static double err_factor(int metric, int DP) {
+// Relative factor f of the candidate-pass error bound used by the
+// certification: |proxy - exact| <= f * (max||x||^2 +
+// 2.1 ||q|| max||x||) for L2, f * (||q||_1 + max||x||_1) for L1.
+//   kmetric 0 (fp32 MFMA, an fmaf chain of DP+1 terms): gamma_{DP+1} + 5u
+//   kmetric 1 (fp32 VALU L1):                           gamma_DP + 3u
+//   kmetric 2 (bf16x3): products exact, accumulation of 3DP+1 terms bounded
+//     with u' = 2^-23 (covers truncating adders), + 2^-15 for the hi/lo
+//     representation error (~3 * 2^-18 relative per product, x2 for -2q).
+static double err_factor(int kmetric, int DP) {
   const double u = std::ldexp(1.0, -24);
-  const int n = metric == 0 ? DP + 1 : DP;
+  if (kmetric == 2) {
+    const double u2 = std::ldexp(1.0, -23);
+    const int n = 3 * DP + 1;
+    return (n * u2 / (1.0 - n * u2) + std::ldexp(1.0, -15)) * 1.02;
+  }
+  const int n = kmetric == 0 ? DP + 1 : DP;
   const double gam = n * u / (1.0 - n * u);
-  return (gam + (metric == 0 ? 5.0 : 3.0) * u) * 1.01;
+  return (gam + (kmetric == 0 ? 5.0 : 3.0) * u) * 1.01;
 }
 
 // Core search: candidate pass + merge/re-rank/certify + rescan.
 int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric, const Sink& sink,
                    hipStream_t s) {
   const TrainDev& t = ctx->train;
-  const int DP = t.DP;
+  int rc;
+  // candidate-pass flavour: kmetric 2 = L2 via bf16x3 MFMA, else fp32
+  int kmetric = metric, DP = t.DP;
+  const float* Xk = t.X32;
+  if (use_bf16x3(ctx, metric)) {
+    if ((rc = ensure_bf16x3(ctx, s))) return rc;
+    kmetric = 2;
+    DP = ctx->DPb;
+    Xk = (const float*)ctx->XB.p;
+  }
   const int n_qt = (int)((m + kQPB - 1) / kQPB);
   const int64_t m_pad = (int64_t)n_qt * kQPB;
   const int64_t n_tiles = t.n_pad / cand_tile_rows(DP);
   int C = (int)std::min<int64_t>(t.n, std::max(2 * W, W + 16));
   C = std::min(C, kMaxUnion);
   int S = 1, R = 8;
-  choose_geometry(ctx, metric, DP, n_qt, n_tiles, C, S, R);
+  choose_geometry(ctx, kmetric, DP, n_qt, n_tiles, C, S, R);
   const int NL = 2 * S;
   C = std::min(C, NL * R);
-  int rc;
   if ((rc = ctx->Q32.ensure((size_t)m_pad * DP * sizeof(float)))) return rc;
   if ((rc = ctx->cand_v.ensure((size_t)m_pad * NL * R * sizeof(float)))) return rc;
   if ((rc = ctx->cand_i.ensure((size_t)m_pad * NL * R * sizeof(int)))) return rc;
   if ((rc = ctx->rescan_q.ensure((size_t)m * sizeof(int) + 16))) return rc;
   if ((rc = ctx->rescan_cnt.ensure(16))) return rc;
 
+  ctx->last_kmetric = kmetric;
   ctx->geom[0] = (int64_t)n_qt * S;
   ctx->geom[1] = S;
   ctx->geom[2] = R;
   ctx->geom[3] = C;
   const bool tm = ctx->timing;
   if (tm) HIP_TRY(hipEventRecord(ctx->ev[0], s));
-  launch_prep_queries(dQ, m, t.d, DP, m_pad, metric == 0 ? -2.0f : 1.0f, (float*)ctx->Q32.p, s);
+  if (kmetric == 2)
+    launch_prep_split(dQ, m, t.d, DP, m_pad, -2.0, (unsigned short*)ctx->Q32.p, s);
+  else
+    launch_prep_queries(dQ, m, t.d, DP, m_pad, metric == 0 ? -2.0f : 1.0f, (float*)ctx->Q32.p, s);
   if (tm) HIP_TRY(hipEventRecord(ctx->ev[1], s));
   CandLaunch cl{};
-  cl.metric = metric;
+  cl.metric = kmetric;
   cl.DP = DP;
   cl.R = R;
   cl.S = S;
   cl.n_qt = n_qt;
   cl.n_pad = t.n_pad;
-  cl.X32 = t.X32;
+  cl.X32 = Xk;
   cl.xinit = metric == 0 ? t.xinit_l2 : t.xinit_l1;
   cl.Q32 = (const float*)ctx->Q32.p;
   cl.out_v = (float*)ctx->cand_v.p;
@@ -287,7 +338,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   if (tm) HIP_TRY(hipEventRecord(ctx->ev[2], s));
   HIP_TRY(hipMemsetAsync(ctx->rescan_cnt.p, 0, sizeof(int), s));
   launch_merge_rerank(metric, (const float*)ctx->cand_v.p, (const int*)ctx->cand_i.p, NL, R, t, dQ,
-                      m, W, C, err_factor(metric, DP), sink, (int*)ctx->rescan_q.p,
+                      m, W, C, err_factor(kmetric, DP), sink, (int*)ctx->rescan_q.p,
                       (int*)ctx->rescan_cnt.p, s);
   HIP_TRY(hipGetLastError());
   if (tm) HIP_TRY(hipEventRecord(ctx->ev[3], s));
@@ -459,6 +510,16 @@ int knn_sync(knn_ctx* ctx) {
 }
 
 int64_t knn_last_rescan_count(knn_ctx* ctx) { return ctx ? ctx->last_rescan : -1; }
+
+int knn_set_precision(knn_ctx* ctx, int mode) {
+  if (!ctx) return knn_fail(KNN_ERR_ARG, "null context");
+  if (mode < KNN_PRECISION_AUTO || mode > KNN_PRECISION_BF16X3)
+    return knn_fail(KNN_ERR_ARG, "unknown precision mode");
+  ctx->precision = mode;
+  return KNN_OK;
+}
+
+int knn_last_candidate_path(knn_ctx* ctx) { return ctx ? ctx->last_kmetric : -1; }
 
 int knn_set_timing(knn_ctx* ctx, int enable) {
   int rc;

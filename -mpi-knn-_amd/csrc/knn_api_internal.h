@@ -23,19 +23,22 @@ struct knn_ctx {
   int64_t idx_off = 0;
   int64_t last_rescan = 0;
   int cu_count = 0;
+  int precision = 0;     // KNN_PRECISION_*
+  int DPb = 0;           // padded dim of the bf16x3 copy (0 = not built)
+  int last_kmetric = -1; // candidate path of the last search (0 fp32 L2, 1 L1, 2 bf16x3)
   knnk::TrainDev train{};
   bool timing = false;
   hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
   double phase_ms[4] = {0, 0, 0, 0};
   int64_t geom[4] = {0, 0, 0, 0};
   // train-side HBM
-  DevBuf X64_own, lab_own, X32, xl2, xl1, stats;
+  DevBuf X64_own, lab_own, X32, xl2, xl1, stats, XB;
   // per-classify workspace
   DevBuf Q64, Q32, cand_v, cand_i, rescan_q, rescan_cnt, ra_k, ra_i, rb_k, rb_i;
   // host-API outputs
   DevBuf o_lab, o_idx, o_dist, o_flags;
   std::vector<DevBuf*> all_bufs() {
-    return {&X64_own, &lab_own, &X32, &xl2, &xl1, &stats, &Q64, &Q32, &cand_v, &cand_i,
+    return {&X64_own, &lab_own, &X32, &xl2, &xl1, &stats, &XB, &Q64, &Q32, &cand_v, &cand_i,
             &rescan_q, &rescan_cnt, &ra_k, &ra_i, &rb_k, &rb_i, &o_lab, &o_idx, &o_dist,
             &o_flags};
   }

@@ -43,10 +43,12 @@ struct TrainDev {
 };
 
 int pad_dim(int d);                 // padded dim the candidate kernels run at
+int pad_dim_bf16x3(int d);          // padded dim of the bf16x3 kernel, -1 if unsupported
 bool cand_supported(int DP);
 int cand_tile_rows(int DP);         // train rows per tile of the kernel serving DP
 int cand_blocks_per_cu(int metric, int DP, int R);  // resident workgroups per CU
 
+// metric: 0 = L2 fp32 MFMA, 1 = L1 fp32 VALU, 2 = L2 bf16x3 MFMA
 struct CandLaunch {
   int metric, DP, R, S, n_qt;
   int64_t n_pad;
@@ -75,5 +77,8 @@ void launch_merge_vote_partials(const double* dist, const int64_t* idx, const in
                                 int64_t* out_idx, double* out_dist, int32_t* out_flags,
                                 hipStream_t s, int64_t q0 = 0, int64_t mq = -1);
 void launch_fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t s);
+// fp64 rows -> [hi(DP) | lo(DP)] bf16 rows of scale*x (candidate metric 2 = L2 via bf16x3)
+void launch_prep_split(const double* X64, int64_t n, int d, int DP, int64_t n_pad, double scale,
+                       unsigned short* out, hipStream_t s);
 
 }  // namespace knnk

@@ -27,6 +27,7 @@
 namespace knnk {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 #define KNN_INF_F __builtin_inff()
 #define KNN_INF_D __builtin_inf()
@@ -200,6 +201,40 @@ void launch_prep_queries(const double* Q64, int64_t m, int d, int DP, int64_t m_
                      DP, m_pad, scale, Q32);
 }
 
+// bf16 hi/lo split of fp64 rows: row r of the output is [hi(DP) | lo(DP)]
+// with hi = bf16(x), lo = bf16(x - hi) (x - hi exact in fp64), scaled by
+// `scale` (exact power of two), zero padding beyond d and on pad rows.
+__device__ __forceinline__ void split_bf16(double x, unsigned short& hi, unsigned short& lo) {
+  const __bf16 h = (__bf16)(float)x;
+  const double r = x - (double)(float)h;
+  const __bf16 l = (__bf16)(float)r;
+  hi = __builtin_bit_cast(unsigned short, h);
+  lo = __builtin_bit_cast(unsigned short, l);
+}
+
+__global__ void __launch_bounds__(256)
+prep_split_kernel(const double* __restrict__ X64, int64_t n, int d, int DP, int64_t n_pad,
+                  double scale, unsigned short* __restrict__ out) {
+  const int64_t total = n_pad * DP;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * 256) {
+    const int64_t row = e / DP;
+    const int c = (int)(e - row * DP);
+    unsigned short hi = 0, lo = 0;
+    if (row < n && c < d) split_bf16(scale * X64[row * d + c], hi, lo);
+    out[row * 2 * DP + c] = hi;
+    out[row * 2 * DP + DP + c] = lo;
+  }
+}
+
+void launch_prep_split(const double* X64, int64_t n, int d, int DP, int64_t n_pad, double scale,
+                       unsigned short* out, hipStream_t s) {
+  int64_t blocks = (n_pad * DP + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(prep_split_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X64, n, d, DP,
+                     n_pad, scale, out);
+}
+
 __global__ void fill_i32_kernel(int32_t* p, int64_t n, int32_t v) {
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256)
     p[e] = v;
@@ -305,10 +340,17 @@ cand_kernel(const float* __restrict__ X32, const float* __restrict__ xinit,
   const int64_t qg = (int64_t)qt * kQPB + wv * 32 + j;
   const float* qrow = Q32 + qg * DP;
 
-  float4 qf[METRIC == 0 ? DP / 8 : 1];
-  if constexpr (METRIC == 0) {
+  // B operand resident in VGPRs for the whole kernel.  METRIC 0: fp32 -2q,
+  // float4 c holds dims 8c+4h..8c+4h+3 (four 32x32x2 k-steps).  METRIC 2:
+  // the row is [qh | ql] in bf16 (-2q split hi/lo); float4 t (t < DP/16) is
+  // qh dims 16t+8h..16t+8h+7, float4 DP/16+t the same dims of ql.
+  float4 qf[METRIC != 1 ? DP / 8 : 1];
+  if constexpr (METRIC != 1) {
 #pragma unroll
-    for (int c = 0; c < DP / 8; ++c) qf[c] = *(const float4*)(qrow + 8 * c + 4 * h);
+    for (int c = 0; c < DP / 8; ++c) {
+      const int off = METRIC == 0 ? 8 * c : (c < DP / 16 ? 8 * c : DP / 2 + 8 * (c - DP / 16));
+      qf[c] = *(const float4*)(qrow + off + 4 * h);
+    }
   }
 
   float L[R];
@@ -384,6 +426,22 @@ cand_kernel(const float* __restrict__ X32, const float* __restrict__ xinit,
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, qf[c].y, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, qf[c].z, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, qf[c].w, acc, 0, 0, 0);
+      }
+    } else if constexpr (METRIC == 2) {
+      // bf16x3 split product on v_mfma_f32_32x32x16_bf16:
+      //   q.x ~= qh.xh + ql.xh + qh.xl   (train row in LDS = [xh | xl])
+      // i.e. one bf16 GEMM with K = 3*DP; ~2^-16 relative product error,
+      // 16x the f32 MFMA rate per instruction -> 5.3x per fp32-equivalent flop.
+      const float* arow = base + j * LS + 4 * h;
+#pragma unroll
+      for (int t = 0; t < DP / 16; ++t) {
+        const bf16x8 ah = __builtin_bit_cast(bf16x8, *(const float4*)(arow + 8 * t));
+        const bf16x8 al = __builtin_bit_cast(bf16x8, *(const float4*)(arow + DP / 2 + 8 * t));
+        const bf16x8 bh = __builtin_bit_cast(bf16x8, qf[t]);
+        const bf16x8 bl = __builtin_bit_cast(bf16x8, qf[DP / 16 + t]);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
       }
     } else {
       // L1 on the VALU: lane's query against its 16 rows, dims in chunks of 4.
@@ -592,6 +650,12 @@ int pad_dim(int d) {
 
 bool cand_supported(int DP) { return DP > 0 && pad_dim(DP) == DP; }
 
+// bf16x3 path: resident kernel only (DP multiple of 16, <= 256).
+int pad_dim_bf16x3(int d) {
+  const int DP = pad_dim((d + 15) / 16 * 16);
+  return (DP <= 256 && DP % 16 == 0) ? DP : -1;
+}
+
 template <class KernelT>
 static int occupancy_of(KernelT k) {
   int nb = 0;
@@ -613,6 +677,10 @@ static void launch_str(const CandLaunch& c, hipStream_t s) {
 
 template <int DP>
 static int blocks_per_cu_res(int R, int metric) {
+  if constexpr (DP % 16 == 0) {
+    if (metric == 2)
+      return R == 8 ? occupancy_of(cand_kernel<DP, 8, 2>) : occupancy_of(cand_kernel<DP, 16, 2>);
+  }
   if (metric == 0) return R == 8 ? occupancy_of(cand_kernel<DP, 8, 0>) : occupancy_of(cand_kernel<DP, 16, 0>);
   return R == 8 ? occupancy_of(cand_kernel<DP, 8, 1>) : occupancy_of(cand_kernel<DP, 16, 1>);
 }
@@ -632,6 +700,12 @@ int cand_tile_rows(int DP) { return DP <= 256 ? kTR : 128; }
 
 template <int DP>
 static void launch_res_dp(const CandLaunch& c, hipStream_t s) {
+  if constexpr (DP % 16 == 0) {
+    if (c.metric == 2) {
+      if (c.R == 8) launch_res<DP, 8, 2>(c, s); else launch_res<DP, 16, 2>(c, s);
+      return;
+    }
+  }
   if (c.metric == 0) {
     if (c.R == 8) launch_res<DP, 8, 0>(c, s); else launch_res<DP, 16, 0>(c, s);
   } else {
@@ -777,7 +851,7 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
     qa = wave_sum_d(qa) * (1.0 + 1e-12);
     const double dw = dk[W - 1];
     if (METRIC == 0) {
-      const double E = f_err * (t.x2max + 2.0 * __builtin_sqrt(qa) * __builtin_sqrt(t.x2max)) + 1e-30;
+      const double E = f_err * (t.x2max + 2.1 * __builtin_sqrt(qa) * __builtin_sqrt(t.x2max)) + 1e-30;
       const double bound = ((double)LBa + qa * (1.0 - 2e-12) - E) * (1.0 - 1e-12);
       cert = bound > dw * dw * (1.0 + 1e-12);
     } else {

@@ -29,8 +29,9 @@ EXPORTED = (
     "knn_search_partial_device", "knn_merge_vote_device", "knn_sync", "knn_last_rescan_count",
     "knn_group_create", "knn_group_destroy", "knn_group_set_train", "knn_group_classify",
     "knn_group_last_compute_seconds", "knn_set_timing", "knn_last_phase_ms",
-    "knn_last_geometry",
+    "knn_last_geometry", "knn_set_precision", "knn_last_candidate_path",
 )
+PRECISION_AUTO, PRECISION_FP32, PRECISION_BF16X3 = 0, 1, 2
 PHASE_PREP, PHASE_CANDIDATE, PHASE_RERANK, PHASE_RESCAN = 0, 1, 2, 3
 
 
@@ -101,6 +102,8 @@ def lib():
         "knn_set_timing": ([P, ctypes.c_int], ctypes.c_int),
         "knn_last_phase_ms": ([P, ctypes.c_int], f64),
         "knn_last_geometry": ([P, ctypes.POINTER(i64)], ctypes.c_int),
+        "knn_set_precision": ([P, ctypes.c_int], ctypes.c_int),
+        "knn_last_candidate_path": ([P], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -199,6 +202,14 @@ class Classifier:
 
     def last_rescan_count(self):
         return int(lib().knn_last_rescan_count(self._h))
+
+    def set_precision(self, mode):
+        """PRECISION_AUTO (bf16x3 where supported), PRECISION_FP32, PRECISION_BF16X3.
+        Results are the exact fp64 top-k in every mode."""
+        _check(lib().knn_set_precision(self._h, int(mode)))
+
+    def last_candidate_path(self):
+        return int(lib().knn_last_candidate_path(self._h))
 
     def set_timing(self, enable=True):
         _check(lib().knn_set_timing(self._h, int(bool(enable))))

@@ -28,7 +28,15 @@ import torch
 import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-PEAK_FP32_TFLOPS = 157.3  # MI355X dense fp32 MFMA (= vector) peak, MI355X_MICROARCH.md
+PEAK_FP32_TFLOPS = 157.3   # MI355X dense fp32 MFMA (= vector) peak, MI355X_MICROARCH.md
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA peak (no sparsity), MI355X_MICROARCH.md
+
+
+def pad_dim(d):
+    for v in (16, 32, 48, 64, 96, 128, 160, 192, 256):
+        if d <= v:
+            return v
+    return d
 
 
 def load_knn():
@@ -130,34 +138,46 @@ def main():
         clf.classify_device(Q.data_ptr(), m, k, knn.L2, out_lab.data_ptr(), None, None,
                             out_flags.data_ptr(), stream)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    cand_ms, rerank_ms, rescans = [], [], 0
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-        cand_ms.append(clf.last_phase_ms(knn.PHASE_CANDIDATE))
-        rerank_ms.append(clf.last_phase_ms(knn.PHASE_RERANK))
-        rescans += clf.last_rescan_count()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    el = float(el.item())
+    def timed(precision, steps, warmup):
+        """warmup + barrier/sync-bracketed timed steps; max over ranks."""
+        clf.set_precision(precision)
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        cand_ms, rerank_ms, rescans = [], [], 0
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+            cand_ms.append(clf.last_phase_ms(knn.PHASE_CANDIDATE))
+            rerank_ms.append(clf.last_phase_ms(knn.PHASE_RERANK))
+            rescans += clf.last_rescan_count()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        return (float(el.item()), float(np.mean(cand_ms)) * 1e-3, float(np.mean(rerank_ms)),
+                rescans, clf.last_candidate_path(), clf.last_geometry())
 
+    flops = 2.0 * n * d * m  # algorithmic, per launch (norm terms excluded)
+    # default path (bf16x3 candidate pass for d <= 256), the measured `value`
+    el, t_cand, rr_ms, rescans, path, geom = timed(knn.PRECISION_AUTO, args.steps, args.warmup)
+    labels_auto = out_lab.clone()
+    # fp32-MFMA candidate pass (the north star's roofline reference), same data
+    el32, t_cand32, rr32, resc32, path32, geom32 = timed(knn.PRECISION_FP32, max(3, args.steps // 2), 1)
+    same_labels = bool(torch.equal(labels_auto, out_lab))
     total_q = m * world * args.steps
     value = total_q / el
-    t_cand = float(np.mean(cand_ms)) * 1e-3
-    flops = 2.0 * n * d * m  # algorithmic, per launch (norm terms excluded)
     achieved = flops / t_cand / 1e12
-    geom = clf.last_geometry()
+    achieved32 = flops / t_cand32 / 1e12
+    bf16 = path == 2
+    peak = PEAK_BF16_TFLOPS if bf16 else PEAK_FP32_TFLOPS
+    mfma_mult = 3.0 if bf16 else 1.0  # MFMA flops per algorithmic flop
     result = {
         "metric": "queries/sec (node) + % MFMA peak, 1M train x 10k query d=128 k=10, 1/2/4/8 GPU",
         "value": value,
@@ -169,24 +189,32 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": "bf16x3" if bf16 else "fp32",
         "data": "synthetic (seeded Gaussian mixture, min-max normalised, fp64 inputs)",
         "config": {"workload": "cfg2: %d train x %d queries per GPU, d=%d, k=%d, L2, %d classes"
                                % (n, m, d, k, C),
                    "n_train": n, "queries_per_gpu": m, "dim": d, "k": k,
                    "parallelism": "query-sharded dp%d" % world,
-                   "candidate_pass": "fp32 MFMA 32x32x2 + fused top-16 per lane",
-                   "rerank": "fp64 exact (reference arithmetic), certified",
+                   "candidate_pass": ("bf16x3 split (qh.xh+ql.xh+qh.xl) on MFMA 32x32x16 bf16"
+                                      if bf16 else "fp32 MFMA 32x32x2") + " + fused top-R per lane",
+                   "rerank": "fp64 exact (reference arithmetic), certified; labels exact",
                    "geometry": geom, "rescanned_queries": rescans},
-        "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_TFLOPS,
-                     "unit": "TFLOP/s", "frac": achieved / PEAK_FP32_TFLOPS, "traffic": None,
-                     "kernel": "cand_kernel<128,16,0>", "kernel_ms": t_cand * 1e3,
-                     "rerank_ms": float(np.mean(rerank_ms)),
-                     "algorithmic_flops_per_launch": flops},
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak,
+                     "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
+                     "kernel": "cand_kernel<%d,%d,%d>" % (pad_dim(d), geom["lists"], path),
+                     "kernel_ms": t_cand * 1e3, "rerank_ms": rr_ms,
+                     "algorithmic_flops_per_launch": flops,
+                     "mfma_flops_per_algorithmic_flop": mfma_mult,
+                     "frac_of_issued_mfma": achieved * mfma_mult / peak},
+        "fp32_path": {"value": m * world * max(3, args.steps // 2) / el32, "unit": "queries/s",
+                      "kernel_ms": t_cand32 * 1e3, "achieved": achieved32,
+                      "peak": PEAK_FP32_TFLOPS, "frac": achieved32 / PEAK_FP32_TFLOPS,
+                      "rescanned_queries": resc32, "geometry": geom32,
+                      "labels_equal_default_path": same_labels},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(X, lab, Q, k, C, out_lab.cpu().numpy())
+        result["cpu_baseline"] = cpu_baseline(X, lab, Q, k, C, labels_auto.cpu().numpy())
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -137,6 +137,20 @@ double knn_last_phase_ms(knn_ctx* ctx, int phase);
  * per query tile, out[2]=list entries per lane (R), out[3]=re-rank count C. */
 int knn_last_geometry(knn_ctx* ctx, int64_t out[4]);
 
+/* Candidate-pass precision for L2 (the result is the exact fp64 top-k in
+ * every mode; this only selects how candidates are found):
+ *   AUTO (default): bf16x3 where supported (d <= 256), else fp32;
+ *   FP32: v_mfma_f32_32x32x2_f32 on fp32 copies;
+ *   BF16X3: q.x as qh.xh + ql.xh + qh.xl on v_mfma_f32_32x32x16_bf16
+ *           (hi/lo bf16 split of the fp64 values, ~2^-16 relative error).
+ * Environment override at knn_create: KNN_PRECISION=fp32|bf16x3. */
+#define KNN_PRECISION_AUTO 0
+#define KNN_PRECISION_FP32 1
+#define KNN_PRECISION_BF16X3 2
+int knn_set_precision(knn_ctx* ctx, int mode);
+/* Candidate kernel flavour of the last search: 0 fp32 L2, 1 fp32 L1, 2 bf16x3 L2. */
+int knn_last_candidate_path(knn_ctx* ctx);
+
 /* Synchronise the context's stream. */
 int knn_sync(knn_ctx* ctx);
 /* Last classify's count of queries that needed the exact rescan. */

@@ -34,9 +34,12 @@ def knn():
     return mod
 
 
-@pytest.fixture(scope="module")
-def clf(knn):
+@pytest.fixture(scope="module", params=["auto", "fp32"])
+def clf(knn, request):
+    """Every parity test runs with the default candidate path (bf16x3 for L2
+    where supported) and with the fp32 path forced."""
     c = knn.Classifier(0)
+    c.set_precision(knn.PRECISION_AUTO if request.param == "auto" else knn.PRECISION_FP32)
     yield c
     c.close()
 
