@@ -240,8 +240,9 @@ static void choose_geometry(knn_ctx* ctx, int metric, int DP, int n_qt, int64_t 
     ctx->cu_count = cus;
   }
   const int S_hi = (int)std::max<int64_t>(1, std::min<int64_t>(64, n_tiles));
-  int bestS = 1, bestR = 8;
-  for (int R : {8, 16}) {
+  int bestS = 1, bestR = 4;
+  for (int R : {4, 8, 16}) {
+    if (ctx->tune_R && R != ctx->tune_R) continue;
     const int64_t slots = (int64_t)cand_blocks_per_cu(metric, DP, R) * ctx->cu_count;
     const int S_lo = std::min(S_hi, std::max(1, (C + 2 * R - 1) / (2 * R)));
     double best = -1.0;
@@ -252,9 +253,12 @@ static void choose_geometry(knn_ctx* ctx, int metric, int DP, int n_qt, int64_t 
       const double eff = (double)wg / (double)(rounds * slots);
       if (eff > best + 1e-3) { best = eff; bS = S; }
     }
+    if (ctx->tune_S) bS = std::min(ctx->tune_S, S_hi);
     bestS = bS;
     bestR = R;
-    if (C <= 4 * bS) break;  // expected per-list share of the C candidates <= 2: R = 8 is ample
+    // expected share of the C re-rank candidates per list (2S lists): R = 4
+    // when <= 1/2, R = 8 when <= 2, else 16 (certification catches the rest)
+    if (ctx->tune_R || (R == 4 && 2 * C <= 2 * bS) || (R == 8 && C <= 4 * bS)) break;
   }
   S_out = bestS;
   R_out = bestR;
@@ -520,6 +524,21 @@ int knn_set_precision(knn_ctx* ctx, int mode) {
 }
 
 int knn_last_candidate_path(knn_ctx* ctx) { return ctx ? ctx->last_kmetric : -1; }
+
+int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value) {
+  if (!ctx || !key) return knn_fail(KNN_ERR_ARG, "null argument");
+  if (!strcmp(key, "R")) {
+    if (value != 0 && value != 4 && value != 8 && value != 16)
+      return knn_fail(KNN_ERR_ARG, "R must be 0 (auto), 4, 8 or 16");
+    ctx->tune_R = (int)value;
+  } else if (!strcmp(key, "S")) {
+    if (value < 0 || value > 64) return knn_fail(KNN_ERR_ARG, "S must be 0 (auto) .. 64");
+    ctx->tune_S = (int)value;
+  } else {
+    return knn_fail(KNN_ERR_ARG, std::string("unknown tuning key ") + key);
+  }
+  return KNN_OK;
+}
 
 int knn_set_timing(knn_ctx* ctx, int enable) {
   int rc;

@@ -22,6 +22,8 @@
 #include <float.h>
 #include <limits.h>
 
+#include <type_traits>
+
 #pragma clang fp contract(off)
 
 namespace knnk {
@@ -675,42 +677,54 @@ static void launch_str(const CandLaunch& c, hipStream_t s) {
                      c.n_qt, c.out_v, c.out_i);
 }
 
+// Compile-time dispatch over (R, METRIC): R in {4, 8, 16}; METRIC 0/1/2
+// (2 = bf16x3, resident kernel with DP % 16 == 0 only).
+template <class F>
+static void with_R(int R, F f) {
+  if (R == 4) f(std::integral_constant<int, 4>{});
+  else if (R == 8) f(std::integral_constant<int, 8>{});
+  else f(std::integral_constant<int, 16>{});
+}
+template <class F>
+static void with_M(int M, F f) {
+  if (M == 0) f(std::integral_constant<int, 0>{});
+  else if (M == 1) f(std::integral_constant<int, 1>{});
+  else f(std::integral_constant<int, 2>{});
+}
+
 template <int DP>
 static int blocks_per_cu_res(int R, int metric) {
-  if constexpr (DP % 16 == 0) {
-    if (metric == 2)
-      return R == 8 ? occupancy_of(cand_kernel<DP, 8, 2>) : occupancy_of(cand_kernel<DP, 16, 2>);
-  }
-  if (metric == 0) return R == 8 ? occupancy_of(cand_kernel<DP, 8, 0>) : occupancy_of(cand_kernel<DP, 16, 0>);
-  return R == 8 ? occupancy_of(cand_kernel<DP, 8, 1>) : occupancy_of(cand_kernel<DP, 16, 1>);
+  int out = 1;
+  with_R(R, [&](auto Rc) {
+    with_M(metric, [&](auto Mc) {
+      if constexpr (Mc.value != 2 || DP % 16 == 0)
+        out = occupancy_of(cand_kernel<DP, Rc.value, Mc.value>);
+    });
+  });
+  return out;
 }
 
 int cand_blocks_per_cu(int metric, int DP, int R) {
 #define KNN_CASE(v) if (DP == v) return blocks_per_cu_res<v>(R, metric);
   KNN_DP_LIST(KNN_CASE)
 #undef KNN_CASE
-  if (metric == 0)
-    return R == 8 ? occupancy_of(cand_stream_kernel<kStreamDC, 8, 0>)
-                  : occupancy_of(cand_stream_kernel<kStreamDC, 16, 0>);
-  return R == 8 ? occupancy_of(cand_stream_kernel<kStreamDC, 8, 1>)
-                : occupancy_of(cand_stream_kernel<kStreamDC, 16, 1>);
+  int out = 1;
+  with_R(R, [&](auto Rc) {
+    if (metric == 1) out = occupancy_of(cand_stream_kernel<kStreamDC, Rc.value, 1>);
+    else out = occupancy_of(cand_stream_kernel<kStreamDC, Rc.value, 0>);
+  });
+  return out;
 }
 
 int cand_tile_rows(int DP) { return DP <= 256 ? kTR : 128; }
 
 template <int DP>
 static void launch_res_dp(const CandLaunch& c, hipStream_t s) {
-  if constexpr (DP % 16 == 0) {
-    if (c.metric == 2) {
-      if (c.R == 8) launch_res<DP, 8, 2>(c, s); else launch_res<DP, 16, 2>(c, s);
-      return;
-    }
-  }
-  if (c.metric == 0) {
-    if (c.R == 8) launch_res<DP, 8, 0>(c, s); else launch_res<DP, 16, 0>(c, s);
-  } else {
-    if (c.R == 8) launch_res<DP, 8, 1>(c, s); else launch_res<DP, 16, 1>(c, s);
-  }
+  with_R(c.R, [&](auto Rc) {
+    with_M(c.metric, [&](auto Mc) {
+      if constexpr (Mc.value != 2 || DP % 16 == 0) launch_res<DP, Rc.value, Mc.value>(c, s);
+    });
+  });
 }
 
 void launch_cand(const CandLaunch& c, hipStream_t s) {
@@ -721,11 +735,10 @@ void launch_cand(const CandLaunch& c, hipStream_t s) {
   }
   KNN_DP_LIST(KNN_CASE)
 #undef KNN_CASE
-  if (c.metric == 0) {
-    if (c.R == 8) launch_str<8, 0>(c, s); else launch_str<16, 0>(c, s);
-  } else {
-    if (c.R == 8) launch_str<8, 1>(c, s); else launch_str<16, 1>(c, s);
-  }
+  with_R(c.R, [&](auto Rc) {
+    if (c.metric == 1) launch_str<Rc.value, 1>(c, s);
+    else launch_str<Rc.value, 0>(c, s);
+  });
 }
 
 // ------------------------------------------------ finish: vote / outputs

@@ -29,7 +29,7 @@ EXPORTED = (
     "knn_search_partial_device", "knn_merge_vote_device", "knn_sync", "knn_last_rescan_count",
     "knn_group_create", "knn_group_destroy", "knn_group_set_train", "knn_group_classify",
     "knn_group_last_compute_seconds", "knn_set_timing", "knn_last_phase_ms",
-    "knn_last_geometry", "knn_set_precision", "knn_last_candidate_path",
+    "knn_last_geometry", "knn_set_precision", "knn_last_candidate_path", "knn_set_tuning",
 )
 PRECISION_AUTO, PRECISION_FP32, PRECISION_BF16X3 = 0, 1, 2
 PHASE_PREP, PHASE_CANDIDATE, PHASE_RERANK, PHASE_RESCAN = 0, 1, 2, 3
@@ -104,6 +104,7 @@ def lib():
         "knn_last_geometry": ([P, ctypes.POINTER(i64)], ctypes.c_int),
         "knn_set_precision": ([P, ctypes.c_int], ctypes.c_int),
         "knn_last_candidate_path": ([P], ctypes.c_int),
+        "knn_set_tuning": ([P, ctypes.c_char_p, i64], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -207,6 +208,10 @@ class Classifier:
         """PRECISION_AUTO (bf16x3 where supported), PRECISION_FP32, PRECISION_BF16X3.
         Results are the exact fp64 top-k in every mode."""
         _check(lib().knn_set_precision(self._h, int(mode)))
+
+    def set_tuning(self, key, value):
+        """Experiment overrides: key "R" (0/4/8/16) or "S" (0..64); 0 = automatic."""
+        _check(lib().knn_set_tuning(self._h, key.encode(), int(value)))
 
     def last_candidate_path(self):
         return int(lib().knn_last_candidate_path(self._h))

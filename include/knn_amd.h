@@ -151,6 +151,10 @@ int knn_set_precision(knn_ctx* ctx, int mode);
 /* Candidate kernel flavour of the last search: 0 fp32 L2, 1 fp32 L1, 2 bf16x3 L2. */
 int knn_last_candidate_path(knn_ctx* ctx);
 
+/* Tuning overrides for experiments (0 = automatic): "R" list entries per
+ * lane (4, 8, 16), "S" train splits per query tile (1..64). */
+int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value);
+
 /* Synchronise the context's stream. */
 int knn_sync(knn_ctx* ctx);
 /* Last classify's count of queries that needed the exact rescan. */

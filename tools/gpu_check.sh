@@ -41,6 +41,7 @@ for s in $stages; do
         SQ_INSTS_MFMA SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_LDS GRBM_GUI_ACTIVE --kernel-trace \
         -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_sq_$TAG" -o run --output-format csv -- \
         python3 "$GRAFT_REPO_ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline ;;
+    tune) step tune 600 python tools/tune.py ${TUNE_ARGS:-} ;;
     *) step custom 600 bash -c "$s" ;;
   esac
 done

@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""In-process A/B timing of candidate-kernel variants on cfg2-shaped data
+(interleaved rounds, medians; cdna_hip_programming.md §5.4 rule 24).
+Usage: python tools/tune.py [--rounds 5] [--n 1000000 --m 10000 --d 128 --k 10]
+Variants: "prec:R:S" e.g. auto:0:0 fp32:8:0 auto:4:0"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--m", type=int, default=10_000)
+    ap.add_argument("--d", type=int, default=128)
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("variants", nargs="*", default=["auto:0:0", "auto:4:0", "auto:8:0", "fp32:0:0"])
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    knn = bench.load_knn()
+    X, lab, Q, _ = bench.synth(a.n, a.m, a.d, 10, 1234, 5678, dev)
+    clf = knn.Classifier(0)
+    clf.set_train_device(X.data_ptr(), lab.data_ptr(), a.n, a.d, 10, keep=(X, lab))
+    clf.set_timing(True)
+    out = torch.empty(a.m, dtype=torch.int32, device=dev)
+    ref = None
+    res = {v: [] for v in a.variants}
+    info = {}
+    prec = {"auto": knn.PRECISION_AUTO, "fp32": knn.PRECISION_FP32, "bf16x3": knn.PRECISION_BF16X3}
+    for r in range(a.rounds + 1):
+        for v in a.variants:
+            p, R, S = v.split(":")
+            clf.set_precision(prec[p])
+            clf.set_tuning("R", int(R))
+            clf.set_tuning("S", int(S))
+            clf.classify_device(Q.data_ptr(), a.m, a.k, knn.L2, out.data_ptr())
+            clf.sync()
+            if r == 0:
+                if ref is None:
+                    ref = out.clone()
+                info[v] = (clf.last_geometry(), clf.last_rescan_count(), bool(torch.equal(ref, out)))
+                continue
+            res[v].append(clf.last_phase_ms(knn.PHASE_CANDIDATE))
+    flops = 2.0 * a.n * a.d * a.m
+    for v in a.variants:
+        ms = np.median(res[v])
+        print("%-14s cand %8.3f ms (min %8.3f)  %7.1f TF/s  %s rescans=%d same_labels=%s"
+              % (v, ms, np.min(res[v]), flops / ms / 1e9, info[v][0], info[v][1], info[v][2]))
+
+
+if __name__ == "__main__":
+    main()
