@@ -337,6 +337,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   cl.Q32 = (const float*)ctx->Q32.p;
   cl.out_v = (float*)ctx->cand_v.p;
   cl.out_i = (int*)ctx->cand_i.p;
+  cl.ablate = ctx->tune_ablate;
   launch_cand(cl, s);
   HIP_TRY(hipGetLastError());
   if (tm) HIP_TRY(hipEventRecord(ctx->ev[2], s));
@@ -531,6 +532,8 @@ int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value) {
     if (value != 0 && value != 4 && value != 8 && value != 16)
       return knn_fail(KNN_ERR_ARG, "R must be 0 (auto), 4, 8 or 16");
     ctx->tune_R = (int)value;
+  } else if (!strcmp(key, "ablate")) {
+    ctx->tune_ablate = (int)value;  // timing experiments only: results become invalid
   } else if (!strcmp(key, "S")) {
     if (value < 0 || value > 64) return knn_fail(KNN_ERR_ARG, "S must be 0 (auto) .. 64");
     ctx->tune_S = (int)value;

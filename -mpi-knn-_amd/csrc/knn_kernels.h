@@ -57,6 +57,7 @@ struct CandLaunch {
   const float* Q32;
   float* out_v;
   int* out_i;
+  int ablate;  // timing-only ablation bits (0 in production)
 };
 
 void launch_prep_train(const double* X64, int64_t n, int d, int DP, int64_t n_pad, float* X32,

@@ -325,7 +325,9 @@ template <int DP, int R, int METRIC>
 __global__ void __launch_bounds__(256)
 cand_kernel(const float* __restrict__ X32, const float* __restrict__ xinit,
             const float* __restrict__ Q32, int n_tiles, int S, int n_qt,
-            float* __restrict__ out_v, int* __restrict__ out_i) {
+            float* __restrict__ out_v, int* __restrict__ out_i, int abl) {
+  // abl: timing-only ablations (results invalid): bit0 = no global staging
+  // loads after the first tile, bit1 = no selection epilogue.  0 in production.
   constexpr int CPR = DP / 4;      // float4 chunks per row
   constexpr int LS = DP + 4;       // LDS row stride in floats (16-B pad)
   constexpr int TF = kTR * LS;     // floats per tile buffer
@@ -406,7 +408,7 @@ cand_kernel(const float* __restrict__ X32, const float* __restrict__ xinit,
   for (int it = 0; it < my_nt; ++it) {
     const int t = split + it * S;
     const bool more = it + 1 < my_nt;
-    if (more) KNN_LOAD_TILE(t + S);  // in flight during this tile's compute
+    if (more && !(abl & 1)) KNN_LOAD_TILE(t + S);  // in flight during this tile's compute
     const float* base = lds + (it & 1) * TF;
     const float* nb = ldsn + (it & 1) * kTR;
 
@@ -464,7 +466,8 @@ cand_kernel(const float* __restrict__ X32, const float* __restrict__ xinit,
       }
     }
 
-    select_block<R>(acc, t * kTR, h, L, I, thr);
+    if (!(abl & 2)) select_block<R>(acc, t * kTR, h, L, I, thr);
+    else if (acc[0] == 1234.5f && acc[15] == 1234.5f) thr = acc[7];  // keep acc live
 
     if (more) KNN_STORE_TILE((it + 1) & 1);
     __syncthreads();
@@ -668,7 +671,8 @@ static int occupancy_of(KernelT k) {
 template <int DP, int R, int METRIC>
 static void launch_res(const CandLaunch& c, hipStream_t s) {
   hipLaunchKernelGGL((cand_kernel<DP, R, METRIC>), dim3((unsigned)(c.n_qt * c.S)), dim3(256), 0, s,
-                     c.X32, c.xinit, c.Q32, (int)(c.n_pad / kTR), c.S, c.n_qt, c.out_v, c.out_i);
+                     c.X32, c.xinit, c.Q32, (int)(c.n_pad / kTR), c.S, c.n_qt, c.out_v, c.out_i,
+                     c.ablate);
 }
 template <int R, int METRIC>
 static void launch_str(const CandLaunch& c, hipStream_t s) {

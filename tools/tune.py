@@ -2,7 +2,8 @@
 """In-process A/B timing of candidate-kernel variants on cfg2-shaped data
 (interleaved rounds, medians; cdna_hip_programming.md §5.4 rule 24).
 Usage: python tools/tune.py [--rounds 5] [--n 1000000 --m 10000 --d 128 --k 10]
-Variants: "prec:R:S" e.g. auto:0:0 fp32:8:0 auto:4:0"""
+Variants: "prec:R:S[:ablate]" e.g. auto:0:0 fp32:8:0 auto:4:0 auto:8:0:1
+(ablate bits: 1 = no staging loads, 2 = no selection epilogue; timing only)"""
 import argparse
 import os
 import sys
@@ -37,10 +38,13 @@ def main():
     prec = {"auto": knn.PRECISION_AUTO, "fp32": knn.PRECISION_FP32, "bf16x3": knn.PRECISION_BF16X3}
     for r in range(a.rounds + 1):
         for v in a.variants:
-            p, R, S = v.split(":")
+            parts = v.split(":")
+            p, R, S = parts[:3]
+            abl = int(parts[3]) if len(parts) > 3 else 0
             clf.set_precision(prec[p])
             clf.set_tuning("R", int(R))
             clf.set_tuning("S", int(S))
+            clf.set_tuning("ablate", abl)
             clf.classify_device(Q.data_ptr(), a.m, a.k, knn.L2, out.data_ptr())
             clf.sync()
             if r == 0:
