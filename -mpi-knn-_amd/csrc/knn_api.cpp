@@ -128,7 +128,9 @@ static int build_train(knn_ctx* ctx, const double* dX, const int32_t* dlab, int6
     return knn_fail(KNN_ERR_ARG, "dimension " + std::to_string(d) + " not supported by this build");
   const int64_t n_pad = (n + kRowAlign - 1) / kRowAlign * kRowAlign;
   int rc;
-  if ((rc = ctx->X32.ensure((size_t)n_pad * DP * sizeof(float)))) return rc;
+  // padded rows [payload | seeds] (+1 KiB slack: the last LDS-DMA piece of
+  // the last tile may read past the final row)
+  if ((rc = ctx->X32.ensure((size_t)n_pad * (DP + 4) * sizeof(float) + 1024))) return rc;
   if ((rc = ctx->xl2.ensure((size_t)n_pad * sizeof(float)))) return rc;
   if ((rc = ctx->xl1.ensure((size_t)n_pad * sizeof(float)))) return rc;
   if ((rc = ctx->stats.ensure(2 * sizeof(unsigned long long)))) return rc;
@@ -169,8 +171,9 @@ static int ensure_bf16x3(knn_ctx* ctx, hipStream_t s) {
   if (DPb <= 0) return knn_fail(KNN_ERR_ARG, "bf16x3 path supports d <= 256");
   if (ctx->DPb == DPb) return KNN_OK;
   int rc;
-  if ((rc = ctx->XB.ensure((size_t)t.n_pad * DPb * sizeof(float)))) return rc;
-  launch_prep_split(t.X64, t.n, t.d, DPb, t.n_pad, 1.0, (unsigned short*)ctx->XB.p, s);
+  if ((rc = ctx->XB.ensure((size_t)t.n_pad * (DPb + 4) * sizeof(float) + 1024))) return rc;
+  launch_prep_split(t.X64, t.n, t.d, DPb, t.n_pad, 1.0, (unsigned short*)ctx->XB.p, 2 * (DPb + 4),
+                    t.xinit_l2, t.xinit_l1, s);
   HIP_TRY(hipGetLastError());
   ctx->DPb = DPb;
   return KNN_OK;
@@ -243,7 +246,7 @@ static void choose_geometry(knn_ctx* ctx, int metric, int DP, int n_qt, int64_t 
   int bestS = 1, bestR = 4;
   for (int R : {4, 8, 16}) {
     if (ctx->tune_R && R != ctx->tune_R) continue;
-    const int64_t slots = (int64_t)cand_blocks_per_cu(metric, DP, R) * ctx->cu_count;
+    const int64_t slots = (int64_t)cand_blocks_per_cu(metric, DP, R, ctx->staging) * ctx->cu_count;
     const int S_lo = std::min(S_hi, std::max(1, (C + 2 * R - 1) / (2 * R)));
     double best = -1.0;
     int bS = S_lo;
@@ -321,7 +324,8 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   const bool tm = ctx->timing;
   if (tm) HIP_TRY(hipEventRecord(ctx->ev[0], s));
   if (kmetric == 2)
-    launch_prep_split(dQ, m, t.d, DP, m_pad, -2.0, (unsigned short*)ctx->Q32.p, s);
+    launch_prep_split(dQ, m, t.d, DP, m_pad, -2.0, (unsigned short*)ctx->Q32.p, 2 * DP, nullptr,
+                      nullptr, s);
   else
     launch_prep_queries(dQ, m, t.d, DP, m_pad, metric == 0 ? -2.0f : 1.0f, (float*)ctx->Q32.p, s);
   if (tm) HIP_TRY(hipEventRecord(ctx->ev[1], s));
@@ -338,6 +342,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   cl.out_v = (float*)ctx->cand_v.p;
   cl.out_i = (int*)ctx->cand_i.p;
   cl.ablate = ctx->tune_ablate;
+  cl.staging = ctx->staging;
   launch_cand(cl, s);
   HIP_TRY(hipGetLastError());
   if (tm) HIP_TRY(hipEventRecord(ctx->ev[2], s));
@@ -532,6 +537,9 @@ int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value) {
     if (value != 0 && value != 4 && value != 8 && value != 16)
       return knn_fail(KNN_ERR_ARG, "R must be 0 (auto), 4, 8 or 16");
     ctx->tune_R = (int)value;
+  } else if (!strcmp(key, "staging")) {
+    if (value != 0 && value != 1) return knn_fail(KNN_ERR_ARG, "staging must be 0 or 1");
+    ctx->staging = (int)value;
   } else if (!strcmp(key, "ablate")) {
     ctx->tune_ablate = (int)value;  // timing experiments only: results become invalid
   } else if (!strcmp(key, "S")) {

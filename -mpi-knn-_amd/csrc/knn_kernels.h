@@ -34,7 +34,7 @@ struct Sink {
 struct TrainDev {
   const double* X64;     // [n][d] fp64 (reference values)
   const int32_t* lab;    // [n]
-  const float* X32;      // [n_pad][DP] fp32, zero padded
+  const float* X32;      // [n_pad][DP+4] fp32 padded rows (payload | seeds), zero padded
   const float* xinit_l2; // [n_pad] fl32(||x32||^2); +inf on pad rows
   const float* xinit_l1; // [n_pad] 0; +inf on pad rows
   int64_t n, n_pad;
@@ -46,7 +46,7 @@ int pad_dim(int d);                 // padded dim the candidate kernels run at
 int pad_dim_bf16x3(int d);          // padded dim of the bf16x3 kernel, -1 if unsupported
 bool cand_supported(int DP);
 int cand_tile_rows(int DP);         // train rows per tile of the kernel serving DP
-int cand_blocks_per_cu(int metric, int DP, int R);  // resident workgroups per CU
+int cand_blocks_per_cu(int metric, int DP, int R, int staging);  // resident workgroups per CU
 
 // metric: 0 = L2 fp32 MFMA, 1 = L1 fp32 VALU, 2 = L2 bf16x3 MFMA
 struct CandLaunch {
@@ -57,7 +57,8 @@ struct CandLaunch {
   const float* Q32;
   float* out_v;
   int* out_i;
-  int ablate;  // timing-only ablation bits (0 in production)
+  int ablate;   // timing-only ablation bits (0 in production)
+  int staging;  // resident kernel: 1 = global_load_lds 3-stage, 0 = register staging
 };
 
 void launch_prep_train(const double* X64, int64_t n, int d, int DP, int64_t n_pad, float* X32,
@@ -79,7 +80,10 @@ void launch_merge_vote_partials(const double* dist, const int64_t* idx, const in
                                 hipStream_t s, int64_t q0 = 0, int64_t mq = -1);
 void launch_fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t s);
 // fp64 rows -> [hi(DP) | lo(DP)] bf16 rows of scale*x (candidate metric 2 = L2 via bf16x3)
+// rows of `out` are row_shorts 16-bit words; xl2/xl1 (train only, else null)
+// fill the padded row's seed floats after the 2*DP bf16 payload
 void launch_prep_split(const double* X64, int64_t n, int d, int DP, int64_t n_pad, double scale,
-                       unsigned short* out, hipStream_t s);
+                       unsigned short* out, int row_shorts, const float* xl2, const float* xl1,
+                       hipStream_t s);
 
 }  // namespace knnk

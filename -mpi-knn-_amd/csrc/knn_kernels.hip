@@ -140,6 +140,7 @@ __global__ void __launch_bounds__(256)
 prep_train_kernel(const double* __restrict__ X64, int64_t n, int d, int DP, int64_t n_pad,
                   float* __restrict__ X32, float* __restrict__ xl2, float* __restrict__ xl1,
                   unsigned long long* __restrict__ stats) {
+  const int RSF = DP + 4;  // padded row: [x32 (DP) | ||x32||^2, l1 seed, 0, 0]
   const int lane = threadIdx.x & 63;
   const int64_t wstride = (int64_t)gridDim.x * 4;
   double m2 = 0.0, m1 = 0.0;
@@ -153,15 +154,20 @@ prep_train_kernel(const double* __restrict__ X64, int64_t n, int d, int DP, int6
         s64 += x * x;
         a64 += __builtin_fabs(x);
       }
-      X32[row * DP + c] = v;
+      X32[row * RSF + c] = v;
       s32 += (double)v * (double)v;
     }
     s32 = wave_sum_d(s32);
     s64 = wave_sum_d(s64);
     a64 = wave_sum_d(a64);
-    if (lane == 0) {
-      xl2[row] = row < n ? (float)s32 : KNN_INF_F;
-      xl1[row] = row < n ? 0.0f : KNN_INF_F;
+    if (lane < 4) {
+      const float s2 = row < n ? (float)s32 : KNN_INF_F;
+      const float s1 = row < n ? 0.0f : KNN_INF_F;
+      X32[row * RSF + DP + lane] = lane == 0 ? s2 : (lane == 1 ? s1 : 0.0f);
+      if (lane == 0) {
+        xl2[row] = s2;
+        xl1[row] = s1;
+      }
     }
     m2 = fmax(m2, s64);
     m1 = fmax(m1, a64);
@@ -216,7 +222,9 @@ __device__ __forceinline__ void split_bf16(double x, unsigned short& hi, unsigne
 
 __global__ void __launch_bounds__(256)
 prep_split_kernel(const double* __restrict__ X64, int64_t n, int d, int DP, int64_t n_pad,
-                  double scale, unsigned short* __restrict__ out) {
+                  double scale, unsigned short* __restrict__ out, int row_shorts,
+                  const float* __restrict__ xl2, const float* __restrict__ xl1) {
+  // row r of `out` (row_shorts 16-bit words) = [hi(DP) | lo(DP) | seeds...]
   const int64_t total = n_pad * DP;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * 256) {
@@ -224,17 +232,22 @@ prep_split_kernel(const double* __restrict__ X64, int64_t n, int d, int DP, int6
     const int c = (int)(e - row * DP);
     unsigned short hi = 0, lo = 0;
     if (row < n && c < d) split_bf16(scale * X64[row * d + c], hi, lo);
-    out[row * 2 * DP + c] = hi;
-    out[row * 2 * DP + DP + c] = lo;
+    out[row * row_shorts + c] = hi;
+    out[row * row_shorts + DP + c] = lo;
+    if (xl2 && c < 4) {  // train rows: the padded row's seed floats
+      float* seed = (float*)(out + row * row_shorts + 2 * DP);
+      seed[c] = c == 0 ? xl2[row] : (c == 1 ? xl1[row] : 0.0f);
+    }
   }
 }
 
 void launch_prep_split(const double* X64, int64_t n, int d, int DP, int64_t n_pad, double scale,
-                       unsigned short* out, hipStream_t s) {
+                       unsigned short* out, int row_shorts, const float* xl2, const float* xl1,
+                       hipStream_t s) {
   int64_t blocks = (n_pad * DP + 255) / 256;
   if (blocks > 16384) blocks = 16384;
   hipLaunchKernelGGL(prep_split_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X64, n, d, DP,
-                     n_pad, scale, out);
+                     n_pad, scale, out, row_shorts, xl2, xl1);
 }
 
 __global__ void fill_i32_kernel(int32_t* p, int64_t n, int32_t v) {
@@ -267,6 +280,22 @@ __device__ __forceinline__ void list_insert(float (&L)[R], int (&I)[R], float v,
   }
   I[0] = cc ? id : I[0];
   L[0] = __builtin_fminf(v, L[0]);
+}
+
+// One 16-B-per-lane LDS-DMA piece (global_load_lds_dwordx4): 64 lanes x 16 B
+// from per-lane global addresses to LDS [lds_addr, lds_addr + 1 KiB).  Issued
+// from inline asm so hipcc neither counts it nor inserts its own
+// s_waitcnt vmcnt(0) before later LDS reads (it would drain the pipeline);
+// the kernel waits with explicit counted vmcnt + s_barrier instead.  M0 is
+// compiler-reserved, so it is saved and restored inside the statement.
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_addr) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_addr))
+      : "memory");
 }
 
 // Fused top-R selection over one 32x32 accumulator block: lane (j, h) holds
@@ -309,37 +338,56 @@ __device__ __forceinline__ void write_lists(float* __restrict__ out_v, int* __re
   }
 }
 
+// Train rows in HBM (X32 for fp32/L1, XB for bf16x3) share one padded row
+// format of RSF = DP + 4 floats: [payload (DP floats) | ||x32||^2, l1 seed,
+// 0, 0], where payload is DP fp32 values or [hi(DP) | lo(DP)] bf16.  A tile
+// is 32 consecutive rows = one contiguous block, copied linearly into LDS;
+// the odd 16-B row stride (DP/4 + 1 chunks) makes the A-fragment reads
+// (ds_read_b128, 16-lane groups on distinct rows) bank-conflict free, and the
+// accumulator seeds come from the same rows.  Pad rows carry +inf seeds.
+//
 // Workgroup = 4 waves = 128 queries; it streams the 32-row train tiles
 // split, split+S, split+2S, ... (round-robin so a run of similar rows is
 // spread over all splits).  Lane (j = lane&31, h = lane>>5) of wave w owns
 // query j of the wave and the train rows rho(i,h) = (i&3) + 8(i>>2) + 4h of
 // every tile (the 32x32 MFMA C/D layout with train rows on A, queries on B).
 //
-// L2, per 32-row tile and wave: DP/2 MFMAs 32x32x2 f32.  A operand (train)
-// from LDS: lane (r, h) reads float4 X[r][8c+4h .. 8c+4h+3] for the four
-// k-steps of group c (ds_read_b128; 16-B row padding makes the 16-lane groups
-// conflict-free since DP/4+1 is odd).  B operand (queries, pre-scaled by -2)
-// stays in VGPRs for the whole kernel with the same k assignment.
-// Accumulators start at ||x_row||^2 (xinit), so acc = ||x||^2 - 2 q.x.
-template <int DP, int R, int METRIC>
+// METRIC 0, per tile and wave: DP/2 MFMAs 32x32x2 f32; lane (r, h) reads
+// float4 X[r][8c+4h ..] for the four k-steps of group c.  METRIC 2: 3*DP/16
+// MFMAs 32x32x16 bf16 (see below).  The B operand (queries, -2 q) stays in
+// VGPRs for the whole kernel.  Accumulators start at ||x_row||^2, so
+// acc = ||x||^2 - 2 q.x.
+//
+// Staging (STG): 1 = global_load_lds (LDS-DMA, no VGPRs): 3 LDS buffers,
+// tile it+2 is issued right after the barrier that opens tile it, and each
+// wave waits with a counted vmcnt for its own pieces of tile it before that
+// barrier -- two tiles of HBM latency hidden, one barrier per tile.
+// 0 = register staging (global_load -> VGPR during the tile, ds_write after;
+// 2 LDS buffers).
+template <int DP, int R, int METRIC, int STG>
 __global__ void __launch_bounds__(256)
-cand_kernel(const float* __restrict__ X32, const float* __restrict__ xinit,
-            const float* __restrict__ Q32, int n_tiles, int S, int n_qt,
-            float* __restrict__ out_v, int* __restrict__ out_i, int abl) {
-  // abl: timing-only ablations (results invalid): bit0 = no global staging
-  // loads after the first tile, bit1 = no selection epilogue.  0 in production.
-  constexpr int CPR = DP / 4;      // float4 chunks per row
-  constexpr int LS = DP + 4;       // LDS row stride in floats (16-B pad)
-  constexpr int TF = kTR * LS;     // floats per tile buffer
-  constexpr int NCH = kTR * CPR;   // float4 chunks per tile
+cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
+            int n_qt, float* __restrict__ out_v, int* __restrict__ out_i, int abl) {
+  // Q32 is deliberately not __restrict__: with it hipcc treats the query
+  // fragments as invariant and re-loads them inside the tile loop instead of
+  // keeping them in VGPRs (its waits would then also drain the LDS-DMA queue).
+  // abl: timing-only ablations (results invalid): bit0 = no staging loads
+  // after the first tiles, bit1 = no selection epilogue.  0 in production.
+  constexpr int RSF = DP + 4;               // row stride (floats), HBM and LDS
+  constexpr int TBY = kTR * RSF * 4;        // tile bytes
+  constexpr int NG = (TBY + 1023) / 1024;   // 1-KiB LDS-DMA pieces per tile
+  constexpr int NB = STG == 1 ? 3 : 2;      // LDS buffers
+  constexpr int BUFF = STG == 1 ? NG * 256 : kTR * RSF;  // floats per buffer
+  constexpr int NCH = kTR * RSF / 4;        // float4 chunks per tile (STG 0)
   constexpr int CPT = (NCH + 255) / 256;
-  __shared__ __attribute__((aligned(16))) float lds[2 * TF + 2 * kTR];
-  float* ldsn = lds + 2 * TF;
+  constexpr int SEED = METRIC == 1 ? DP + 1 : DP;  // seed float within a row
+  __shared__ __attribute__((aligned(16))) float lds[NB * BUFF];
 
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int split = bid / n_qt;
   const int qt = bid - split * n_qt;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int j = lane & 31, h = lane >> 5;
   const int64_t qg = (int64_t)qt * kQPB + wv * 32 + j;
   const float* qrow = Q32 + qg * DP;
@@ -350,10 +398,34 @@ cand_kernel(const float* __restrict__ X32, const float* __restrict__ xinit,
   // qh dims 16t+8h..16t+8h+7, float4 DP/16+t the same dims of ql.
   float4 qf[METRIC != 1 ? DP / 8 : 1];
   if constexpr (METRIC != 1) {
+    // Loaded with inline asm (loads + their vmcnt(0) in one statement): with
+    // ordinary loads hipcc places the vmcnt waits for these registers at
+    // their first MFMA use INSIDE the tile loop, where each executes every
+    // tile and -- counting all vector-memory ops -- drains the in-flight
+    // LDS-DMA pieces of the staging pipeline.
 #pragma unroll
-    for (int c = 0; c < DP / 8; ++c) {
-      const int off = METRIC == 0 ? 8 * c : (c < DP / 16 ? 8 * c : DP / 2 + 8 * (c - DP / 16));
-      qf[c] = *(const float4*)(qrow + off + 4 * h);
+    for (int c0 = 0; c0 < DP / 8; c0 += 4) {
+      const float* p[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int c = c0 + u < DP / 8 ? c0 + u : c0;
+        const int off = METRIC == 0 ? 8 * c : (c < DP / 16 ? 8 * c : DP / 2 + 8 * (c - DP / 16));
+        p[u] = qrow + off + 4 * h;
+      }
+      float4 v0, v1, v2, v3;
+      asm volatile(
+          "global_load_dwordx4 %0, %4, off\n\t"
+          "global_load_dwordx4 %1, %5, off\n\t"
+          "global_load_dwordx4 %2, %6, off\n\t"
+          "global_load_dwordx4 %3, %7, off\n\t"
+          "s_waitcnt vmcnt(0)"
+          : "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3)
+          : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3])
+          : "memory");
+      qf[c0] = v0;
+      if (c0 + 1 < DP / 8) qf[c0 + 1] = v1;
+      if (c0 + 2 < DP / 8) qf[c0 + 2] = v2;
+      if (c0 + 3 < DP / 8) qf[c0 + 3] = v3;
     }
   }
 
@@ -365,12 +437,22 @@ cand_kernel(const float* __restrict__ X32, const float* __restrict__ xinit,
 
   const int my_nt = split < n_tiles ? (n_tiles - split + S - 1) / S : 0;
 
-  // Staging registers: global -> VGPR issued before the tile's compute,
-  // VGPR -> LDS after it (named registers, no array: an array here is left
-  // as a scratch alloca by hipcc).
-  static_assert(CPT <= 8, "tile staging supports DP <= 256");
-  float4 st0, st1, st2, st3, st4, st5, st6, st7;
-  float4 stn = make_float4(0.f, 0.f, 0.f, 0.f);
+  // ---- staging primitives
+  // STG 1: this wave's LDS-DMA pieces i = wv, wv+4, ... of tile t -> buffer b.
+  // The last piece may read past the tile (and past the last row: the HBM
+  // allocation carries 1 KiB of slack); it lands in the buffer's tail.
+  constexpr int G_HI = (NG + 3) / 4, G_LO = NG / 4;
+#define KNN_ISSUE(t_, b_)                                                              \
+  do {                                                                                 \
+    const char* g_ = (const char*)Xr + (int64_t)(t_) * TBY + lane * 16;                \
+    const uint32_t l_ = lds_base + (uint32_t)((b_) * BUFF * 4);                        \
+    for (int i_ = wv; i_ < NG; i_ += 4) glds16(g_ + i_ * 1024, l_ + (uint32_t)(i_ * 1024)); \
+  } while (0)
+  // LDS byte address of the staging array (wave-uniform)
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)lds;
+  // STG 0: named staging registers (an array here is left as a scratch alloca)
+  static_assert(STG == 1 || CPT <= 9, "register staging supports DP <= 256");
+  float4 st0, st1, st2, st3, st4, st5, st6, st7, st8;
 #define KNN_LD1(i_, v_)                                                               \
   if constexpr (CPT > i_) {                                                           \
     const int c_ = tid + 256 * i_;                                                    \
@@ -379,50 +461,65 @@ cand_kernel(const float* __restrict__ X32, const float* __restrict__ xinit,
 #define KNN_ST1(i_, v_)                                                               \
   if constexpr (CPT > i_) {                                                           \
     const int c_ = tid + 256 * i_;                                                    \
-    if (NCH % 256 == 0 || c_ < NCH) {                                                 \
-      const int row_ = c_ / CPR, col_ = c_ - row_ * CPR;                              \
-      *(float4*)(base_ + row_ * LS + col_ * 4) = v_;                                  \
-    }                                                                                 \
+    if (NCH % 256 == 0 || c_ < NCH) *(float4*)(base_ + 4 * c_) = v_;                  \
   }
 #define KNN_LOAD_TILE(t_)                                                             \
   do {                                                                                \
-    const float4* src_ = (const float4*)(X32 + (int64_t)(t_) * kTR * DP);             \
-    KNN_LD1(0, st0) KNN_LD1(1, st1) KNN_LD1(2, st2) KNN_LD1(3, st3)                   \
-    KNN_LD1(4, st4) KNN_LD1(5, st5) KNN_LD1(6, st6) KNN_LD1(7, st7)                   \
-    if (tid < kTR / 4) stn = ((const float4*)(xinit + (int64_t)(t_) * kTR))[tid];    \
+    const float4* src_ = (const float4*)(Xr + (int64_t)(t_) * kTR * RSF);             \
+    KNN_LD1(0, st0) KNN_LD1(1, st1) KNN_LD1(2, st2) KNN_LD1(3, st3) KNN_LD1(4, st4)   \
+    KNN_LD1(5, st5) KNN_LD1(6, st6) KNN_LD1(7, st7) KNN_LD1(8, st8)                   \
   } while (0)
 #define KNN_STORE_TILE(buf_)                                                          \
   do {                                                                                \
-    float* base_ = lds + (buf_) * TF;                                                 \
-    KNN_ST1(0, st0) KNN_ST1(1, st1) KNN_ST1(2, st2) KNN_ST1(3, st3)                   \
-    KNN_ST1(4, st4) KNN_ST1(5, st5) KNN_ST1(6, st6) KNN_ST1(7, st7)                   \
-    if (tid < kTR / 4) *(float4*)(ldsn + (buf_) * kTR + 4 * tid) = stn;               \
+    float* base_ = lds + (buf_) * BUFF;                                               \
+    KNN_ST1(0, st0) KNN_ST1(1, st1) KNN_ST1(2, st2) KNN_ST1(3, st3) KNN_ST1(4, st4)   \
+    KNN_ST1(5, st5) KNN_ST1(6, st6) KNN_ST1(7, st7) KNN_ST1(8, st8)                   \
   } while (0)
 
-  if (my_nt > 0) {
-    KNN_LOAD_TILE(split);
-    KNN_STORE_TILE(0);
+  if constexpr (STG == 1) {
+    if (my_nt > 0) KNN_ISSUE(split, 0);
+    if (my_nt > 1) KNN_ISSUE(split + S, 1);
+  } else {
+    if (my_nt > 0) {
+      KNN_LOAD_TILE(split);
+      KNN_STORE_TILE(0);
+    }
+    __syncthreads();
   }
-  __syncthreads();
 
   for (int it = 0; it < my_nt; ++it) {
     const int t = split + it * S;
-    const bool more = it + 1 < my_nt;
-    if (more && !(abl & 1)) KNN_LOAD_TILE(t + S);  // in flight during this tile's compute
-    const float* base = lds + (it & 1) * TF;
-    const float* nb = ldsn + (it & 1) * kTR;
+    int cur;
+    if constexpr (STG == 1) {
+      // this wave's pieces of tile `it` have landed once at most the pieces
+      // of tile it+1 remain outstanding; the barrier then publishes all
+      // waves' pieces and retires every read of buffer (it-1)%3 before it is
+      // refilled with tile it+2.
+      // wait + barrier in ONE asm statement with a memory clobber, so no LDS
+      // read can be hoisted above the barrier (a bare s_barrier builtin does
+      // not order memory) and no vmcnt(0) drains the in-flight tiles.
+      if (it + 1 < my_nt) {
+        if (wv < NG % 4 || NG % 4 == 0)
+          asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" :: "n"(G_HI) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" :: "n"(G_LO) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (it + 2 < my_nt && !(abl & 1)) KNN_ISSUE(t + 2 * S, (it + 2) % 3);
+      cur = it % 3;
+    } else {
+      if (it + 1 < my_nt && !(abl & 1)) KNN_LOAD_TILE(t + S);  // in flight during compute
+      cur = it & 1;
+    }
+    const float* base = lds + cur * BUFF;
 
     f32x16 acc;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const float4 nv = *(const float4*)(nb + 8 * g + 4 * h);
-      acc[4 * g + 0] = nv.x;
-      acc[4 * g + 1] = nv.y;
-      acc[4 * g + 2] = nv.z;
-      acc[4 * g + 3] = nv.w;
-    }
+    for (int i = 0; i < 16; ++i) acc[i] = base[((i & 3) + 8 * (i >> 2) + 4 * h) * RSF + SEED];
     if constexpr (METRIC == 0) {
-      const float* arow = base + j * LS + 4 * h;
+      const float* arow = base + j * RSF + 4 * h;
 #pragma unroll
       for (int c = 0; c < DP / 8; ++c) {
         const float4 a = *(const float4*)(arow + 8 * c);
@@ -433,16 +530,16 @@ cand_kernel(const float* __restrict__ X32, const float* __restrict__ xinit,
       }
     } else if constexpr (METRIC == 2) {
       // bf16x3 split product on v_mfma_f32_32x32x16_bf16:
-      //   q.x ~= qh.xh + ql.xh + qh.xl   (train row in LDS = [xh | xl])
+      //   q.x ~= qh.xh + ql.xh + qh.xl   (train row payload = [xh | xl])
       // i.e. one bf16 GEMM with K = 3*DP; ~2^-16 relative product error,
       // 16x the f32 MFMA rate per instruction -> 5.3x per fp32-equivalent flop.
-      const float* arow = base + j * LS + 4 * h;
+      const float* arow = base + j * RSF + 4 * h;
 #pragma unroll
-      for (int t = 0; t < DP / 16; ++t) {
-        const bf16x8 ah = __builtin_bit_cast(bf16x8, *(const float4*)(arow + 8 * t));
-        const bf16x8 al = __builtin_bit_cast(bf16x8, *(const float4*)(arow + DP / 2 + 8 * t));
-        const bf16x8 bh = __builtin_bit_cast(bf16x8, qf[t]);
-        const bf16x8 bl = __builtin_bit_cast(bf16x8, qf[DP / 16 + t]);
+      for (int tt = 0; tt < DP / 16; ++tt) {
+        const bf16x8 ah = __builtin_bit_cast(bf16x8, *(const float4*)(arow + 8 * tt));
+        const bf16x8 al = __builtin_bit_cast(bf16x8, *(const float4*)(arow + DP / 2 + 8 * tt));
+        const bf16x8 bh = __builtin_bit_cast(bf16x8, qf[tt]);
+        const bf16x8 bl = __builtin_bit_cast(bf16x8, qf[DP / 16 + tt]);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
@@ -450,12 +547,12 @@ cand_kernel(const float* __restrict__ X32, const float* __restrict__ xinit,
     } else {
       // L1 on the VALU: lane's query against its 16 rows, dims in chunks of 4.
 #pragma unroll 2
-      for (int c = 0; c < CPR; ++c) {
+      for (int c = 0; c < DP / 4; ++c) {
         const float4 qv = *(const float4*)(qrow + 4 * c);
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int r = (i & 3) + 8 * (i >> 2) + 4 * h;
-          const float4 xv = *(const float4*)(base + r * LS + 4 * c);
+          const float4 xv = *(const float4*)(base + r * RSF + 4 * c);
           float a = acc[i];
           a = a + __builtin_fabsf(qv.x - xv.x);
           a = a + __builtin_fabsf(qv.y - xv.y);
@@ -469,11 +566,15 @@ cand_kernel(const float* __restrict__ X32, const float* __restrict__ xinit,
     if (!(abl & 2)) select_block<R>(acc, t * kTR, h, L, I, thr);
     else if (acc[0] == 1234.5f && acc[15] == 1234.5f) thr = acc[7];  // keep acc live
 
-    if (more) KNN_STORE_TILE((it + 1) & 1);
-    __syncthreads();
+    if constexpr (STG == 0) {
+      if (it + 1 < my_nt) KNN_STORE_TILE((it + 1) & 1);
+      __syncthreads();
+    }
   }
+  if constexpr (STG == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   write_lists<R>(out_v, out_i, qg, S, split, h, L, I);
+#undef KNN_ISSUE
 #undef KNN_LOAD_TILE
 #undef KNN_STORE_TILE
 #undef KNN_LD1
@@ -527,19 +628,19 @@ cand_stream_kernel(const float* __restrict__ X32, const float* __restrict__ xini
   do {                                                                                  \
     const int it_ = (st_) / nch, c_ = (st_) - it_ * nch;                                \
     const int t_ = split + it_ * S;                                                     \
-    const float* xs_ = X32 + (int64_t)t_ * TRS * DP + c_ * DC;                          \
+    const float* xs_ = X32 + (int64_t)t_ * TRS * (DP + 4) + c_ * DC;                    \
     const float* qs_ = qbase + c_ * DC;                                                 \
     int e_ = tid;                                                                       \
-    a0 = *(const float4*)(xs_ + (e_ / CPR) * DP + (e_ % CPR) * 4);                      \
+    a0 = *(const float4*)(xs_ + (e_ / CPR) * (DP + 4) + (e_ % CPR) * 4);                \
     b0 = *(const float4*)(qs_ + (e_ / CPR) * DP + (e_ % CPR) * 4);                      \
     e_ += 256;                                                                          \
-    a1 = *(const float4*)(xs_ + (e_ / CPR) * DP + (e_ % CPR) * 4);                      \
+    a1 = *(const float4*)(xs_ + (e_ / CPR) * (DP + 4) + (e_ % CPR) * 4);                \
     b1 = *(const float4*)(qs_ + (e_ / CPR) * DP + (e_ % CPR) * 4);                      \
     e_ += 256;                                                                          \
-    a2 = *(const float4*)(xs_ + (e_ / CPR) * DP + (e_ % CPR) * 4);                      \
+    a2 = *(const float4*)(xs_ + (e_ / CPR) * (DP + 4) + (e_ % CPR) * 4);                \
     b2 = *(const float4*)(qs_ + (e_ / CPR) * DP + (e_ % CPR) * 4);                      \
     e_ += 256;                                                                          \
-    a3 = *(const float4*)(xs_ + (e_ / CPR) * DP + (e_ % CPR) * 4);                      \
+    a3 = *(const float4*)(xs_ + (e_ / CPR) * (DP + 4) + (e_ % CPR) * 4);                \
     b3 = *(const float4*)(qs_ + (e_ / CPR) * DP + (e_ % CPR) * 4);                      \
     if (c_ == 0 && tid < TRS / 4) stn = ((const float4*)(xinit + (int64_t)t_ * TRS))[tid]; \
   } while (0)
@@ -670,9 +771,14 @@ static int occupancy_of(KernelT k) {
 
 template <int DP, int R, int METRIC>
 static void launch_res(const CandLaunch& c, hipStream_t s) {
-  hipLaunchKernelGGL((cand_kernel<DP, R, METRIC>), dim3((unsigned)(c.n_qt * c.S)), dim3(256), 0, s,
-                     c.X32, c.xinit, c.Q32, (int)(c.n_pad / kTR), c.S, c.n_qt, c.out_v, c.out_i,
-                     c.ablate);
+  if (c.staging == 0)
+    hipLaunchKernelGGL((cand_kernel<DP, R, METRIC, 0>), dim3((unsigned)(c.n_qt * c.S)), dim3(256),
+                       0, s, c.X32, c.Q32, (int)(c.n_pad / kTR), c.S, c.n_qt, c.out_v, c.out_i,
+                       c.ablate);
+  else
+    hipLaunchKernelGGL((cand_kernel<DP, R, METRIC, 1>), dim3((unsigned)(c.n_qt * c.S)), dim3(256),
+                       0, s, c.X32, c.Q32, (int)(c.n_pad / kTR), c.S, c.n_qt, c.out_v, c.out_i,
+                       c.ablate);
 }
 template <int R, int METRIC>
 static void launch_str(const CandLaunch& c, hipStream_t s) {
@@ -697,19 +803,21 @@ static void with_M(int M, F f) {
 }
 
 template <int DP>
-static int blocks_per_cu_res(int R, int metric) {
+static int blocks_per_cu_res(int R, int metric, int stg) {
   int out = 1;
   with_R(R, [&](auto Rc) {
     with_M(metric, [&](auto Mc) {
-      if constexpr (Mc.value != 2 || DP % 16 == 0)
-        out = occupancy_of(cand_kernel<DP, Rc.value, Mc.value>);
+      if constexpr (Mc.value != 2 || DP % 16 == 0) {
+        if (stg == 0) out = occupancy_of(cand_kernel<DP, Rc.value, Mc.value, 0>);
+        else out = occupancy_of(cand_kernel<DP, Rc.value, Mc.value, 1>);
+      }
     });
   });
   return out;
 }
 
-int cand_blocks_per_cu(int metric, int DP, int R) {
-#define KNN_CASE(v) if (DP == v) return blocks_per_cu_res<v>(R, metric);
+int cand_blocks_per_cu(int metric, int DP, int R, int stg) {
+#define KNN_CASE(v) if (DP == v) return blocks_per_cu_res<v>(R, metric, stg);
   KNN_DP_LIST(KNN_CASE)
 #undef KNN_CASE
   int out = 1;

@@ -152,7 +152,8 @@ int knn_set_precision(knn_ctx* ctx, int mode);
 int knn_last_candidate_path(knn_ctx* ctx);
 
 /* Tuning overrides for experiments (0 = automatic): "R" list entries per
- * lane (4, 8, 16), "S" train splits per query tile (1..64). */
+ * lane (4, 8, 16), "S" train splits per query tile (1..64), "staging"
+ * (1 = LDS-DMA pipeline, default; 0 = register staging). */
 int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value);
 
 /* Synchronise the context's stream. */
