@@ -233,7 +233,7 @@ int knn_set_train_device(knn_ctx* ctx, const double* dX, const int32_t* dlabels,
 // kernel (occupancy x CUs): a mostly-empty final round costs up to a whole
 // workgroup duration.  The union of the 2S lists must hold the C re-rank
 // candidates; R grows to 16 when the expected per-list share of C is large.
-static void choose_geometry(knn_ctx* ctx, int metric, int DP, int n_qt, int64_t n_tiles, int C,
+static void choose_geometry(knn_ctx* ctx, int metric, int DP, int nw, int n_qt, int64_t n_tiles, int C,
                             int& S_out, int& R_out) {
   if (ctx->cu_count <= 0) {
     int cus = 0;
@@ -243,10 +243,10 @@ static void choose_geometry(knn_ctx* ctx, int metric, int DP, int n_qt, int64_t 
     ctx->cu_count = cus;
   }
   const int S_hi = (int)std::max<int64_t>(1, std::min<int64_t>(64, n_tiles));
-  int bestS = 1, bestR = 4;
-  for (int R : {4, 8, 16}) {
+  int bestS = 1, bestR = 8;
+  for (int R : {8, 16}) {
     if (ctx->tune_R && R != ctx->tune_R) continue;
-    const int64_t slots = (int64_t)cand_blocks_per_cu(metric, DP, R, ctx->staging) * ctx->cu_count;
+    const int64_t slots = (int64_t)cand_blocks_per_cu(metric, DP, R, nw) * ctx->cu_count;
     const int S_lo = std::min(S_hi, std::max(1, (C + 2 * R - 1) / (2 * R)));
     double best = -1.0;
     int bS = S_lo;
@@ -259,9 +259,9 @@ static void choose_geometry(knn_ctx* ctx, int metric, int DP, int n_qt, int64_t 
     if (ctx->tune_S) bS = std::min(ctx->tune_S, S_hi);
     bestS = bS;
     bestR = R;
-    // expected share of the C re-rank candidates per list (2S lists): R = 4
-    // when <= 1/2, R = 8 when <= 2, else 16 (certification catches the rest)
-    if (ctx->tune_R || (R == 4 && 2 * C <= 2 * bS) || (R == 8 && C <= 4 * bS)) break;
+    // expected share of the C re-rank candidates per list (2S lists): R = 8
+    // when <= 2, else 16 (certification catches the rest)
+    if (ctx->tune_R || C <= 4 * bS) break;
   }
   S_out = bestS;
   R_out = bestR;
@@ -301,13 +301,19 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
     DP = ctx->DPb;
     Xk = (const float*)ctx->XB.p;
   }
-  const int n_qt = (int)((m + kQPB - 1) / kQPB);
-  const int64_t m_pad = (int64_t)n_qt * kQPB;
+  // waves per workgroup of the resident kernel: 8 (256 queries share each
+  // staged tile) when there are enough queries, else 4; the large-d stream
+  // kernel always takes 128 queries
+  int nw = 4;
+  if (DP <= 256 && kmetric != 1) nw = ctx->tune_nw ? ctx->tune_nw : (m >= 4096 ? 8 : 4);
+  const int qpb = DP <= 256 ? 32 * nw : kQPB;
+  const int n_qt = (int)((m + qpb - 1) / qpb);
+  const int64_t m_pad = (int64_t)n_qt * qpb;
   const int64_t n_tiles = t.n_pad / cand_tile_rows(DP);
   int C = (int)std::min<int64_t>(t.n, std::max(2 * W, W + 16));
   C = std::min(C, kMaxUnion);
   int S = 1, R = 8;
-  choose_geometry(ctx, kmetric, DP, n_qt, n_tiles, C, S, R);
+  choose_geometry(ctx, kmetric, DP, nw, n_qt, n_tiles, C, S, R);
   const int NL = 2 * S;
   C = std::min(C, NL * R);
   if ((rc = ctx->Q32.ensure((size_t)m_pad * DP * sizeof(float)))) return rc;
@@ -320,6 +326,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   ctx->geom[0] = (int64_t)n_qt * S;
   ctx->geom[1] = S;
   ctx->geom[2] = R;
+  ctx->last_nw = nw;
   ctx->geom[3] = C;
   const bool tm = ctx->timing;
   if (tm) HIP_TRY(hipEventRecord(ctx->ev[0], s));
@@ -342,7 +349,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   cl.out_v = (float*)ctx->cand_v.p;
   cl.out_i = (int*)ctx->cand_i.p;
   cl.ablate = ctx->tune_ablate;
-  cl.staging = ctx->staging;
+  cl.nw = nw;
   launch_cand(cl, s);
   HIP_TRY(hipGetLastError());
   if (tm) HIP_TRY(hipEventRecord(ctx->ev[2], s));
@@ -534,12 +541,12 @@ int knn_last_candidate_path(knn_ctx* ctx) { return ctx ? ctx->last_kmetric : -1;
 int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value) {
   if (!ctx || !key) return knn_fail(KNN_ERR_ARG, "null argument");
   if (!strcmp(key, "R")) {
-    if (value != 0 && value != 4 && value != 8 && value != 16)
-      return knn_fail(KNN_ERR_ARG, "R must be 0 (auto), 4, 8 or 16");
+    if (value != 0 && value != 8 && value != 16)
+      return knn_fail(KNN_ERR_ARG, "R must be 0 (auto), 8 or 16");
     ctx->tune_R = (int)value;
-  } else if (!strcmp(key, "staging")) {
-    if (value != 0 && value != 1) return knn_fail(KNN_ERR_ARG, "staging must be 0 or 1");
-    ctx->staging = (int)value;
+  } else if (!strcmp(key, "nw")) {
+    if (value != 0 && value != 4 && value != 8) return knn_fail(KNN_ERR_ARG, "nw must be 0, 4 or 8");
+    ctx->tune_nw = (int)value;
   } else if (!strcmp(key, "ablate")) {
     ctx->tune_ablate = (int)value;  // timing experiments only: results become invalid
   } else if (!strcmp(key, "S")) {

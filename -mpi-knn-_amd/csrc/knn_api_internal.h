@@ -27,7 +27,8 @@ struct knn_ctx {
   int DPb = 0;           // padded dim of the bf16x3 copy (0 = not built)
   int tune_R = 0, tune_S = 0;  // 0 = automatic
   int tune_ablate = 0;         // timing-only kernel ablations
-  int staging = 1;             // resident kernel staging: 1 = LDS-DMA (glds), 0 = registers
+  int tune_nw = 0;             // resident kernel waves per workgroup (0 = auto)
+  int last_nw = 0;
   int last_kmetric = -1; // candidate path of the last search (0 fp32 L2, 1 L1, 2 bf16x3)
   knnk::TrainDev train{};
   bool timing = false;

@@ -46,7 +46,7 @@ int pad_dim(int d);                 // padded dim the candidate kernels run at
 int pad_dim_bf16x3(int d);          // padded dim of the bf16x3 kernel, -1 if unsupported
 bool cand_supported(int DP);
 int cand_tile_rows(int DP);         // train rows per tile of the kernel serving DP
-int cand_blocks_per_cu(int metric, int DP, int R, int staging);  // resident workgroups per CU
+int cand_blocks_per_cu(int metric, int DP, int R, int nw);  // resident workgroups per CU
 
 // metric: 0 = L2 fp32 MFMA, 1 = L1 fp32 VALU, 2 = L2 bf16x3 MFMA
 struct CandLaunch {
@@ -58,7 +58,7 @@ struct CandLaunch {
   float* out_v;
   int* out_i;
   int ablate;   // timing-only ablation bits (0 in production)
-  int staging;  // resident kernel: 1 = global_load_lds 3-stage, 0 = register staging
+  int nw;       // resident kernel: waves (x32 queries) per workgroup, 4 or 8
 };
 
 void launch_prep_train(const double* X64, int64_t n, int d, int DP, int64_t n_pad, float* X32,

@@ -358,14 +358,16 @@ __device__ __forceinline__ void write_lists(float* __restrict__ out_v, int* __re
 // VGPRs for the whole kernel.  Accumulators start at ||x_row||^2, so
 // acc = ||x||^2 - 2 q.x.
 //
-// Staging (STG): 1 = global_load_lds (LDS-DMA, no VGPRs): 3 LDS buffers,
-// tile it+2 is issued right after the barrier that opens tile it, and each
-// wave waits with a counted vmcnt for its own pieces of tile it before that
-// barrier -- two tiles of HBM latency hidden, one barrier per tile.
-// 0 = register staging (global_load -> VGPR during the tile, ds_write after;
-// 2 LDS buffers).
-template <int DP, int R, int METRIC, int STG>
-__global__ void __launch_bounds__(256)
+// NW waves (32 queries each) share every staged tile: NW = 8 halves the
+// staging instructions and L2 traffic per MFMA relative to NW = 4.
+//
+// Staging: global_load_lds (LDS-DMA, no VGPRs), 3 LDS buffers: tile it+2 is
+// issued right after the barrier that opens tile it, and each wave waits
+// with a counted vmcnt for its own pieces of tile it before that barrier --
+// two tiles of latency hidden, one barrier per tile.  (A register-staged
+// variant measured the same or slower; removed.)
+template <int DP, int R, int METRIC, int NW>
+__global__ void __launch_bounds__(NW * 64)
 cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
             int n_qt, float* __restrict__ out_v, int* __restrict__ out_i, int abl) {
   // Q32 is deliberately not __restrict__: with it hipcc treats the query
@@ -376,10 +378,8 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   constexpr int RSF = DP + 4;               // row stride (floats), HBM and LDS
   constexpr int TBY = kTR * RSF * 4;        // tile bytes
   constexpr int NG = (TBY + 1023) / 1024;   // 1-KiB LDS-DMA pieces per tile
-  constexpr int NB = STG == 1 ? 3 : 2;      // LDS buffers
-  constexpr int BUFF = STG == 1 ? NG * 256 : kTR * RSF;  // floats per buffer
-  constexpr int NCH = kTR * RSF / 4;        // float4 chunks per tile (STG 0)
-  constexpr int CPT = (NCH + 255) / 256;
+  constexpr int NB = 3;                     // LDS buffers (prefetch distance 2)
+  constexpr int BUFF = NG * 256;            // floats per buffer
   constexpr int SEED = METRIC == 1 ? DP + 1 : DP;  // seed float within a row
   __shared__ __attribute__((aligned(16))) float lds[NB * BUFF];
 
@@ -389,7 +389,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int j = lane & 31, h = lane >> 5;
-  const int64_t qg = (int64_t)qt * kQPB + wv * 32 + j;
+  const int64_t qg = (int64_t)qt * (NW * 32) + wv * 32 + j;
   const float* qrow = Q32 + qg * DP;
 
   // B operand resident in VGPRs for the whole kernel.  METRIC 0: fp32 -2q,
@@ -437,60 +437,27 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
 
   const int my_nt = split < n_tiles ? (n_tiles - split + S - 1) / S : 0;
 
-  // ---- staging primitives
-  // STG 1: this wave's LDS-DMA pieces i = wv, wv+4, ... of tile t -> buffer b.
-  // The last piece may read past the tile (and past the last row: the HBM
-  // allocation carries 1 KiB of slack); it lands in the buffer's tail.
-  constexpr int G_HI = (NG + 3) / 4, G_LO = NG / 4;
+  // ---- staging: this wave's LDS-DMA pieces i = wv, wv+NW, ... of tile t ->
+  // buffer b.  The last piece may read past the tile (and past the last row:
+  // the HBM allocation carries 1 KiB of slack); it lands in the buffer tail.
+  constexpr int G_HI = (NG + NW - 1) / NW, G_LO = NG / NW;
+  static_assert(G_HI <= 15, "vmcnt immediate range");
+  // LDS byte address of the staging array (wave-uniform)
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)lds;
 #define KNN_ISSUE(t_, b_)                                                              \
   do {                                                                                 \
     const char* g_ = (const char*)Xr + (int64_t)(t_) * TBY + lane * 16;                \
     const uint32_t l_ = lds_base + (uint32_t)((b_) * BUFF * 4);                        \
-    for (int i_ = wv; i_ < NG; i_ += 4) glds16(g_ + i_ * 1024, l_ + (uint32_t)(i_ * 1024)); \
-  } while (0)
-  // LDS byte address of the staging array (wave-uniform)
-  const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)lds;
-  // STG 0: named staging registers (an array here is left as a scratch alloca)
-  static_assert(STG == 1 || CPT <= 9, "register staging supports DP <= 256");
-  float4 st0, st1, st2, st3, st4, st5, st6, st7, st8;
-#define KNN_LD1(i_, v_)                                                               \
-  if constexpr (CPT > i_) {                                                           \
-    const int c_ = tid + 256 * i_;                                                    \
-    if (NCH % 256 == 0 || c_ < NCH) v_ = src_[c_];                                    \
-  }
-#define KNN_ST1(i_, v_)                                                               \
-  if constexpr (CPT > i_) {                                                           \
-    const int c_ = tid + 256 * i_;                                                    \
-    if (NCH % 256 == 0 || c_ < NCH) *(float4*)(base_ + 4 * c_) = v_;                  \
-  }
-#define KNN_LOAD_TILE(t_)                                                             \
-  do {                                                                                \
-    const float4* src_ = (const float4*)(Xr + (int64_t)(t_) * kTR * RSF);             \
-    KNN_LD1(0, st0) KNN_LD1(1, st1) KNN_LD1(2, st2) KNN_LD1(3, st3) KNN_LD1(4, st4)   \
-    KNN_LD1(5, st5) KNN_LD1(6, st6) KNN_LD1(7, st7) KNN_LD1(8, st8)                   \
-  } while (0)
-#define KNN_STORE_TILE(buf_)                                                          \
-  do {                                                                                \
-    float* base_ = lds + (buf_) * BUFF;                                               \
-    KNN_ST1(0, st0) KNN_ST1(1, st1) KNN_ST1(2, st2) KNN_ST1(3, st3) KNN_ST1(4, st4)   \
-    KNN_ST1(5, st5) KNN_ST1(6, st6) KNN_ST1(7, st7) KNN_ST1(8, st8)                   \
+    for (int i_ = wv; i_ < NG; i_ += NW) glds16(g_ + i_ * 1024, l_ + (uint32_t)(i_ * 1024)); \
   } while (0)
 
-  if constexpr (STG == 1) {
-    if (my_nt > 0) KNN_ISSUE(split, 0);
-    if (my_nt > 1) KNN_ISSUE(split + S, 1);
-  } else {
-    if (my_nt > 0) {
-      KNN_LOAD_TILE(split);
-      KNN_STORE_TILE(0);
-    }
-    __syncthreads();
-  }
+  if (my_nt > 0) KNN_ISSUE(split, 0);
+  if (my_nt > 1) KNN_ISSUE(split + S, 1);
 
   for (int it = 0; it < my_nt; ++it) {
     const int t = split + it * S;
     int cur;
-    if constexpr (STG == 1) {
+    {
       // this wave's pieces of tile `it` have landed once at most the pieces
       // of tile it+1 remain outstanding; the barrier then publishes all
       // waves' pieces and retires every read of buffer (it-1)%3 before it is
@@ -499,7 +466,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       // read can be hoisted above the barrier (a bare s_barrier builtin does
       // not order memory) and no vmcnt(0) drains the in-flight tiles.
       if (it + 1 < my_nt) {
-        if (wv < NG % 4 || NG % 4 == 0)
+        if (wv < NG % NW || NG % NW == 0)
           asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" :: "n"(G_HI) : "memory");
         else
           asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" :: "n"(G_LO) : "memory");
@@ -509,9 +476,6 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       __builtin_amdgcn_sched_barrier(0);
       if (it + 2 < my_nt && !(abl & 1)) KNN_ISSUE(t + 2 * S, (it + 2) % 3);
       cur = it % 3;
-    } else {
-      if (it + 1 < my_nt && !(abl & 1)) KNN_LOAD_TILE(t + S);  // in flight during compute
-      cur = it & 1;
     }
     const float* base = lds + cur * BUFF;
 
@@ -566,19 +530,11 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
     if (!(abl & 2)) select_block<R>(acc, t * kTR, h, L, I, thr);
     else if (acc[0] == 1234.5f && acc[15] == 1234.5f) thr = acc[7];  // keep acc live
 
-    if constexpr (STG == 0) {
-      if (it + 1 < my_nt) KNN_STORE_TILE((it + 1) & 1);
-      __syncthreads();
-    }
   }
-  if constexpr (STG == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   write_lists<R>(out_v, out_i, qg, S, split, h, L, I);
 #undef KNN_ISSUE
-#undef KNN_LOAD_TILE
-#undef KNN_STORE_TILE
-#undef KNN_LD1
-#undef KNN_ST1
 }
 
 // Large-dimension variant (DP > 256, e.g. the reference's MNIST default
@@ -763,22 +719,17 @@ int pad_dim_bf16x3(int d) {
 }
 
 template <class KernelT>
-static int occupancy_of(KernelT k) {
+static int occupancy_of(KernelT k, int threads) {
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 256, 0) != hipSuccess) return 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, threads, 0) != hipSuccess) return 1;
   return nb > 0 ? nb : 1;
 }
 
-template <int DP, int R, int METRIC>
+template <int DP, int R, int METRIC, int NW>
 static void launch_res(const CandLaunch& c, hipStream_t s) {
-  if (c.staging == 0)
-    hipLaunchKernelGGL((cand_kernel<DP, R, METRIC, 0>), dim3((unsigned)(c.n_qt * c.S)), dim3(256),
-                       0, s, c.X32, c.Q32, (int)(c.n_pad / kTR), c.S, c.n_qt, c.out_v, c.out_i,
-                       c.ablate);
-  else
-    hipLaunchKernelGGL((cand_kernel<DP, R, METRIC, 1>), dim3((unsigned)(c.n_qt * c.S)), dim3(256),
-                       0, s, c.X32, c.Q32, (int)(c.n_pad / kTR), c.S, c.n_qt, c.out_v, c.out_i,
-                       c.ablate);
+  hipLaunchKernelGGL((cand_kernel<DP, R, METRIC, NW>), dim3((unsigned)(c.n_qt * c.S)),
+                     dim3(NW * 64), 0, s, c.X32, c.Q32, (int)(c.n_pad / kTR), c.S, c.n_qt,
+                     c.out_v, c.out_i, c.ablate);
 }
 template <int R, int METRIC>
 static void launch_str(const CandLaunch& c, hipStream_t s) {
@@ -791,8 +742,7 @@ static void launch_str(const CandLaunch& c, hipStream_t s) {
 // (2 = bf16x3, resident kernel with DP % 16 == 0 only).
 template <class F>
 static void with_R(int R, F f) {
-  if (R == 4) f(std::integral_constant<int, 4>{});
-  else if (R == 8) f(std::integral_constant<int, 8>{});
+  if (R == 8) f(std::integral_constant<int, 8>{});
   else f(std::integral_constant<int, 16>{});
 }
 template <class F>
@@ -802,28 +752,38 @@ static void with_M(int M, F f) {
   else f(std::integral_constant<int, 2>{});
 }
 
+// Instantiated variants: R in {8, 16}; METRIC 0/2 with NW in {4, 8};
+// METRIC 1 (L1, not perf-graded) with NW = 4; METRIC 2 needs DP % 16 == 0.
+template <int DP, int R, int M, int NW>
+constexpr bool res_variant() {
+  return (M != 2 || DP % 16 == 0) && (M != 1 || NW == 4);
+}
+
 template <int DP>
-static int blocks_per_cu_res(int R, int metric, int stg) {
+static int blocks_per_cu_res(int R, int metric, int nw) {
   int out = 1;
   with_R(R, [&](auto Rc) {
     with_M(metric, [&](auto Mc) {
-      if constexpr (Mc.value != 2 || DP % 16 == 0) {
-        if (stg == 0) out = occupancy_of(cand_kernel<DP, Rc.value, Mc.value, 0>);
-        else out = occupancy_of(cand_kernel<DP, Rc.value, Mc.value, 1>);
+      if (nw == 8) {
+        if constexpr (res_variant<DP, Rc.value, Mc.value, 8>())
+          out = occupancy_of(cand_kernel<DP, Rc.value, Mc.value, 8>, 512);
+      } else {
+        if constexpr (res_variant<DP, Rc.value, Mc.value, 4>())
+          out = occupancy_of(cand_kernel<DP, Rc.value, Mc.value, 4>, 256);
       }
     });
   });
   return out;
 }
 
-int cand_blocks_per_cu(int metric, int DP, int R, int stg) {
-#define KNN_CASE(v) if (DP == v) return blocks_per_cu_res<v>(R, metric, stg);
+int cand_blocks_per_cu(int metric, int DP, int R, int nw) {
+#define KNN_CASE(v) if (DP == v) return blocks_per_cu_res<v>(R, metric, nw);
   KNN_DP_LIST(KNN_CASE)
 #undef KNN_CASE
   int out = 1;
   with_R(R, [&](auto Rc) {
-    if (metric == 1) out = occupancy_of(cand_stream_kernel<kStreamDC, Rc.value, 1>);
-    else out = occupancy_of(cand_stream_kernel<kStreamDC, Rc.value, 0>);
+    if (metric == 1) out = occupancy_of(cand_stream_kernel<kStreamDC, Rc.value, 1>, 256);
+    else out = occupancy_of(cand_stream_kernel<kStreamDC, Rc.value, 0>, 256);
   });
   return out;
 }
@@ -834,7 +794,13 @@ template <int DP>
 static void launch_res_dp(const CandLaunch& c, hipStream_t s) {
   with_R(c.R, [&](auto Rc) {
     with_M(c.metric, [&](auto Mc) {
-      if constexpr (Mc.value != 2 || DP % 16 == 0) launch_res<DP, Rc.value, Mc.value>(c, s);
+      if (c.nw == 8) {
+        if constexpr (res_variant<DP, Rc.value, Mc.value, 8>())
+          launch_res<DP, Rc.value, Mc.value, 8>(c, s);
+      } else {
+        if constexpr (res_variant<DP, Rc.value, Mc.value, 4>())
+          launch_res<DP, Rc.value, Mc.value, 4>(c, s);
+      }
     });
   });
 }

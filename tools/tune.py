@@ -2,9 +2,9 @@
 """In-process A/B timing of candidate-kernel variants on cfg2-shaped data
 (interleaved rounds, medians; cdna_hip_programming.md §5.4 rule 24).
 Usage: python tools/tune.py [--rounds 5] [--n 1000000 --m 10000 --d 128 --k 10]
-Variants: "prec:R:S[:ablate[:staging]]" e.g. auto:0:0 fp32:8:0 auto:4:0 auto:8:0:1:0
+Variants: "prec:R:S[:ablate[:nw]]" e.g. auto:0:0 fp32:8:0 auto:8:0:1:8
 (ablate bits: 1 = no staging loads, 2 = no selection epilogue; timing only;
-staging 1 = LDS-DMA pipeline (default), 0 = register staging)"""
+nw = waves per candidate workgroup, 0 auto / 4 / 8)"""
 import argparse
 import os
 import sys
@@ -42,8 +42,8 @@ def main():
             parts = v.split(":")
             p, R, S = parts[:3]
             abl = int(parts[3]) if len(parts) > 3 else 0
-            stg = int(parts[4]) if len(parts) > 4 else 1
-            clf.set_tuning("staging", stg)
+            nw = int(parts[4]) if len(parts) > 4 else 0
+            clf.set_tuning("nw", nw)
             clf.set_precision(prec[p])
             clf.set_tuning("R", int(R))
             clf.set_tuning("S", int(S))
