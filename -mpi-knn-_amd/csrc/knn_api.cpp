@@ -248,14 +248,19 @@ static void choose_geometry(knn_ctx* ctx, int metric, int DP, int nw, int n_qt, 
     if (ctx->tune_R && R != ctx->tune_R) continue;
     const int64_t slots = (int64_t)cand_blocks_per_cu(metric, DP, R, nw) * ctx->cu_count;
     const int S_lo = std::min(S_hi, std::max(1, (C + 2 * R - 1) / (2 * R)));
-    double best = -1.0;
-    int bS = S_lo;
-    for (int S = S_lo; S <= S_hi; S++) {
+    auto eff_of = [&](int S) {
       const int64_t wg = (int64_t)n_qt * S;
       const int64_t rounds = (wg + slots - 1) / slots;
-      const double eff = (double)wg / (double)(rounds * slots);
-      if (eff > best + 1e-3) { best = eff; bS = S; }
-    }
+      return (double)wg / (double)(rounds * slots);
+    };
+    double best = -1.0;
+    for (int S = S_lo; S <= S_hi; S++) best = std::max(best, eff_of(S));
+    // smallest S within 2 % of the best fill: fewer, longer lists mean fewer
+    // list insertions per tile (the early, insertion-heavy part of each
+    // list's stream is paid once per list)
+    int bS = S_lo;
+    for (int S = S_lo; S <= S_hi; S++)
+      if (eff_of(S) >= best - 0.02) { bS = S; break; }
     if (ctx->tune_S) bS = std::min(ctx->tune_S, S_hi);
     bestS = bS;
     bestR = R;
