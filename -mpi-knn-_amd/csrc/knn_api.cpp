@@ -509,17 +509,18 @@ int knn_search_partial_device(knn_ctx* ctx, const double* dQ, int64_t m, int32_t
 
 int knn_merge_vote_device(knn_ctx* ctx, const double* d_dist, const int64_t* d_idx,
                           const int32_t* d_lab, int32_t parts, int64_t m, int32_t w, int32_t k,
-                          int32_t* d_labels, int64_t* d_out_idx, double* d_out_dist,
-                          int32_t* d_flags, void* stream) {
+                          int64_t q0, int64_t mq, int32_t* d_labels, int64_t* d_out_idx,
+                          double* d_out_dist, int32_t* d_flags, void* stream) {
   int rc;
   if ((rc = device_guard(ctx))) return rc;
   if (parts <= 0 || w <= 0 || k < 0 || k > w || (int64_t)parts * w > 4096)
     return knn_fail(KNN_ERR_ARG, "bad merge geometry (need 0 <= k <= w, parts*w <= 4096)");
+  if (q0 < 0 || mq < 0 || q0 + mq > m) return knn_fail(KNN_ERR_ARG, "query slice out of range");
   if (!d_labels) return knn_fail(KNN_ERR_ARG, "null labels output");
-  if (m == 0) return KNN_OK;
+  if (mq == 0) return KNN_OK;
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   launch_merge_vote_partials(d_dist, d_idx, d_lab, parts, m, w, k, d_labels, d_out_idx,
-                             d_out_dist, d_flags, s);
+                             d_out_dist, d_flags, s, q0, mq);
   HIP_TRY(hipGetLastError());
   return KNN_OK;
 }

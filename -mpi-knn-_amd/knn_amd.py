@@ -91,7 +91,8 @@ def lib():
         "knn_classify": ([P, P, i64, i32, i32, P, P, P, P], ctypes.c_int),
         "knn_classify_device": ([P, P, i64, i32, i32, P, P, P, P, P], ctypes.c_int),
         "knn_search_partial_device": ([P, P, i64, i32, i32, P, P, P, P], ctypes.c_int),
-        "knn_merge_vote_device": ([P, P, P, P, i32, i64, i32, i32, P, P, P, P, P], ctypes.c_int),
+        "knn_merge_vote_device": ([P, P, P, P, i32, i64, i32, i32, i64, i64, P, P, P, P, P],
+                                  ctypes.c_int),
         "knn_sync": ([P], ctypes.c_int),
         "knn_last_rescan_count": ([P], i64),
         "knn_group_create": ([ctypes.POINTER(P), ctypes.c_int, P, ctypes.c_int], ctypes.c_int),
@@ -193,10 +194,12 @@ class Classifier:
                                                d_idx, d_lab, stream))
 
     def merge_vote_device(self, d_dist, d_idx, d_lab, parts, m, w, k, d_labels, d_out_idx=None,
-                          d_out_dist=None, d_flags=None, stream=None):
+                          d_out_dist=None, d_flags=None, stream=None, q0=0, mq=None):
+        """k-way merge of [parts][m][w] lists + vote for queries [q0, q0+mq)."""
+        mq = m - q0 if mq is None else mq
         _check(lib().knn_merge_vote_device(self._h, d_dist, d_idx, d_lab, int(parts), m, int(w),
-                                           int(k), d_labels, d_out_idx, d_out_dist, d_flags,
-                                           stream))
+                                           int(k), int(q0), int(mq), d_labels, d_out_idx,
+                                           d_out_dist, d_flags, stream))
 
     def sync(self):
         _check(lib().knn_sync(self._h))

@@ -1,20 +1,23 @@
 #!/usr/bin/env python3
 """bench.py -- queries/sec of the KNN classify hot path on MI355X.
 
-Metric (BASELINE.json): queries/sec (node) + % of the fp32-MFMA roofline on
-configs[1] = 1M train x 10k queries, d=128, k=10 (L2), per GPU.  A step is
-one knn_classify_device call over the rank's 10k queries (fused fp32-MFMA
-distance + top-R candidate kernel, fp64 exact re-rank + certification +
-first-to-max vote, exact rescan of uncertified queries if any).  Inputs are
-synthetic (seeded Gaussian mixture, min-max normalised, fp64 like the
-reference's Data_train) and resident in HBM before timing starts.
+Metric (BASELINE.json): queries/sec (node) + % MFMA peak on configs[1] =
+1M train x 10k queries, d=128, k=10 (L2), per GPU.  A step is one
+knn_classify_device call over the rank's 10k queries: fused MFMA distance +
+top-R candidate kernel, fp64 exact re-rank + certification + first-to-max
+vote, exact rescan of uncertified queries if any.  Inputs are synthetic
+(seeded Gaussian mixture, min-max normalised, fp64 like the reference's
+Data_train) and resident in HBM before timing starts.
 
-Multi-GPU (query-sharded, north_star mode a): the train set is broadcast from
-rank 0 with torch.distributed (RCCL over xGMI) before timing; every rank
-classifies its own 10k queries (weak scaling, no data-path collective).
+Multi-GPU (--mode query, default; north_star mode a): the train set is
+broadcast from rank 0 with torch.distributed (RCCL over xGMI) before timing;
+every rank classifies its own 10k queries (weak scaling, no data-path
+collective).  --mode train (mode b, cfg4 shape: --n-train 100000000 --dim 96):
+rank r holds train rows [n r/W, n (r+1)/W); a step = local exact top-(k+1)
++ RCCL all-gather of the lists + k-way merge/vote of the rank's query slice.
 
 Run: python bench.py [--gpus N --steps K --warmup W]
-     (N>1 via python -m torch.distributed.run --nproc-per-node N bench.py ...)
+     (N>1: python -m torch.distributed.run --nproc-per-node N bench.py ...)
 """
 import argparse
 import importlib.util
@@ -28,8 +31,21 @@ import torch
 import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "-mpi-knn-_amd")
 PEAK_FP32_TFLOPS = 157.3   # MI355X dense fp32 MFMA (= vector) peak, MI355X_MICROARCH.md
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA peak (no sparsity), MI355X_MICROARCH.md
+METRIC = "queries/sec (node) + % MFMA peak, 1M train x 10k query d=128 k=10, 1/2/4/8 GPU"
+
+
+def _load(name):
+    spec = importlib.util.spec_from_file_location(name, os.path.join(PKG, name + ".py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def load_knn():
+    return _load("knn_amd")
 
 
 def pad_dim(d):
@@ -39,32 +55,33 @@ def pad_dim(d):
     return d
 
 
-def load_knn():
-    spec = importlib.util.spec_from_file_location(
-        "knn_amd", os.path.join(ROOT, "-mpi-knn-_amd", "knn_amd.py"))
-    mod = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(mod)
-    return mod
-
-
-def synth(n, m, d, classes, seed_train, seed_query, device):
-    """Gaussian mixture (class = cluster), min-max normalised over the train
-    rows like cpp:229-306 (queries clipped into the same scale), fp64."""
+def synth(n, m, d, classes, seed_train, seed_query, device, row0=0, n_total=None):
+    """Gaussian mixture (class = cluster), values scaled into [0,1] like the
+    reference's min-max normalisation (cpp:229-306), fp64.  Rows [row0,
+    row0+n) of a virtual n_total-row train set (train sharding), generated
+    in chunks so a 100M-row shard needs no temporaries of its size."""
     g = torch.Generator(device=device)
     g.manual_seed(seed_train)
     centres = torch.rand((classes, d), generator=g, device=device, dtype=torch.float64) * 4 - 2
-    lab = torch.randint(0, classes, (n,), generator=g, device=device, dtype=torch.int32)
-    X = centres[lab.long()] + torch.randn((n, d), generator=g, device=device, dtype=torch.float64)
+    lo, hi = -2.0 - 4.5, 2.0 + 4.5  # fixed scale (centres in [-2,2] + N(0,1) tails)
+    X = torch.empty((n, d), device=device, dtype=torch.float64)
+    lab = torch.empty(n, device=device, dtype=torch.int32)
+    chunk = 1 << 20
+    for c0 in range(0, n, chunk):
+        c1 = min(n, c0 + chunk)
+        gc = torch.Generator(device=device)
+        gc.manual_seed(seed_train * 1000003 + (row0 + c0) // chunk)
+        lc = torch.randint(0, classes, (c1 - c0,), generator=gc, device=device, dtype=torch.int32)
+        xc = centres[lc.long()] + torch.randn((c1 - c0, d), generator=gc, device=device,
+                                              dtype=torch.float64)
+        X[c0:c1] = ((xc - lo) / (hi - lo)).clamp_(0.0, 1.0)
+        lab[c0:c1] = lc
     gq = torch.Generator(device=device)
     gq.manual_seed(seed_query)
     qlab = torch.randint(0, classes, (m,), generator=gq, device=device, dtype=torch.int32)
     Q = centres[qlab.long()] + torch.randn((m, d), generator=gq, device=device, dtype=torch.float64)
-    mn = X.min(0).values
-    mx = X.max(0).values
-    rng = torch.where(mx - mn != 0, mx - mn, torch.ones_like(mx))
-    X = ((X - mn) / rng).contiguous()
-    Q = ((Q - mn) / rng).contiguous()
-    return X, lab.contiguous(), Q, qlab
+    Q = ((Q - lo) / (hi - lo)).clamp_(0.0, 1.0).contiguous()
+    return X, lab, Q, qlab
 
 
 def cpu_baseline(X, lab, Q, k, classes, gpu_labels, budget_s=12.0):
@@ -74,12 +91,9 @@ def cpu_baseline(X, lab, Q, k, classes, gpu_labels, budget_s=12.0):
     import oracle
     cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
     cores = max(1, min(cores, 16))
-    Xh = X.cpu().numpy()
-    lh = lab.cpu().numpy()
-    Qh = Q.cpu().numpy()
-    # calibrate: one query per thread
+    Xh, lh, Qh = X.cpu().numpy(), lab.cpu().numpy(), Q.cpu().numpy()
     t0 = time.perf_counter()
-    oracle.knn(Xh, lh, Qh[:cores], k, True, classes, nthreads=cores)
+    oracle.knn(Xh, lh, Qh[:cores], k, True, classes, nthreads=cores)  # calibrate
     per_round = time.perf_counter() - t0
     rounds = int(max(1, min(32, (budget_s - per_round) / max(per_round, 1e-6))))
     sample = min(Qh.shape[0], cores * rounds)
@@ -99,121 +113,161 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n-train", type=int, default=1_000_000)
-    ap.add_argument("--queries", type=int, default=10_000, help="queries per GPU")
+    ap.add_argument("--mode", choices=("query", "train"), default="query")
+    ap.add_argument("--n-train", type=int, default=1_000_000, help="train rows (whole job)")
+    ap.add_argument("--queries", type=int, default=10_000,
+                    help="queries per GPU (query mode) / in total (train mode)")
     ap.add_argument("--dim", type=int, default=128)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--classes", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fp32-path", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        args.gpus = world
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
-
+    kd = _load("knn_dist")
     knn = load_knn()
     n, m, d, k, C = args.n_train, args.queries, args.dim, args.k, args.classes
-
-    # train on rank 0, RCCL broadcast (≙ MPI_Bcast cpp:224-225); own queries per rank
-    X, lab, Q, qlab = synth(n, m, d, C, 1234, 5678 + rank, dev)
-    if world > 1:
-        dist.broadcast(X, 0)
-        dist.broadcast(lab, 0)
-    torch.cuda.synchronize()
-
-    clf = knn.Classifier(local)
-    clf.set_train_device(X.data_ptr(), lab.data_ptr(), n, d, C, keep=(X, lab))
-    clf.set_timing(True)
-    out_lab = torch.empty(m, dtype=torch.int32, device=dev)
-    out_flags = torch.empty(m, dtype=torch.int32, device=dev)
+    sync = torch.cuda.synchronize
     stream = torch.cuda.current_stream().cuda_stream
+    clf = knn.Classifier(local)
+    clf.set_timing(True)
 
-    def step():
-        clf.classify_device(Q.data_ptr(), m, k, knn.L2, out_lab.data_ptr(), None, None,
-                            out_flags.data_ptr(), stream)
+    if args.mode == "query":
+        # train generated on rank 0 and RCCL-broadcast (≙ MPI_Bcast cpp:224-225)
+        X, lab, Q, _ = synth(n, m, d, C, 1234, 5678 + rank, dev)
+        kd.broadcast_train(X, lab)
+        sync()
+        clf.set_train_device(X.data_ptr(), lab.data_ptr(), n, d, C, keep=(X, lab))
+        out_lab = torch.empty(m, dtype=torch.int32, device=dev)
+        out_flags = torch.empty(m, dtype=torch.int32, device=dev)
+        stats = {"cand": [], "rr": [], "resc": 0}
 
-    def timed(precision, steps, warmup):
-        """warmup + barrier/sync-bracketed timed steps; max over ranks."""
-        clf.set_precision(precision)
-        for _ in range(warmup):
-            step()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        cand_ms, rerank_ms, rescans = [], [], 0
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            step()
-            cand_ms.append(clf.last_phase_ms(knn.PHASE_CANDIDATE))
-            rerank_ms.append(clf.last_phase_ms(knn.PHASE_RERANK))
-            rescans += clf.last_rescan_count()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-        if world > 1:
-            dist.all_reduce(el, op=dist.ReduceOp.MAX)
-        return (float(el.item()), float(np.mean(cand_ms)) * 1e-3, float(np.mean(rerank_ms)),
-                rescans, clf.last_candidate_path(), clf.last_geometry())
+        def step():
+            clf.classify_device(Q.data_ptr(), m, k, knn.L2, out_lab.data_ptr(), None, None,
+                                out_flags.data_ptr(), stream)
+            stats["cand"].append(clf.last_phase_ms(knn.PHASE_CANDIDATE))
+            stats["rr"].append(clf.last_phase_ms(knn.PHASE_RERANK))
+            stats["resc"] += clf.last_rescan_count()
 
-    flops = 2.0 * n * d * m  # algorithmic, per launch (norm terms excluded)
-    # default path (bf16x3 candidate pass for d <= 256), the measured `value`
-    el, t_cand, rr_ms, rescans, path, geom = timed(knn.PRECISION_AUTO, args.steps, args.warmup)
-    labels_auto = out_lab.clone()
-    # fp32-MFMA candidate pass (the north star's roofline reference), same data
-    el32, t_cand32, rr32, resc32, path32, geom32 = timed(knn.PRECISION_FP32, max(3, args.steps // 2), 1)
-    same_labels = bool(torch.equal(labels_auto, out_lab))
-    total_q = m * world * args.steps
-    value = total_q / el
-    achieved = flops / t_cand / 1e12
-    achieved32 = flops / t_cand32 / 1e12
-    bf16 = path == 2
+        def run(precision, steps, warmup):
+            clf.set_precision(precision)
+            for key in ("cand", "rr"):
+                stats[key] = []
+            stats["resc"] = 0
+            el = kd.timed(step, steps, warmup, sync, dev)
+            cand = stats["cand"][warmup:]
+            return dict(el=el, t_cand=float(np.mean(cand)) * 1e-3,
+                        rr=float(np.mean(stats["rr"][warmup:])), resc=stats["resc"],
+                        path=clf.last_candidate_path(), geom=clf.last_geometry())
+
+        flops = 2.0 * n * d * m  # algorithmic, per launch per GPU (norm terms excluded)
+        main_r = run(knn.PRECISION_AUTO, args.steps, args.warmup)
+        labels_auto = out_lab.clone()
+        fp32_r = None
+        if not args.no_fp32_path:
+            fp32_r = run(knn.PRECISION_FP32, max(3, args.steps // 2), 1)
+        same = bool(torch.equal(labels_auto, out_lab))
+        total_q = m * world * args.steps
+        workload = ("cfg2: %d train x %d queries per GPU, d=%d, k=%d, L2, %d classes"
+                    % (n, m, d, k, C))
+        parallelism = "query-sharded dp%d" % world
+    else:
+        # train-sharded: this rank's rows only; the same queries on every rank
+        r0, r1 = kd.shard_range(n, world, rank)
+        X, lab, Q, _ = synth(r1 - r0, m, d, C, 1234, 5678, dev, row0=r0, n_total=n)
+        sync()
+        clf.set_train_device(X.data_ptr(), lab.data_ptr(), r1 - r0, d, C, idx_offset=r0,
+                             keep=(X, lab))
+        w = k + 1
+        pd_ = torch.empty((m, w), dtype=torch.float64, device=dev)
+        pi_ = torch.empty((m, w), dtype=torch.int64, device=dev)
+        pl_ = torch.empty((m, w), dtype=torch.int32, device=dev)
+        q0, q1 = kd.shard_range(m, world, rank)
+        out_lab = torch.empty(max(1, q1 - q0), dtype=torch.int32, device=dev)
+        stats = {"cand": [], "rr": [], "resc": 0}
+
+        def search_partial(Qt):
+            clf.search_partial_device(Qt.data_ptr(), m, w, knn.L2, pd_.data_ptr(), pi_.data_ptr(),
+                                      pl_.data_ptr(), stream)
+            stats["cand"].append(clf.last_phase_ms(knn.PHASE_CANDIDATE))
+            stats["rr"].append(clf.last_phase_ms(knn.PHASE_RERANK))
+            stats["resc"] += clf.last_rescan_count()
+            return pd_, pi_, pl_
+
+        def merge_vote(gd, gi, gl, parts, a, b):  # k-way merge + vote of this rank's slice
+            clf.merge_vote_device(gd.data_ptr(), gi.data_ptr(), gl.data_ptr(), parts, m, w, k,
+                                  out_lab.data_ptr(), stream=stream, q0=a, mq=b - a)
+            return out_lab
+
+        def step():
+            kd.train_sharded(search_partial, merge_vote, Q, m, w, k, dev)
+
+        def run(precision, steps, warmup):
+            clf.set_precision(precision)
+            for key in ("cand", "rr"):
+                stats[key] = []
+            stats["resc"] = 0
+            el = kd.timed(step, steps, warmup, sync, dev)
+            return dict(el=el, t_cand=float(np.mean(stats["cand"][warmup:])) * 1e-3,
+                        rr=float(np.mean(stats["rr"][warmup:])), resc=stats["resc"],
+                        path=clf.last_candidate_path(), geom=clf.last_geometry())
+
+        flops = 2.0 * (r1 - r0) * d * m
+        main_r = run(knn.PRECISION_AUTO, args.steps, args.warmup)
+        fp32_r, same = None, None
+        total_q = m * args.steps
+        workload = ("cfg4-shape: %d train (sharded) x %d queries, d=%d, k=%d, L2, %d classes"
+                    % (n, m, d, k, C))
+        parallelism = "train-sharded tp%d" % world
+
+    bf16 = main_r["path"] == 2
     peak = PEAK_BF16_TFLOPS if bf16 else PEAK_FP32_TFLOPS
-    mfma_mult = 3.0 if bf16 else 1.0  # MFMA flops per algorithmic flop
+    mfma_mult = 3.0 if bf16 else 1.0  # MFMA flops issued per algorithmic flop
+    achieved = flops / main_r["t_cand"] / 1e12
+    geom = main_r["geom"]
     result = {
-        "metric": "queries/sec (node) + % MFMA peak, 1M train x 10k query d=128 k=10, 1/2/4/8 GPU",
-        "value": value,
+        "metric": METRIC,
+        "value": total_q / main_r["el"],
         "unit": "queries/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": el / args.steps * 1e3,
+        "ms_per_step": main_r["el"] / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if args.mode == "query" else "strong",
         "vs_baseline": None,
         "dtype": "bf16x3" if bf16 else "fp32",
-        "data": "synthetic (seeded Gaussian mixture, min-max normalised, fp64 inputs)",
-        "config": {"workload": "cfg2: %d train x %d queries per GPU, d=%d, k=%d, L2, %d classes"
-                               % (n, m, d, k, C),
-                   "n_train": n, "queries_per_gpu": m, "dim": d, "k": k,
-                   "parallelism": "query-sharded dp%d" % world,
+        "data": "synthetic (seeded Gaussian mixture scaled to [0,1], fp64 inputs)",
+        "config": {"workload": workload, "n_train": n, "queries": m, "dim": d, "k": k,
+                   "parallelism": parallelism,
                    "candidate_pass": ("bf16x3 split (qh.xh+ql.xh+qh.xl) on MFMA 32x32x16 bf16"
                                       if bf16 else "fp32 MFMA 32x32x2") + " + fused top-R per lane",
                    "rerank": "fp64 exact (reference arithmetic), certified; labels exact",
-                   "geometry": geom, "rescanned_queries": rescans},
-        "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak,
-                     "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
-                     "kernel": "cand_kernel<%d,%d,%d>" % (pad_dim(d), geom["lists"], path),
-                     "kernel_ms": t_cand * 1e3, "rerank_ms": rr_ms,
+                   "geometry": geom, "rescanned_queries": main_r["resc"]},
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                     "frac": achieved / peak, "traffic": None,
+                     "kernel": "cand_kernel<%d,%d,%d>" % (pad_dim(d), geom["lists"], main_r["path"]),
+                     "kernel_ms": main_r["t_cand"] * 1e3, "rerank_ms": main_r["rr"],
                      "algorithmic_flops_per_launch": flops,
                      "mfma_flops_per_algorithmic_flop": mfma_mult,
                      "frac_of_issued_mfma": achieved * mfma_mult / peak},
-        "fp32_path": {"value": m * world * max(3, args.steps // 2) / el32, "unit": "queries/s",
-                      "kernel_ms": t_cand32 * 1e3, "achieved": achieved32,
-                      "peak": PEAK_FP32_TFLOPS, "frac": achieved32 / PEAK_FP32_TFLOPS,
-                      "rescanned_queries": resc32, "geometry": geom32,
-                      "labels_equal_default_path": same_labels},
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if fp32_r is not None:
+        a32 = flops / fp32_r["t_cand"] / 1e12
+        result["fp32_path"] = {
+            "value": m * world * max(3, args.steps // 2) / fp32_r["el"], "unit": "queries/s",
+            "kernel_ms": fp32_r["t_cand"] * 1e3, "achieved": a32, "peak": PEAK_FP32_TFLOPS,
+            "frac": a32 / PEAK_FP32_TFLOPS, "rescanned_queries": fp32_r["resc"],
+            "geometry": fp32_r["geom"], "labels_equal_default_path": same}
+    if rank == 0 and world == 1 and args.mode == "query" and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(X, lab, Q, k, C, labels_auto.cpu().numpy())
     if rank == 0:
         print(json.dumps(result), flush=True)

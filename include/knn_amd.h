@@ -116,12 +116,13 @@ int knn_search_partial_device(knn_ctx* ctx, const double* dQ, int64_t m, int32_t
                               int32_t* d_lab, void* stream);
 /* k-way merge of `parts` sorted lists per query, laid out [parts][m][w]
  * (the layout an all-gather of knn_search_partial outputs produces), then
- * the reference vote over the first k of the merged order.  Device pointers;
- * d_out_idx/d_out_dist/d_flags nullable. */
+ * the reference vote over the first k of the merged order, for queries
+ * [q0, q0+mq) (a rank's slice; q0=0, mq=m for all).  Outputs are indexed
+ * from 0 (row q-q0).  Device pointers; d_out_idx/d_out_dist/d_flags nullable. */
 int knn_merge_vote_device(knn_ctx* ctx, const double* d_dist, const int64_t* d_idx,
                           const int32_t* d_lab, int32_t parts, int64_t m, int32_t w, int32_t k,
-                          int32_t* d_labels, int64_t* d_out_idx, double* d_out_dist,
-                          int32_t* d_flags, void* stream);
+                          int64_t q0, int64_t mq, int32_t* d_labels, int64_t* d_out_idx,
+                          double* d_out_dist, int32_t* d_flags, void* stream);
 
 /* Per-phase device timing with HIP events recorded on the stream the
  * kernels run on (off by default).  Phases: 0 = query prep, 1 = candidate

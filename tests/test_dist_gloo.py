@@ -1,0 +1,102 @@
+"""world_size-2 gloo tests of the multi-process decomposition (knn_dist.py)
+on CPU, with the oracle as the per-rank compute: the N>1 paths of bench.py
+and of the train-sharded mode, without a GPU."""
+import importlib.util
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _load(name, path):
+    spec = importlib.util.spec_from_file_location(name, path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _data(n=3000, m=257, d=24, classes=5, seed=4):
+    rng = np.random.default_rng(seed)
+    centres = rng.uniform(-2, 2, (classes, d))
+    lab = rng.integers(0, classes, n + m).astype(np.int32)
+    X = np.round((centres[lab] + rng.standard_normal((n + m, d))) * 1024) / 1024
+    return X[:n].copy(), lab[:n].copy(), X[n:].copy()
+
+
+def _worker(rank, world, port, mode, out_path):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle
+    import dist_ref
+    kd = _load("knn_dist", os.path.join(ROOT, "-mpi-knn-_amd", "knn_dist.py"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    tr, lab, te = _data()
+    n, m, k = tr.shape[0], te.shape[0], 7
+    if mode == "query":
+        X = torch.from_numpy(tr) if rank == 0 else torch.zeros_like(torch.from_numpy(tr))
+        L = torch.from_numpy(lab) if rank == 0 else torch.zeros(n, dtype=torch.int32)
+        kd.broadcast_train(X, L)                       # ≙ MPI_Bcast cpp:224-225
+        q0, q1 = kd.shard_range(m, world, rank)        # ≙ MPI_Scatter cpp:226
+        got, _, _ = oracle.knn(X.numpy(), L.numpy(), te[q0:q1], k, True, 5, nthreads=2)
+        full = kd.gather_slices(torch.from_numpy(got), m)  # ≙ MPI_Gather cpp:383
+        el = kd.timed(lambda: None, 3, 1, lambda: None)
+        result = dict(labels=full.numpy(), el=np.array([el]))
+    else:
+        w = k + 1
+        r0, r1 = kd.shard_range(n, world, rank)
+
+        def search_partial(Q):
+            _, idx, dd = oracle.knn(tr[r0:r1], lab[r0:r1], Q, w, True, 5, n_out=w, nthreads=2)
+            gl = lab[r0:r1][idx]
+            return (torch.from_numpy(dd), torch.from_numpy(idx + r0), torch.from_numpy(gl))
+
+        def merge_vote(gd, gi, gl, parts, q0, q1):
+            labs, _, _ = dist_ref.merge_vote(gd.numpy(), gi.numpy(), gl.numpy(), k, q0, q1)
+            return torch.from_numpy(labs)
+
+        mine, (q0, q1) = kd.train_sharded(search_partial, merge_vote, te, m, w, k)
+        full = kd.gather_slices(mine, m)
+        result = dict(labels=full.numpy())
+    if rank == 0:
+        np.savez(out_path, **result)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["query", "train"])
+def test_two_rank_decomposition_matches_single_process(mode, tmp_path):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    out = str(tmp_path / "r.npz")
+    mp.spawn(_worker, args=(2, _free_port(), mode, out), nprocs=2, join=True)
+    tr, lab, te = _data()
+    want, _, _ = oracle.knn(tr, lab, te, 7, True, 5)
+    got = np.load(out)["labels"]
+    np.testing.assert_array_equal(got, want)
+
+
+def test_shard_ranges_cover_ragged():
+    kd = _load("knn_dist", os.path.join(ROOT, "-mpi-knn-_amd", "knn_dist.py"))
+    for n in (0, 1, 7, 10000, 10001):
+        for world in (1, 2, 3, 8):
+            spans = [kd.shard_range(n, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            assert max(b - a for a, b in spans) - min(b - a for a, b in spans) <= 1
