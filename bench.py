@@ -37,6 +37,15 @@ PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA peak (no sparsity), MI355X_M
 METRIC = "queries/sec (node) + % MFMA peak, 1M train x 10k query d=128 k=10, 1/2/4/8 GPU"
 
 
+def log(*a):
+    """Progress to stderr (the JSON result line is the only stdout output)."""
+    if int(os.environ.get("RANK", "0")) == 0:
+        print("[bench %.1fs]" % (time.perf_counter() - T0), *a, file=sys.stderr, flush=True)
+
+
+T0 = time.perf_counter()
+
+
 def _load(name):
     spec = importlib.util.spec_from_file_location(name, os.path.join(PKG, name + ".py"))
     mod = importlib.util.module_from_spec(spec)
@@ -144,6 +153,7 @@ def main():
         X, lab, Q, _ = synth(n, m, d, C, 1234, 5678 + rank, dev)
         kd.broadcast_train(X, lab)
         sync()
+        log("synthetic train ready: %d rows x %d" % (n, d))
         clf.set_train_device(X.data_ptr(), lab.data_ptr(), n, d, C, keep=(X, lab))
         out_lab = torch.empty(m, dtype=torch.int32, device=dev)
         out_flags = torch.empty(m, dtype=torch.int32, device=dev)
@@ -169,6 +179,7 @@ def main():
 
         flops = 2.0 * n * d * m  # algorithmic, per launch per GPU (norm terms excluded)
         main_r = run(knn.PRECISION_AUTO, args.steps, args.warmup)
+        log("default path done: %.3f ms/step" % (main_r["el"] / args.steps * 1e3))
         labels_auto = out_lab.clone()
         fp32_r = None
         if not args.no_fp32_path:
@@ -183,6 +194,7 @@ def main():
         r0, r1 = kd.shard_range(n, world, rank)
         X, lab, Q, _ = synth(r1 - r0, m, d, C, 1234, 5678, dev, row0=r0, n_total=n)
         sync()
+        log("synthetic shard ready: %d rows x %d" % (r1 - r0, d))
         clf.set_train_device(X.data_ptr(), lab.data_ptr(), r1 - r0, d, C, idx_offset=r0,
                              keep=(X, lab))
         w = k + 1
@@ -208,6 +220,8 @@ def main():
 
         def step():
             kd.train_sharded(search_partial, merge_vote, Q, m, w, k, dev)
+            log("train-sharded step: cand %.2f ms rerank %.2f ms rescans %d"
+                % (stats["cand"][-1], stats["rr"][-1], stats["resc"]))
 
         def run(precision, steps, warmup):
             clf.set_precision(precision)
@@ -268,6 +282,7 @@ def main():
             "frac": a32 / PEAK_FP32_TFLOPS, "rescanned_queries": fp32_r["resc"],
             "geometry": fp32_r["geom"], "labels_equal_default_path": same}
     if rank == 0 and world == 1 and args.mode == "query" and not args.no_cpu_baseline:
+        log("cpu baseline ...")
         result["cpu_baseline"] = cpu_baseline(X, lab, Q, k, C, labels_auto.cpu().numpy())
     if rank == 0:
         print(json.dumps(result), flush=True)

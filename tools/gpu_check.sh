@@ -5,7 +5,7 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 TAG=${TAG:-r1}
-stages="${*:-smoke tests bench}"
+if [ $# -eq 0 ]; then set -- smoke tests bench; fi
 step() {  # step <name> <limit-seconds> <cmd...>
   local name=$1 lim=$2; shift 2
   echo "== $name: $*"
@@ -16,7 +16,7 @@ step() {  # step <name> <limit-seconds> <cmd...>
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
   return 0
 }
-for s in $stages; do
+for s in "$@"; do
   case $s in
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) step tests 900 python -m pytest tests -m gpu -q -p no:cacheprovider -x ;;
