@@ -93,6 +93,26 @@ def synth(n, m, d, classes, seed_train, seed_query, device, row0=0, n_total=None
     return X, lab, Q, qlab
 
 
+def pmc_traffic(kernel, n, m, d, k):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC pass
+    (profiles/*_traffic_*.json, made by tools/traffic_json.py: 2*FETCH_SIZE +
+    WRITE_SIZE, KiB -> B) when it profiled this exact workload; else None.
+    Counters cannot be read from inside the timed process itself."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic_*.json")), reverse=True):
+        try:
+            rec = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        wl = rec.get("workload", {})
+        if (wl.get("n_train"), wl.get("queries"), wl.get("dim"), wl.get("k")) != (n, m, d, k):
+            continue
+        kr = rec.get("kernels", {}).get(kernel)
+        if kr:
+            return kr["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+    return None, None
+
+
 def cpu_baseline(X, lab, Q, k, classes, gpu_labels, budget_s=12.0):
     """Oracle (CPU restatement of the reference, bit-identical on the golden
     fixtures) on a bounded query sample using all host cores."""
@@ -177,6 +197,7 @@ def main():
                         rr=float(np.mean(stats["rr"][warmup:])), resc=stats["resc"],
                         path=clf.last_candidate_path(), geom=clf.last_geometry())
 
+        n_rank, m_rank = n, m
         flops = 2.0 * n * d * m  # algorithmic, per launch per GPU (norm terms excluded)
         main_r = run(knn.PRECISION_AUTO, args.steps, args.warmup)
         log("default path done: %.3f ms/step" % (main_r["el"] / args.steps * 1e3))
@@ -233,6 +254,7 @@ def main():
                         rr=float(np.mean(stats["rr"][warmup:])), resc=stats["resc"],
                         path=clf.last_candidate_path(), geom=clf.last_geometry())
 
+        n_rank, m_rank = r1 - r0, m
         flops = 2.0 * (r1 - r0) * d * m
         main_r = run(knn.PRECISION_AUTO, args.steps, args.warmup)
         fp32_r, same = None, None
@@ -246,6 +268,11 @@ def main():
     mfma_mult = 3.0 if bf16 else 1.0  # MFMA flops issued per algorithmic flop
     achieved = flops / main_r["t_cand"] / 1e12
     geom = main_r["geom"]
+    n_qt = max(1, geom["workgroups"] // max(1, geom["splits"]))
+    nw = 8 if -(-m_rank // n_qt) > 128 else 4  # waves per workgroup (32 queries each)
+    kname = ("cand_kernel<%d,%d,%d,%d>" % (pad_dim(d), geom["lists"], main_r["path"], nw)
+             if d <= 256 else "cand_stream_kernel<32,%d,%d>" % (geom["lists"], main_r["path"]))
+    traffic, traffic_src = pmc_traffic(kname, n_rank, m_rank, d, k)
     result = {
         "metric": METRIC,
         "value": total_q / main_r["el"],
@@ -266,8 +293,10 @@ def main():
                    "rerank": "fp64 exact (reference arithmetic), certified; labels exact",
                    "geometry": geom, "rescanned_queries": main_r["resc"]},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                     "frac": achieved / peak, "traffic": None,
-                     "kernel": "cand_kernel<%d,%d,%d>" % (pad_dim(d), geom["lists"], main_r["path"]),
+                     "frac": achieved / peak, "traffic": traffic,
+                     "traffic_unit": "bytes per launch (HBM, PMC)", "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_launch": (n_rank + m_rank) * d * 4 + m_rank * k * 8,
+                     "kernel": kname,
                      "kernel_ms": main_r["t_cand"] * 1e3, "rerank_ms": main_r["rr"],
                      "algorithmic_flops_per_launch": flops,
                      "mfma_flops_per_algorithmic_flop": mfma_mult,

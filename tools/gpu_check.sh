@@ -16,6 +16,7 @@ step() {  # step <name> <limit-seconds> <cmd...>
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
   return 0
 }
+nc=0
 for s in "$@"; do
   case $s in
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
@@ -42,6 +43,6 @@ for s in "$@"; do
         -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_sq_$TAG" -o run --output-format csv -- \
         python3 "$GRAFT_REPO_ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline ;;
     tune) step tune 600 python tools/tune.py ${TUNE_ARGS:-} ;;
-    *) step custom 600 bash -c "$s" ;;
+    *) nc=$((nc+1)); step custom$nc 600 bash -c "$s" ;;
   esac
 done
