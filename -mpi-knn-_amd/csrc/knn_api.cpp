@@ -96,6 +96,10 @@ int knn_create(knn_ctx** out, int device) {
     delete c;
     return knn_fail(KNN_ERR_DEVICE, "hipHostMalloc failed");
   }
+  if (hipDeviceGetAttribute(&c->cu_count, hipDeviceAttributeMultiprocessorCount, device) !=
+          hipSuccess ||
+      c->cu_count <= 0)
+    c->cu_count = 256;
   if (const char* e = getenv("KNN_PRECISION")) {
     if (!strcmp(e, "fp32")) c->precision = KNN_PRECISION_FP32;
     else if (!strcmp(e, "bf16x3")) c->precision = KNN_PRECISION_BF16X3;
@@ -235,13 +239,6 @@ int knn_set_train_device(knn_ctx* ctx, const double* dX, const int32_t* dlabels,
 // candidates; R grows to 16 when the expected per-list share of C is large.
 static void choose_geometry(knn_ctx* ctx, int metric, int DP, int nw, int n_qt, int64_t n_tiles, int C,
                             int& S_out, int& R_out) {
-  if (ctx->cu_count <= 0) {
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess ||
-        cus <= 0)
-      cus = 256;
-    ctx->cu_count = cus;
-  }
   const int S_hi = (int)std::max<int64_t>(1, std::min<int64_t>(64, n_tiles));
   int bestS = 1, bestR = 8;
   for (int R : {8, 16}) {
@@ -522,6 +519,75 @@ int knn_merge_vote_device(knn_ctx* ctx, const double* d_dist, const int64_t* d_i
   launch_merge_vote_partials(d_dist, d_idx, d_lab, parts, m, w, k, d_labels, d_out_idx,
                              d_out_dist, d_flags, s, q0, mq);
   HIP_TRY(hipGetLastError());
+  return KNN_OK;
+}
+
+int knn_minmax_device(knn_ctx* ctx, const double* d_X, int64_t rows, int32_t d, double* d_max,
+                      double* d_min, int32_t init, void* stream) {
+  int rc;
+  if ((rc = device_guard(ctx))) return rc;
+  if (rows < 0 || d <= 0 || (rows > 0 && !d_X) || !d_max || !d_min)
+    return knn_fail(KNN_ERR_ARG, "bad minmax arguments");
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  const int64_t R = minmax_rows_per_sweep(rows, d, ctx->cu_count);
+  if ((rc = ctx->nrm_part.ensure((size_t)2 * d * R * sizeof(double)))) return rc;
+  launch_minmax(d_X, rows, d, R, (double*)ctx->nrm_part.p, d_max, d_min, init, s);
+  HIP_TRY(hipGetLastError());
+  return KNN_OK;
+}
+
+int knn_normalize_device(knn_ctx* ctx, double* d_X, int64_t rows, int32_t d,
+                         const double* d_max, const double* d_min, void* stream) {
+  int rc;
+  if ((rc = device_guard(ctx))) return rc;
+  if (rows < 0 || d <= 0 || (rows > 0 && !d_X) || !d_max || !d_min)
+    return knn_fail(KNN_ERR_ARG, "bad normalize arguments");
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  launch_normalize_apply(d_X, rows, d, minmax_rows_per_sweep(rows, d, ctx->cu_count), d_max,
+                         d_min, s);
+  HIP_TRY(hipGetLastError());
+  return KNN_OK;
+}
+
+int knn_normalize(knn_ctx* ctx, double* const* sets, const int64_t* rows, int32_t nsets,
+                  int32_t d, double* out_max, double* out_min) {
+  int rc;
+  if ((rc = device_guard(ctx))) return rc;
+  if (nsets < 0 || d <= 0 || (nsets > 0 && (!sets || !rows)))
+    return knn_fail(KNN_ERR_ARG, "bad normalize arguments");
+  int64_t total = 0;
+  for (int i = 0; i < nsets; i++) {
+    if (rows[i] < 0 || (rows[i] > 0 && !sets[i])) return knn_fail(KNN_ERR_ARG, "bad set");
+    total += rows[i];
+  }
+  hipStream_t s = ctx->stream;
+  if ((rc = ctx->nrm_mm.ensure((size_t)2 * d * sizeof(double)))) return rc;
+  if ((rc = ctx->nrm_X.ensure((size_t)std::max<int64_t>(total, 1) * d * sizeof(double)))) return rc;
+  double* dmax = (double*)ctx->nrm_mm.p;
+  double* dmin = dmax + d;
+  double* dX = (double*)ctx->nrm_X.p;
+  int64_t off = 0;
+  for (int i = 0; i < nsets; i++) {  // cpp:245-274 over every set
+    double* di = dX + off * d;
+    if (rows[i] > 0)
+      HIP_TRY(hipMemcpyAsync(di, sets[i], (size_t)rows[i] * d * sizeof(double),
+                             hipMemcpyHostToDevice, s));
+    if ((rc = knn_minmax_device(ctx, di, rows[i], d, dmax, dmin, i == 0, s))) return rc;
+    off += rows[i];
+  }
+  if (nsets == 0 && (rc = knn_minmax_device(ctx, nullptr, 0, d, dmax, dmin, 1, s))) return rc;
+  off = 0;
+  for (int i = 0; i < nsets; i++) {  // cpp:279-305
+    double* di = dX + off * d;
+    if ((rc = knn_normalize_device(ctx, di, rows[i], d, dmax, dmin, s))) return rc;
+    if (rows[i] > 0)
+      HIP_TRY(hipMemcpyAsync(sets[i], di, (size_t)rows[i] * d * sizeof(double),
+                             hipMemcpyDeviceToHost, s));
+    off += rows[i];
+  }
+  if (out_max) HIP_TRY(hipMemcpyAsync(out_max, dmax, d * sizeof(double), hipMemcpyDeviceToHost, s));
+  if (out_min) HIP_TRY(hipMemcpyAsync(out_min, dmin, d * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
   return KNN_OK;
 }
 

@@ -41,10 +41,12 @@ struct knn_ctx {
   DevBuf Q64, Q32, cand_v, cand_i, rescan_q, rescan_cnt, ra_k, ra_i, rb_k, rb_i;
   // host-API outputs
   DevBuf o_lab, o_idx, o_dist, o_flags;
+  // normalisation: per-thread partial max/min, bounds, host-API staging
+  DevBuf nrm_part, nrm_mm, nrm_X;
   std::vector<DevBuf*> all_bufs() {
     return {&X64_own, &lab_own, &X32, &xl2, &xl1, &stats, &XB, &Q64, &Q32, &cand_v, &cand_i,
             &rescan_q, &rescan_cnt, &ra_k, &ra_i, &rb_k, &rb_i, &o_lab, &o_idx, &o_dist,
-            &o_flags};
+            &o_flags, &nrm_part, &nrm_mm, &nrm_X};
   }
 };
 

@@ -33,6 +33,7 @@ struct knn_group {
   std::vector<DevBuf> X, lab;                  // per-device train rows (full or shard)
   std::vector<DevBuf> Q, olab, oidx, odist, oflags;
   std::vector<DevBuf> pd, pi, pl, gd, gi, gl;  // train-sharded partial / gathered lists
+  std::vector<DevBuf> nX, nmm;                 // normalisation shards / per-dim bounds
   int64_t n = 0;
   int d = 0;
   int class_cnt = 0;
@@ -99,7 +100,7 @@ int knn_group_create(knn_group** out, int ndev, const int* devs, int mode) {
     }
   }
   for (auto* v : {&g->X, &g->lab, &g->Q, &g->olab, &g->oidx, &g->odist, &g->oflags, &g->pd,
-                  &g->pi, &g->pl, &g->gd, &g->gi, &g->gl})
+                  &g->pi, &g->pl, &g->gd, &g->gi, &g->gl, &g->nX, &g->nmm})
     v->resize(ndev);
   *out = g;
   return KNN_OK;
@@ -113,7 +114,7 @@ int knn_group_destroy(knn_group* g) {
       (void)hipDeviceSynchronize();
     }
     for (auto* v : {&g->X, &g->lab, &g->Q, &g->olab, &g->oidx, &g->odist, &g->oflags, &g->pd,
-                    &g->pi, &g->pl, &g->gd, &g->gi, &g->gl})
+                    &g->pi, &g->pl, &g->gd, &g->gi, &g->gl, &g->nX, &g->nmm})
       if (i < (int)v->size()) (*v)[i].release();
   }
   for (auto c : g->comms)
@@ -339,5 +340,73 @@ int knn_group_classify(knn_group* g, const double* Q, int64_t m, int32_t k, int3
 }
 
 double knn_group_last_compute_seconds(knn_group* g) { return g ? g->last_compute : -1.0; }
+
+int knn_group_normalize(knn_group* g, double* const* sets, const int64_t* rows, int32_t nsets,
+                        int32_t d) {
+  if (!g || nsets < 0 || d <= 0 || (nsets > 0 && (!sets || !rows)))
+    return knn_fail(KNN_ERR_ARG, "bad normalize arguments");
+  for (int s = 0; s < nsets; s++)
+    if (rows[s] < 0 || (rows[s] > 0 && !sets[s])) return knn_fail(KNN_ERR_ARG, "bad set");
+  const int G = g->ndev;
+  // shard s of device i: rows [rows[s]*i/G, rows[s]*(i+1)/G) (≙ the rank's
+  // batch_train / batch_test / batch_val rows, cpp:245-274)
+  auto shard = [&](int s, int i, int64_t& r0, int64_t& r1) {
+    r0 = rows[s] * i / G;
+    r1 = rows[s] * (i + 1) / G;
+  };
+  int rc = for_each_dev(g, [&](int i) {
+    int64_t total = 0, r0, r1;
+    for (int s = 0; s < nsets; s++) {
+      shard(s, i, r0, r1);
+      total += r1 - r0;
+    }
+    int e;
+    if ((e = g->nX[i].ensure((size_t)std::max<int64_t>(total, 1) * d * sizeof(double)))) return e;
+    if ((e = g->nmm[i].ensure((size_t)2 * d * sizeof(double)))) return e;
+    knn_ctx* c = g->ctx[i];
+    double* mx = (double*)g->nmm[i].p;
+    int64_t off = 0;
+    for (int s = 0; s < nsets; s++) {
+      shard(s, i, r0, r1);
+      double* dX = (double*)g->nX[i].p + off * d;
+      if (r1 > r0 && hipMemcpyAsync(dX, sets[s] + r0 * d, (size_t)(r1 - r0) * d * sizeof(double),
+                                    hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        return knn_fail(KNN_ERR_DEVICE, "H2D of normalisation shard failed");
+      if ((e = knn_minmax_device(c, dX, r1 - r0, d, mx, mx + d, s == 0, nullptr))) return e;
+      off += r1 - r0;
+    }
+    if (nsets == 0) return knn_minmax_device(c, nullptr, 0, d, mx, mx + d, 1, nullptr);
+    return KNN_OK;
+  });
+  if (rc) return rc;
+  if (G > 1) {  // ≙ MPI_Allreduce MAX / MIN, cpp:276-277
+    NCCL_G(ncclGroupStart());
+    for (int i = 0; i < G; i++) {
+      double* mx = (double*)g->nmm[i].p;
+      NCCL_G(ncclAllReduce(mx, mx, d, ncclFloat64, ncclMax, g->comms[i], g->ctx[i]->stream));
+      NCCL_G(ncclAllReduce(mx + d, mx + d, d, ncclFloat64, ncclMin, g->comms[i],
+                           g->ctx[i]->stream));
+    }
+    NCCL_G(ncclGroupEnd());
+  }
+  return for_each_dev(g, [&](int i) {  // cpp:279-305 on each shard, back to the host
+    knn_ctx* c = g->ctx[i];
+    const double* mx = (const double*)g->nmm[i].p;
+    int64_t off = 0, r0, r1;
+    for (int s = 0; s < nsets; s++) {
+      shard(s, i, r0, r1);
+      double* dX = (double*)g->nX[i].p + off * d;
+      int e;
+      if ((e = knn_normalize_device(c, dX, r1 - r0, d, mx, mx + d, nullptr))) return e;
+      if (r1 > r0 && hipMemcpyAsync(sets[s] + r0 * d, dX, (size_t)(r1 - r0) * d * sizeof(double),
+                                    hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+        return knn_fail(KNN_ERR_DEVICE, "D2H of normalised shard failed");
+      off += r1 - r0;
+    }
+    return hipStreamSynchronize(c->stream) == hipSuccess
+               ? KNN_OK
+               : knn_fail(KNN_ERR_DEVICE, "normalisation failed");
+  });
+}
 
 }  // extern "C"

@@ -86,4 +86,13 @@ void launch_prep_split(const double* X64, int64_t n, int d, int DP, int64_t n_pa
                        unsigned short* out, int row_shorts, const float* xl2, const float* xl1,
                        hipStream_t s);
 
+// Min-max normalisation (knn_normalize.hip, cpp:229-306).  R = rows per
+// grid sweep; `partial` holds 2*d*R doubles.  launch_minmax folds the set's
+// per-dim max/min into out_max/out_min (init: start from -1 / 999999).
+int64_t minmax_rows_per_sweep(int64_t rows, int d, int cu_count);
+void launch_minmax(const double* X, int64_t rows, int d, int64_t R, double* partial,
+                   double* out_max, double* out_min, int init, hipStream_t s);
+void launch_normalize_apply(double* X, int64_t rows, int d, int64_t R, const double* vmax,
+                            const double* vmin, hipStream_t s);
+
 }  // namespace knnk

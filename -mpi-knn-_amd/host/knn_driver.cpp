@@ -12,7 +12,7 @@
 //     label per line (cpp:390-392), "Running time is <t> second" (cpp:398)
 // Extra flags: --gpus N (default 1), --mode query|train (multi-GPU layout),
 // --strict (exit 1 unless N_* divisible by --gpus, as MPI_Abort cpp:127-129),
-// --threads T (CSV/normalisation threads), --output path.
+// --threads T (CSV parsing threads), --output path.
 // The timed region spans the same work as the reference (barrier to
 // barrier: CSV parsing, distribution, normalisation, both passes, output).
 #include <chrono>
@@ -96,50 +96,6 @@ int parse_args(int argc, char** argv, Config& c) {
   exit(1);  // ≙ MPI_Abort(MPI_COMM_WORLD, 1)
 }
 
-template <class F>
-void parallel_rows(int64_t n, int threads, F f) {
-  std::vector<std::thread> th;
-  for (int t = 0; t < threads; t++)
-    th.emplace_back([=] { f(n * t / threads, n * (t + 1) / threads, t); });
-  for (auto& x : th) x.join();
-}
-
-// cpp:229-306.  Per-dim max/min over train, test and validation rows with
-// the reference's initial values (max=-1, min=999999: a dim entirely below
-// -1 keeps max=-1, entirely above 999999 keeps min=999999), then
-// x = (x-min)/(max-min) on dims where max-min != 0.  min/max are exact, so
-// the parallel reduction order does not matter.
-void normalize(std::vector<double*> sets, std::vector<int64_t> rows, int dim, int threads) {
-  std::vector<double> mx(dim, -1.0), mn(dim, 999999.0);
-  for (size_t s = 0; s < sets.size(); s++) {
-    std::vector<std::vector<double>> tmx(threads, mx), tmn(threads, mn);
-    parallel_rows(rows[s], threads, [&](int64_t r0, int64_t r1, int t) {
-      double* a = sets[s];
-      for (int64_t i = r0; i < r1; i++)
-        for (int j = 0; j < dim; j++) {
-          const double data = a[i * dim + j];
-          if (data > tmx[t][j]) tmx[t][j] = data;
-          if (data < tmn[t][j]) tmn[t][j] = data;
-        }
-    });
-    for (int t = 0; t < threads; t++)
-      for (int j = 0; j < dim; j++) {
-        if (tmx[t][j] > mx[j]) mx[j] = tmx[t][j];
-        if (tmn[t][j] < mn[j]) mn[j] = tmn[t][j];
-      }
-  }
-  for (size_t s = 0; s < sets.size(); s++) {
-    parallel_rows(rows[s], threads, [&](int64_t r0, int64_t r1, int) {
-      double* a = sets[s];
-      for (int64_t i = r0; i < r1; i++)
-        for (int j = 0; j < dim; j++) {
-          const int64_t aim = i * dim + j;
-          if (mx[j] - mn[j] != 0) a[aim] = (a[aim] - mn[j]) / (mx[j] - mn[j]);
-        }
-    });
-  }
-}
-
 void load(const std::string& path, int dim, bool with_label, int64_t rows, std::vector<double>& X,
           std::vector<int32_t>* lab, int threads) {
   X.assign((size_t)rows * dim, 0.0);
@@ -177,11 +133,12 @@ int main(int argc, char** argv) {
   load(c.test_file, c.dim, false, c.N_test, Xte, nullptr, c.threads);
   if (c.Validation) load(c.validation_file, c.dim, true, c.N_val, Xva, &Lva, c.threads);
 
-  if (c.Normalize) {
+  if (c.Normalize) {  // cpp:229-306 on the GPUs: sharded min/max + RCCL all-reduce + apply
     std::vector<double*> sets{Xtr.data(), Xte.data()};
     std::vector<int64_t> rows{c.N_train, c.N_test};
     if (c.Validation) { sets.push_back(Xva.data()); rows.push_back(c.N_val); }
-    normalize(sets, rows, c.dim, c.threads);
+    if (knn_group_normalize(g, sets.data(), rows.data(), (int32_t)sets.size(), c.dim))
+      die(knn_last_error());
   }
 
   if (knn_group_set_train(g, Xtr.data(), Ltr.data(), c.N_train, c.dim, c.class_cnt))

@@ -30,6 +30,7 @@ EXPORTED = (
     "knn_group_create", "knn_group_destroy", "knn_group_set_train", "knn_group_classify",
     "knn_group_last_compute_seconds", "knn_set_timing", "knn_last_phase_ms",
     "knn_last_geometry", "knn_set_precision", "knn_last_candidate_path", "knn_set_tuning",
+    "knn_minmax_device", "knn_normalize_device", "knn_normalize", "knn_group_normalize",
 )
 PRECISION_AUTO, PRECISION_FP32, PRECISION_BF16X3 = 0, 1, 2
 PHASE_PREP, PHASE_CANDIDATE, PHASE_RERANK, PHASE_RESCAN = 0, 1, 2, 3
@@ -106,6 +107,10 @@ def lib():
         "knn_set_precision": ([P, ctypes.c_int], ctypes.c_int),
         "knn_last_candidate_path": ([P], ctypes.c_int),
         "knn_set_tuning": ([P, ctypes.c_char_p, i64], ctypes.c_int),
+        "knn_minmax_device": ([P, P, i64, i32, P, P, i32, P], ctypes.c_int),
+        "knn_normalize_device": ([P, P, i64, i32, P, P, P], ctypes.c_int),
+        "knn_normalize": ([P, P, P, i32, i32, P, P], ctypes.c_int),
+        "knn_group_normalize": ([P, P, P, i32, i32], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -126,6 +131,21 @@ def _ptr(a):
 
 def _f64(a):
     return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def _set_arrays(sets):
+    """Host sets (C-contiguous float64 [rows, d], normalised in place) ->
+    (pointer array, rows array, nsets, d)."""
+    sets = [s for s in sets if s is not None]
+    if not sets:
+        raise ValueError("no sets")
+    d = sets[0].shape[1]
+    for s in sets:
+        if s.dtype != np.float64 or not s.flags["C_CONTIGUOUS"] or s.ndim != 2 or s.shape[1] != d:
+            raise ValueError("sets must be C-contiguous float64 [rows, %d] arrays" % d)
+    ptrs = (ctypes.c_void_p * len(sets))(*[s.ctypes.data for s in sets])
+    rows = (ctypes.c_int64 * len(sets))(*[s.shape[0] for s in sets])
+    return ptrs, rows, len(sets), d
 
 
 class Classifier:
@@ -230,6 +250,23 @@ class Classifier:
         _check(lib().knn_last_geometry(self._h, out))
         return dict(workgroups=out[0], splits=out[1], lists=out[2], rerank=out[3])
 
+    def normalize(self, *sets):
+        """Min-max normalisation of host sets in place (cpp:229-306): e.g.
+        normalize(train, test, val).  Returns (max, min) per dimension."""
+        ptrs, rows, ns, d = _set_arrays(sets)
+        mx, mn = np.empty(d), np.empty(d)
+        _check(lib().knn_normalize(self._h, ptrs, rows, ns, d, _ptr(mx), _ptr(mn)))
+        return mx, mn
+
+    def minmax_device(self, dX_ptr, rows, d, d_max, d_min, init=True, stream=None):
+        """Fold a device set into per-dim bounds (init: start at -1/999999)."""
+        _check(lib().knn_minmax_device(self._h, dX_ptr, int(rows), int(d), d_max, d_min,
+                                       int(bool(init)), stream))
+
+    def normalize_device(self, dX_ptr, rows, d, d_max, d_min, stream=None):
+        _check(lib().knn_normalize_device(self._h, dX_ptr, int(rows), int(d), d_max, d_min,
+                                          stream))
+
 
 class Group:
     """Single-process multi-GPU classifier over RCCL (mode 0 query-sharded,
@@ -272,6 +309,12 @@ class Group:
 
     def last_compute_seconds(self):
         return float(lib().knn_group_last_compute_seconds(self._h))
+
+    def normalize(self, *sets):
+        """Sharded normalisation of host sets in place with an RCCL MAX/MIN
+        all-reduce of the bounds (cpp:229-306)."""
+        ptrs, rows, ns, d = _set_arrays(sets)
+        _check(lib().knn_group_normalize(self._h, ptrs, rows, ns, d))
 
 
 def run_reference_program(cfg: KnnConfig, workdir, gpus=1, mode="query", extra=()):

@@ -89,6 +89,25 @@ def _all_gather_stack(t):
     return torch.stack(out, 0)
 
 
+def normalize_sharded(local_sets, minmax, apply, d, device=None):
+    """Transductive min-max normalisation with the reference's decomposition
+    (cpp:229-306): minmax(set, mx, mn, init) folds this rank's rows of each
+    set into per-dim bounds (init: start from -1 / 999999, cpp:239-243), the
+    bounds are all-reduced MAX / MIN (≙ MPI_Allreduce cpp:276-277), then
+    apply(set, mx, mn) rewrites the local rows in place.  Returns (mx, mn)."""
+    world, _ = world_info()
+    mx = torch.full((d,), -1.0, dtype=torch.float64, device=device)
+    mn = torch.full((d,), 999999.0, dtype=torch.float64, device=device)
+    for i, s in enumerate(local_sets):
+        minmax(s, mx, mn, i == 0)
+    if world > 1:
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(mn, op=dist.ReduceOp.MIN)
+    for s in local_sets:
+        apply(s, mx, mn)
+    return mx, mn
+
+
 def train_sharded(search_partial, merge_vote, Q, m, w, k, device=None):
     """Mode b.  search_partial(Q) -> (dist f64[m,w], idx i64[m,w], lab i32[m,w])
     for this rank's train shard (global indices); merge_vote(d, i, l, parts,

@@ -124,6 +124,25 @@ int knn_merge_vote_device(knn_ctx* ctx, const double* d_dist, const int64_t* d_i
                           int64_t q0, int64_t mq, int32_t* d_labels, int64_t* d_out_idx,
                           double* d_out_dist, int32_t* d_flags, void* stream);
 
+/* ---- min-max normalisation (replaces cpp:229-306, bit-exact in fp64) -----
+ * Transductive, like the reference: per-dimension max/min over the train
+ * rows AND every query set, starting from max = -1 / min = 999999
+ * (cpp:239-243, strict compares), then x = (x - min)/(max - min) on the
+ * dimensions where max - min != 0.
+ * knn_minmax_device folds one device set [rows x d] (fp64, row-major) into
+ *   d_max/d_min (device, d doubles each); init != 0 starts from -1/999999
+ *   (the first set), 0 folds into the current values (later sets, or the
+ *   result of an all-reduce over ranks, ≙ MPI_Allreduce cpp:276-277).
+ * knn_normalize_device applies the bounds to a device set in place.
+ * knn_normalize runs both on host sets in place (sets[i] has rows[i] rows;
+ *   e.g. {train, test, val}); out_max/out_min (nullable) receive the bounds. */
+int knn_minmax_device(knn_ctx* ctx, const double* d_X, int64_t rows, int32_t d, double* d_max,
+                      double* d_min, int32_t init, void* stream);
+int knn_normalize_device(knn_ctx* ctx, double* d_X, int64_t rows, int32_t d,
+                         const double* d_max, const double* d_min, void* stream);
+int knn_normalize(knn_ctx* ctx, double* const* sets, const int64_t* rows, int32_t nsets,
+                  int32_t d, double* out_max, double* out_min);
+
 /* Per-phase device timing with HIP events recorded on the stream the
  * kernels run on (off by default).  Phases: 0 = query prep, 1 = candidate
  * kernel (fused MFMA distance + top-R), 2 = merge/re-rank/vote, 3 = exact
@@ -182,6 +201,12 @@ int knn_group_classify(knn_group* g, const double* Q, int64_t m, int32_t k, int3
 /* Seconds of the last group classify spent between the first enqueue and
  * the last device completion (device-resident inputs, excludes H2D/D2H). */
 double knn_group_last_compute_seconds(knn_group* g);
+/* Normalisation over the group (cpp:229-306 with the reference's own
+ * decomposition): GPU g takes rows [r*g/G, r*(g+1)/G) of every host set,
+ * reduces its max/min, ncclAllReduce MAX/MIN combines them (≙ MPI_Allreduce
+ * cpp:276-277), and each GPU rewrites its rows in place. */
+int knn_group_normalize(knn_group* g, double* const* sets, const int64_t* rows, int32_t nsets,
+                        int32_t d);
 
 #ifdef __cplusplus
 }

@@ -31,3 +31,24 @@ def merge_vote(gd, gi, gl, k, q0, q1):
         idxs.append([e[1] for e in top])
         dists.append([e[0] for e in top])
     return np.array(labs, np.int32), np.array(idxs, np.int64), np.array(dists, np.float64)
+
+
+def minmax_fold(X, mx, mn, init):
+    """Per-rank statistics of cpp:245-274 on a torch CPU shard (the caller
+    starts mx/mn at -1/999999): strict compares, NaN never wins."""
+    if X.shape[0] == 0:
+        return
+    a = X.numpy()
+    colmax = np.where(np.isnan(a), -np.inf, a).max(0)
+    colmin = np.where(np.isnan(a), np.inf, a).min(0)
+    m, n = mx.numpy(), mn.numpy()
+    np.copyto(m, np.where(colmax > m, colmax, m))
+    np.copyto(n, np.where(colmin < n, colmin, n))
+
+
+def minmax_apply(X, mx, mn):
+    """cpp:279-305: (x - min)/(max - min) where max - min != 0."""
+    a, m, n = X.numpy(), mx.numpy(), mn.numpy()
+    r = m - n
+    keep = r != 0
+    a[:, keep] = (a[:, keep] - n[keep]) / r[keep]

@@ -48,7 +48,18 @@ def _worker(rank, world, port, mode, out_path):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     tr, lab, te = _data()
     n, m, k = tr.shape[0], te.shape[0], 7
-    if mode == "query":
+    if mode == "normalize":
+        # each rank its row shard of train / test (≙ batch_train / batch_test)
+        va = te[::3].copy()
+        shards = []
+        for a in (tr, te, va):
+            r0, r1 = kd.shard_range(a.shape[0], world, rank)
+            shards.append(torch.from_numpy(a[r0:r1].copy()))
+        mx, mn = kd.normalize_sharded(shards, dist_ref.minmax_fold, dist_ref.minmax_apply,
+                                      tr.shape[1])
+        full = [kd.gather_slices(s, a.shape[0]).numpy() for s, a in zip(shards, (tr, te, va))]
+        result = dict(tr=full[0], te=full[1], va=full[2], mx=mx.numpy(), mn=mn.numpy())
+    elif mode == "query":
         X = torch.from_numpy(tr) if rank == 0 else torch.zeros_like(torch.from_numpy(tr))
         L = torch.from_numpy(lab) if rank == 0 else torch.zeros(n, dtype=torch.int32)
         kd.broadcast_train(X, L)                       # ≙ MPI_Bcast cpp:224-225
@@ -77,6 +88,20 @@ def _worker(rank, world, port, mode, out_path):
         np.savez(out_path, **result)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def test_two_rank_normalisation_matches_oracle(tmp_path):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    out = str(tmp_path / "n.npz")
+    mp.spawn(_worker, args=(2, _free_port(), "normalize", out), nprocs=2, join=True)
+    tr, _, te = _data()
+    va = te[::3].copy()
+    oracle.normalize(tr, te, va)
+    got = np.load(out)
+    for name, want in (("tr", tr), ("te", te), ("va", va)):
+        assert got[name].tobytes() == want.tobytes(), name
 
 
 @pytest.mark.parametrize("mode", ["query", "train"])
