@@ -45,9 +45,10 @@ def _sets(n, m, v, d, seed, special=True):
         X[:, 1] = rng.uniform(-9, -2, n + m + v)     # all below -1: max stays -1
         X[:, 2] = rng.uniform(1.5e6, 2e6, n + m + v)  # all above 999999: min stays 999999
         X[:, 3] = np.round(X[:, 3])                  # integer-valued, ties
-        X[5, 4] = np.inf                             # range inf -> values nan / 0
-        X[7, 5] = -np.inf
-        X[11, 6] = np.nan                            # NaN never wins a compare
+        N = n + m + v                                # tiny sets: wrap the special rows
+        X[5 % N, 4] = np.inf                         # range inf -> values nan / 0
+        X[7 % N, 5] = -np.inf
+        X[11 % N, 6] = np.nan                        # NaN never wins a compare
         X[:, 7] = 0.0                                # zero-range zeros
     return X[:n].copy(), X[n:n + m].copy(), X[n + m:].copy()
 
