@@ -4,7 +4,7 @@
 // train set lives in HBM in two forms: the caller's fp64 rows (exact
 // re-rank, ≙ Data_train cpp:140) and a padded fp32 copy + per-row seeds for
 // the MFMA candidate pass.  Queries are classified by the pipeline in
-// knn_kernels.hip; there is no host compute path.
+// knn_cand.hip / knn_select.hip; there is no host compute path.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -175,9 +175,19 @@ static int ensure_bf16x3(knn_ctx* ctx, hipStream_t s) {
   if (DPb <= 0) return knn_fail(KNN_ERR_ARG, "bf16x3 path supports d <= 256");
   if (ctx->DPb == DPb) return KNN_OK;
   int rc;
-  if ((rc = ctx->XB.ensure((size_t)t.n_pad * (DPb + 4) * sizeof(float) + 1024))) return rc;
-  launch_prep_split(t.X64, t.n, t.d, DPb, t.n_pad, 1.0, (unsigned short*)ctx->XB.p, 2 * (DPb + 4),
-                    t.xinit_l2, t.xinit_l1, s);
+  if (bf16x3_streamed(DPb)) {
+    // S3 stream kernel: tile-chunk images (4 B per dim: hi + lo) + seeds,
+    // rows padded to whole 256-row tiles
+    const int64_t n3 = (t.n + kS3Rows - 1) / kS3Rows * kS3Rows;
+    if ((rc = ctx->XB.ensure((size_t)n3 * DPb * 4))) return rc;
+    if ((rc = ctx->XS.ensure((size_t)n3 * sizeof(float)))) return rc;
+    launch_prep_split_tiled(t.X64, t.n, t.d, DPb, n3, 1.0, (unsigned short*)ctx->XB.p, t.xinit_l2,
+                            (float*)ctx->XS.p, s);
+  } else {
+    if ((rc = ctx->XB.ensure((size_t)t.n_pad * (DPb + 4) * sizeof(float) + 1024))) return rc;
+    launch_prep_split(t.X64, t.n, t.d, DPb, t.n_pad, 1.0, (unsigned short*)ctx->XB.p,
+                      2 * (DPb + 4), t.xinit_l2, t.xinit_l1, s);
+  }
   HIP_TRY(hipGetLastError());
   ctx->DPb = DPb;
   return KNN_OK;
@@ -304,14 +314,17 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
     Xk = (const float*)ctx->XB.p;
   }
   // waves per workgroup of the resident kernel: 8 (256 queries share each
-  // staged tile) when there are enough queries, else 4; the large-d stream
-  // kernel always takes 128 queries
+  // staged tile) when there are enough queries, else 4; the large-d fp32
+  // stream kernel always takes 128 queries, the bf16x3 one (S3) 256
+  const bool s3 = kmetric == 2 && bf16x3_streamed(DP);
   int nw = 4;
   if (DP <= 256 && kmetric != 1) nw = ctx->tune_nw ? ctx->tune_nw : (m >= 4096 ? 8 : 4);
-  const int qpb = DP <= 256 ? 32 * nw : kQPB;
+  if (s3) nw = 8;
+  const int qpb = s3 ? kS3Rows : (DP <= 256 ? 32 * nw : kQPB);
   const int n_qt = (int)((m + qpb - 1) / qpb);
   const int64_t m_pad = (int64_t)n_qt * qpb;
-  const int64_t n_tiles = t.n_pad / cand_tile_rows(DP);
+  const int64_t n_pad3 = (t.n + kS3Rows - 1) / kS3Rows * kS3Rows;
+  const int64_t n_tiles = s3 ? n_pad3 / kS3Rows : t.n_pad / cand_tile_rows(DP);
   int C = (int)std::min<int64_t>(t.n, std::max(2 * W, W + 16));
   C = std::min(C, kMaxUnion);
   int S = 1, R = 8;
@@ -332,7 +345,10 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   ctx->geom[3] = C;
   const bool tm = ctx->timing;
   if (tm) HIP_TRY(hipEventRecord(ctx->ev[0], s));
-  if (kmetric == 2)
+  if (s3)
+    launch_prep_split_tiled(dQ, m, t.d, DP, m_pad, -2.0, (unsigned short*)ctx->Q32.p, nullptr,
+                            nullptr, s);
+  else if (kmetric == 2)
     launch_prep_split(dQ, m, t.d, DP, m_pad, -2.0, (unsigned short*)ctx->Q32.p, 2 * DP, nullptr,
                       nullptr, s);
   else
@@ -352,7 +368,12 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   cl.out_i = (int*)ctx->cand_i.p;
   cl.ablate = ctx->tune_ablate;
   cl.nw = nw;
-  launch_cand(cl, s);
+  if (s3)
+    launch_cand_s3((const unsigned short*)ctx->XB.p, (const float*)ctx->XS.p,
+                   (const unsigned short*)ctx->Q32.p, DP, n_pad3, R, S, n_qt, cl.out_v, cl.out_i,
+                   cl.ablate, s);
+  else
+    launch_cand(cl, s);
   HIP_TRY(hipGetLastError());
   if (tm) HIP_TRY(hipEventRecord(ctx->ev[2], s));
   HIP_TRY(hipMemsetAsync(ctx->rescan_cnt.p, 0, sizeof(int), s));

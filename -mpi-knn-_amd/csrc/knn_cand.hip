@@ -1,0 +1,408 @@
+// knn_cand.hip -- MI355X (gfx950, CDNA4) candidate kernels of the KNN classify path.
+//
+// Pipeline per classify call (reference loop: cpp:308-381):
+//   1. prep_queries      fp64 queries -> fp32 (x -2 for L2) MFMA operands
+//   2. cand_kernel       fused distance + per-lane top-R selection.
+//        L2: -2 q.x^T on v_mfma_f32_32x32x2_f32 with the accumulator seeded by
+//            ||x||^2, so the chain ends at ||x||^2 - 2 q.x (the rank-equivalent
+//            of ||q - x||^2 for a fixed query; cpp:33-50).
+//        L1: sum |q - x| on the VALU (cpp:51-67; no GEMM identity exists).
+//        The distance matrix is never materialised: each lane keeps a sorted
+//        register list of its R best rows and a threshold filter.
+//   3. merge_rerank      per query: union of all lists -> best C by the fp32
+//        proxy -> exact fp64 reference distances for those C (sequential sum,
+//        no FMA, correctly rounded sqrt) -> sort by (dist, idx) -> certify
+//        that no excluded row can enter the top-w (rigorous fp32 error
+//        bound) -> first-to-max vote (cpp:324-337) or partial list output.
+//   4. rescan (rare)     queries that fail certification get an exact fp64
+//        scan over every row (chunked sort + tree reduce).
+// The result is the reference's fp64 top-k with ties ordered by train index.
+//
+// This TU: the large-d fp32 stream kernel, the bf16x3 large-d S3 kernel and
+// the dispatch over all candidate kernels (the register-resident kernel is
+// instantiated in knn_cand_res.hip, one object per group of dimensions).
+#include "knn_device.h"
+
+namespace knnk {
+
+#define KNN_DECL(v)                                          \
+  void launch_res_##v(const CandLaunch& c, hipStream_t s);   \
+  int blocks_res_##v(int R, int metric, int nw);
+KNN_DP_LIST(KNN_DECL)
+#undef KNN_DECL
+
+// Large-dimension variant (DP > 256, e.g. the reference's MNIST default
+// d=784): the query tile no longer fits in VGPRs, so both operands are staged
+// through LDS in chunks of DC dims.  Workgroup tile = 128 queries x 128 train
+// rows (4 waves x (32 queries x 4 row blocks)); per chunk each wave issues
+// 4 x DC/2 MFMAs reading its B fragment once per 8 dims and reusing it over
+// the 4 row blocks.  LDS: 2 buffers x (A 128xDC + B 128xDC), rows padded by
+// 16 B (DC/4 + 1 odd -> conflict-free ds_read_b128).  Same selection epilogue
+// after the last chunk of a tile.
+template <int DC, int R, int METRIC>
+__global__ void __launch_bounds__(256)
+cand_stream_kernel(const float* __restrict__ X32, const float* __restrict__ xinit,
+                   const float* __restrict__ Q32, int DP, int n_tiles, int S, int n_qt,
+                   float* __restrict__ out_v, int* __restrict__ out_i) {
+  constexpr int TRS = 128;          // train rows per tile
+  constexpr int LS = DC + 4;        // LDS row stride (floats)
+  constexpr int OP = TRS * LS;      // floats per operand image
+  constexpr int CPR = DC / 4;       // float4 per row chunk
+  constexpr int NCH = TRS * CPR;    // float4 per operand chunk
+  constexpr int CPT = NCH / 256;    // per thread
+  static_assert(CPT == 4, "staging below is written for 4 float4 per operand");
+  __shared__ __attribute__((aligned(16))) float lds[2 * 2 * OP + 2 * TRS];
+  float* ldsn = lds + 4 * OP;
+
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / n_qt;
+  const int qt = bid - split * n_qt;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int j = lane & 31, h = lane >> 5;
+  const int64_t qg = (int64_t)qt * kQPB + wv * 32 + j;
+  const int nch = DP / DC;
+
+  float L[R];
+  int I[R];
+#pragma unroll
+  for (int t = 0; t < R; ++t) { L[t] = KNN_INF_F; I[t] = -1; }
+  float thr = KNN_INF_F;
+
+  const int my_nt = split < n_tiles ? (n_tiles - split + S - 1) / S : 0;
+  const int total = my_nt * nch;
+
+  float4 a0, a1, a2, a3, b0, b1, b2, b3;
+  float4 stn = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float* qbase = Q32 + (int64_t)qt * kQPB * DP;
+#define KNN_SLOAD(st_)                                                                  \
+  do {                                                                                  \
+    const int it_ = (st_) / nch, c_ = (st_) - it_ * nch;                                \
+    const int t_ = split + it_ * S;                                                     \
+    const float* xs_ = X32 + (int64_t)t_ * TRS * (DP + 4) + c_ * DC;                    \
+    const float* qs_ = qbase + c_ * DC;                                                 \
+    int e_ = tid;                                                                       \
+    a0 = *(const float4*)(xs_ + (e_ / CPR) * (DP + 4) + (e_ % CPR) * 4);                \
+    b0 = *(const float4*)(qs_ + (e_ / CPR) * DP + (e_ % CPR) * 4);                      \
+    e_ += 256;                                                                          \
+    a1 = *(const float4*)(xs_ + (e_ / CPR) * (DP + 4) + (e_ % CPR) * 4);                \
+    b1 = *(const float4*)(qs_ + (e_ / CPR) * DP + (e_ % CPR) * 4);                      \
+    e_ += 256;                                                                          \
+    a2 = *(const float4*)(xs_ + (e_ / CPR) * (DP + 4) + (e_ % CPR) * 4);                \
+    b2 = *(const float4*)(qs_ + (e_ / CPR) * DP + (e_ % CPR) * 4);                      \
+    e_ += 256;                                                                          \
+    a3 = *(const float4*)(xs_ + (e_ / CPR) * (DP + 4) + (e_ % CPR) * 4);                \
+    b3 = *(const float4*)(qs_ + (e_ / CPR) * DP + (e_ % CPR) * 4);                      \
+    if (c_ == 0 && tid < TRS / 4) stn = ((const float4*)(xinit + (int64_t)t_ * TRS))[tid]; \
+  } while (0)
+#define KNN_SSTORE(st_, buf_)                                                           \
+  do {                                                                                  \
+    float* A_ = lds + (buf_) * 2 * OP;                                                  \
+    float* B_ = A_ + OP;                                                                \
+    int e_ = tid;                                                                       \
+    *(float4*)(A_ + (e_ / CPR) * LS + (e_ % CPR) * 4) = a0;                             \
+    *(float4*)(B_ + (e_ / CPR) * LS + (e_ % CPR) * 4) = b0;                             \
+    e_ += 256;                                                                          \
+    *(float4*)(A_ + (e_ / CPR) * LS + (e_ % CPR) * 4) = a1;                             \
+    *(float4*)(B_ + (e_ / CPR) * LS + (e_ % CPR) * 4) = b1;                             \
+    e_ += 256;                                                                          \
+    *(float4*)(A_ + (e_ / CPR) * LS + (e_ % CPR) * 4) = a2;                             \
+    *(float4*)(B_ + (e_ / CPR) * LS + (e_ % CPR) * 4) = b2;                             \
+    e_ += 256;                                                                          \
+    *(float4*)(A_ + (e_ / CPR) * LS + (e_ % CPR) * 4) = a3;                             \
+    *(float4*)(B_ + (e_ / CPR) * LS + (e_ % CPR) * 4) = b3;                             \
+    const int c_ = (st_) % nch;                                                         \
+    if (c_ == 0 && tid < TRS / 4) *(float4*)(ldsn + (buf_) * TRS + 4 * tid) = stn;      \
+  } while (0)
+
+  if (total > 0) {
+    KNN_SLOAD(0);
+    KNN_SSTORE(0, 0);
+  }
+  __syncthreads();
+
+  f32x16 acc0, acc1, acc2, acc3;
+  for (int st = 0; st < total; ++st) {
+    const int it = st / nch, c = st - it * nch;
+    const int t = split + it * S;
+    const bool more = st + 1 < total;
+    if (more) KNN_SLOAD(st + 1);
+    const float* A = lds + (st & 1) * 2 * OP;
+    const float* B = A + OP;
+    if (c == 0) {
+      // the norms were staged with chunk 0 of this tile into buffer (st & 1)
+      const float* nb = ldsn + (st & 1) * TRS;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 n0 = *(const float4*)(nb + 0 * 32 + 8 * g + 4 * h);
+        const float4 n1 = *(const float4*)(nb + 1 * 32 + 8 * g + 4 * h);
+        const float4 n2 = *(const float4*)(nb + 2 * 32 + 8 * g + 4 * h);
+        const float4 n3 = *(const float4*)(nb + 3 * 32 + 8 * g + 4 * h);
+        acc0[4 * g] = n0.x; acc0[4 * g + 1] = n0.y; acc0[4 * g + 2] = n0.z; acc0[4 * g + 3] = n0.w;
+        acc1[4 * g] = n1.x; acc1[4 * g + 1] = n1.y; acc1[4 * g + 2] = n1.z; acc1[4 * g + 3] = n1.w;
+        acc2[4 * g] = n2.x; acc2[4 * g + 1] = n2.y; acc2[4 * g + 2] = n2.z; acc2[4 * g + 3] = n2.w;
+        acc3[4 * g] = n3.x; acc3[4 * g + 1] = n3.y; acc3[4 * g + 2] = n3.z; acc3[4 * g + 3] = n3.w;
+      }
+    }
+    if constexpr (METRIC == 0) {
+      const float* brow = B + (wv * 32 + j) * LS + 4 * h;
+      const float* arow = A + j * LS + 4 * h;
+#pragma unroll
+      for (int g = 0; g < DC / 8; ++g) {
+        const float4 b = *(const float4*)(brow + 8 * g);
+        const float4 x0 = *(const float4*)(arow + 0 * 32 * LS + 8 * g);
+        const float4 x1 = *(const float4*)(arow + 1 * 32 * LS + 8 * g);
+        const float4 x2 = *(const float4*)(arow + 2 * 32 * LS + 8 * g);
+        const float4 x3 = *(const float4*)(arow + 3 * 32 * LS + 8 * g);
+#define KNN_MF4(acc_, x_)                                                               \
+  acc_ = __builtin_amdgcn_mfma_f32_32x32x2f32(x_.x, b.x, acc_, 0, 0, 0);                \
+  acc_ = __builtin_amdgcn_mfma_f32_32x32x2f32(x_.y, b.y, acc_, 0, 0, 0);                \
+  acc_ = __builtin_amdgcn_mfma_f32_32x32x2f32(x_.z, b.z, acc_, 0, 0, 0);                \
+  acc_ = __builtin_amdgcn_mfma_f32_32x32x2f32(x_.w, b.w, acc_, 0, 0, 0);
+        KNN_MF4(acc0, x0) KNN_MF4(acc1, x1) KNN_MF4(acc2, x2) KNN_MF4(acc3, x3)
+#undef KNN_MF4
+      }
+    } else {
+      const float* brow = B + (wv * 32 + j) * LS;
+#pragma unroll 2
+      for (int g = 0; g < DC / 4; ++g) {
+        const float4 qv = *(const float4*)(brow + 4 * g);
+#define KNN_L1B(acc_, blk_)                                                             \
+  _Pragma("unroll") for (int i = 0; i < 16; ++i) {                                      \
+    const int r = (blk_) * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;                         \
+    const float4 xv = *(const float4*)(A + r * LS + 4 * g);                             \
+    float a = acc_[i];                                                                  \
+    a = a + __builtin_fabsf(qv.x - xv.x);                                               \
+    a = a + __builtin_fabsf(qv.y - xv.y);                                               \
+    a = a + __builtin_fabsf(qv.z - xv.z);                                               \
+    a = a + __builtin_fabsf(qv.w - xv.w);                                               \
+    acc_[i] = a;                                                                        \
+  }
+        KNN_L1B(acc0, 0) KNN_L1B(acc1, 1) KNN_L1B(acc2, 2) KNN_L1B(acc3, 3)
+#undef KNN_L1B
+      }
+    }
+    if (c == nch - 1) {
+      select_block<R>(acc0, t * TRS + 0, h, L, I, thr);
+      select_block<R>(acc1, t * TRS + 32, h, L, I, thr);
+      select_block<R>(acc2, t * TRS + 64, h, L, I, thr);
+      select_block<R>(acc3, t * TRS + 96, h, L, I, thr);
+    }
+    if (more) KNN_SSTORE(st + 1, (st + 1) & 1);
+    __syncthreads();
+  }
+  write_lists<R>(out_v, out_i, qg, S, split, h, L, I);
+#undef KNN_SLOAD
+#undef KNN_SSTORE
+}
+
+// -------------------------------------- bf16x3 large-dimension kernel (S3)
+// For DP > 256 with the bf16x3 L2 candidate pass (cfg5: d = 960, k = 100;
+// the reference's MNIST default d = 784).  Neither operand fits in VGPRs, so
+// both are staged per chunk of 16 dims (one 32x32x16 k-step).  Workgroup =
+// 8 waves, tile = 256 queries x 256 train rows; wave w owns queries
+// 32w..32w+31 against all 256 rows as 8 accumulator blocks (128 acc
+// registers), so one staged chunk (32 KiB: 16 KiB of rows + 16 KiB of
+// queries) feeds 8 x 24 MFMAs -- 98 MACs per staged byte, a third of what the
+// XCD L2 can deliver at the full MFMA rate.  The epilogue (the same register
+// top-R lists as cand_kernel) runs once per tile, i.e. every DP/16 chunks.
+//
+// HBM images are pre-laid out exactly as the LDS images, so LDS-DMA copies
+// them linearly: block (tile, chunk) = 256 rows x 64 B, row r holding the
+// four 16-B slots {hi k0-7, hi k8-15, lo k0-7, lo k8-15} at slot position
+// s ^ ((r >> 2) & 3).  That XOR makes every 16-lane group of a ds_read_b128
+// (lanes on rows {0-3,12-15,20-27} etc.) touch 16 distinct 16-B bank groups.
+// Seeds (fl32 ||x32||^2, +inf on pad rows) travel as one 1-KiB piece with
+// chunk 0 of each tile.
+template <int R>
+__global__ void __launch_bounds__(512)
+cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* QT, int nch,
+               int n_tiles, int S, int n_qt, float* __restrict__ out_v, int* __restrict__ out_i,
+               int abl) {
+  // abl: timing-only ablations as in cand_kernel (bit0 no staging after the
+  // first steps, bit1 no selection epilogue); 0 in production.
+  constexpr int BLK = kS3R * 64;        // bytes of one operand image
+  constexpr int BUFB = 2 * BLK + 1024;  // A (rows) | B (queries) | seeds
+  constexpr int NB = 3;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[NB * BUFB];
+
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / n_qt;
+  const int qt = bid - split * n_qt;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int j = lane & 31, h = lane >> 5;
+  const int64_t qg = (int64_t)qt * kS3Q + wv * 32 + j;
+  // fragment byte offsets inside an image (the swizzle depends on j only:
+  // rows 32b + j and 32w + j share (r >> 2) & 3)
+  const int sw = (j >> 2) & 3;
+  const int off_hi = j * 64 + ((h ^ sw) << 4);
+  const int off_lo = j * 64 + (((2 + h) ^ sw) << 4);
+  const int off_q = wv * 32 * 64;
+
+  const int my_nt = split < n_tiles ? (n_tiles - split + S - 1) / S : 0;
+  const int total = my_nt * nch;
+  const uint32_t lds_base =
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)lds;
+
+  // issue cursor (chunk, tile, buffer) of the next step to stage
+  int ic = 0, itile = split, ib = 0;
+  auto issue = [&]() {
+    const char* gA = (const char*)XT + ((int64_t)itile * nch + ic) * BLK + lane * 16;
+    const char* gB = (const char*)QT + ((int64_t)qt * nch + ic) * BLK + lane * 16;
+    const uint32_t l = lds_base + (uint32_t)(ib * BUFB);
+    glds16(gA + wv * 1024, l + wv * 1024);
+    glds16(gA + (wv + 8) * 1024, l + (wv + 8) * 1024);
+    glds16(gB + wv * 1024, l + BLK + wv * 1024);
+    glds16(gB + (wv + 8) * 1024, l + BLK + (wv + 8) * 1024);
+    if (ic == 0 && wv == 0)
+      glds16((const char*)(XS + (int64_t)itile * kS3R) + lane * 16, l + 2 * BLK);
+    if (++ic == nch) { ic = 0; itile += S; }
+    if (++ib == NB) ib = 0;
+  };
+
+  float L[R];
+  int I[R];
+#pragma unroll
+  for (int t = 0; t < R; ++t) { L[t] = KNN_INF_F; I[t] = -1; }
+  float thr = KNN_INF_F;
+
+  if (total > 0) issue();
+  if (total > 1) issue();
+
+  f32x16 acc[8];
+  int c = 0, t = split, cb = 0;
+  for (int st = 0; st < total; ++st) {
+    // own pieces of step st landed (those of st+1 may still be in flight),
+    // then the barrier publishes every wave's pieces and retires all reads
+    // of the buffer that the issue below refills.
+    if (st + 1 < total) {
+      if (wv == 0 && c + 1 == nch)
+        asm volatile("s_waitcnt vmcnt(5)\n\ts_barrier" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (st + 2 < total && !(abl & 1)) issue();
+
+    const unsigned char* buf = lds + cb * BUFB;
+    if (c == 0) {
+      const float* seed = (const float*)(buf + 2 * BLK);
+#pragma unroll
+      for (int bb = 0; bb < 8; ++bb) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 s4 = *(const float4*)(seed + 32 * bb + 8 * g + 4 * h);
+          acc[bb][4 * g] = s4.x;
+          acc[bb][4 * g + 1] = s4.y;
+          acc[bb][4 * g + 2] = s4.z;
+          acc[bb][4 * g + 3] = s4.w;
+        }
+      }
+    }
+    const bf16x8 bh = *(const bf16x8*)(buf + BLK + off_q + off_hi);
+    const bf16x8 bl = *(const bf16x8*)(buf + BLK + off_q + off_lo);
+#pragma unroll
+    for (int bb = 0; bb < 8; ++bb) {
+      const bf16x8 ah = *(const bf16x8*)(buf + bb * 32 * 64 + off_hi);
+      const bf16x8 al = *(const bf16x8*)(buf + bb * 32 * 64 + off_lo);
+      acc[bb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[bb], 0, 0, 0);
+      acc[bb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[bb], 0, 0, 0);
+      acc[bb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[bb], 0, 0, 0);
+    }
+    if (c == nch - 1) {
+      if (!(abl & 2)) {
+#pragma unroll
+        for (int bb = 0; bb < 8; ++bb) select_block<R>(acc[bb], t * kS3R + 32 * bb, h, L, I, thr);
+      } else if (acc[0][0] == 1234.5f && acc[7][15] == 1234.5f) {
+        thr = acc[3][7];  // keep the accumulators live
+      }
+    }
+    if (++c == nch) { c = 0; t += S; }
+    if (++cb == NB) cb = 0;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  write_lists<R>(out_v, out_i, qg, S, split, h, L, I);
+}
+
+
+int pad_dim(int d) {
+#define KNN_CASE(v) if (d <= v) return v;
+  KNN_DP_LIST(KNN_CASE)
+#undef KNN_CASE
+  return (d + kStreamDC - 1) / kStreamDC * kStreamDC;  // streamed kernel
+}
+
+bool cand_supported(int DP) { return DP > 0 && pad_dim(DP) == DP; }
+
+// bf16x3 path: resident kernel for DP <= 256 (a multiple of 16 in the
+// resident list), the S3 stream kernel above it (any multiple of 16).
+int pad_dim_bf16x3(int d) {
+  const int d16 = (d + 15) / 16 * 16;
+  if (d16 > 256) return d16;
+  const int DP = pad_dim(d16);
+  return (DP <= 256 && DP % 16 == 0) ? DP : -1;
+}
+
+bool bf16x3_streamed(int DP) { return DP > 256; }
+
+int s3_blocks_per_cu(int R) {
+  return R == 8 ? occupancy_of(cand_s3_kernel<8>, 512) : occupancy_of(cand_s3_kernel<16>, 512);
+}
+
+void launch_cand_s3(const unsigned short* XT, const float* XS, const unsigned short* QT, int DP,
+                    int64_t n_pad, int R, int S, int n_qt, float* out_v, int* out_i, int ablate,
+                    hipStream_t s) {
+  const int nch = DP / kS3DC;
+  const int n_tiles = (int)(n_pad / kS3R);
+  if (R == 8)
+    hipLaunchKernelGGL(cand_s3_kernel<8>, dim3((unsigned)(n_qt * S)), dim3(512), 0, s, XT, XS, QT,
+                       nch, n_tiles, S, n_qt, out_v, out_i, ablate);
+  else
+    hipLaunchKernelGGL(cand_s3_kernel<16>, dim3((unsigned)(n_qt * S)), dim3(512), 0, s, XT, XS, QT,
+                       nch, n_tiles, S, n_qt, out_v, out_i, ablate);
+}
+
+template <int R, int METRIC>
+static void launch_str(const CandLaunch& c, hipStream_t s) {
+  hipLaunchKernelGGL((cand_stream_kernel<kStreamDC, R, METRIC>), dim3((unsigned)(c.n_qt * c.S)),
+                     dim3(256), 0, s, c.X32, c.xinit, c.Q32, c.DP, (int)(c.n_pad / 128), c.S,
+                     c.n_qt, c.out_v, c.out_i);
+}
+
+int cand_blocks_per_cu(int metric, int DP, int R, int nw) {
+  if (metric == 2 && bf16x3_streamed(DP)) return s3_blocks_per_cu(R);
+#define KNN_CASE(v) if (DP == v) return blocks_res_##v(R, metric, nw);
+  KNN_DP_LIST(KNN_CASE)
+#undef KNN_CASE
+  int out = 1;
+  if (R == 8)
+    out = occupancy_of(metric == 1 ? cand_stream_kernel<kStreamDC, 8, 1>
+                                   : cand_stream_kernel<kStreamDC, 8, 0>, 256);
+  else
+    out = occupancy_of(metric == 1 ? cand_stream_kernel<kStreamDC, 16, 1>
+                                   : cand_stream_kernel<kStreamDC, 16, 0>, 256);
+  return out;
+}
+
+int cand_tile_rows(int DP) { return DP <= 256 ? kTR : 128; }
+
+void launch_cand(const CandLaunch& c, hipStream_t s) {
+#define KNN_CASE(v)                \
+  if (c.DP == v) {                 \
+    launch_res_##v(c, s);          \
+    return;                        \
+  }
+  KNN_DP_LIST(KNN_CASE)
+#undef KNN_CASE
+  if (c.R == 8) {
+    if (c.metric == 1) launch_str<8, 1>(c, s);
+    else launch_str<8, 0>(c, s);
+  } else {
+    if (c.metric == 1) launch_str<16, 1>(c, s);
+    else launch_str<16, 0>(c, s);
+  }
+}
+
+}  // namespace knnk

@@ -1,0 +1,285 @@
+// knn_cand_res.hip -- the register-resident candidate kernel (d <= 256),
+// compiled once per group of padded dimensions (-DKNN_GROUP=0..3) so the
+// many (DP, R, metric, waves) instantiations build in parallel.
+#include "knn_device.h"
+
+namespace knnk {
+
+// Train rows in HBM (X32 for fp32/L1, XB for bf16x3) share one padded row
+// format of RSF = DP + 4 floats: [payload (DP floats) | ||x32||^2, l1 seed,
+// 0, 0], where payload is DP fp32 values or [hi(DP) | lo(DP)] bf16.  A tile
+// is 32 consecutive rows = one contiguous block, copied linearly into LDS;
+// the odd 16-B row stride (DP/4 + 1 chunks) makes the A-fragment reads
+// (ds_read_b128, 16-lane groups on distinct rows) bank-conflict free, and the
+// accumulator seeds come from the same rows.  Pad rows carry +inf seeds.
+//
+// Workgroup = 4 waves = 128 queries; it streams the 32-row train tiles
+// split, split+S, split+2S, ... (round-robin so a run of similar rows is
+// spread over all splits).  Lane (j = lane&31, h = lane>>5) of wave w owns
+// query j of the wave and the train rows rho(i,h) = (i&3) + 8(i>>2) + 4h of
+// every tile (the 32x32 MFMA C/D layout with train rows on A, queries on B).
+//
+// METRIC 0, per tile and wave: DP/2 MFMAs 32x32x2 f32; lane (r, h) reads
+// float4 X[r][8c+4h ..] for the four k-steps of group c.  METRIC 2: 3*DP/16
+// MFMAs 32x32x16 bf16 (see below).  The B operand (queries, -2 q) stays in
+// VGPRs for the whole kernel.  Accumulators start at ||x_row||^2, so
+// acc = ||x||^2 - 2 q.x.
+//
+// NW waves (32 queries each) share every staged tile: NW = 8 halves the
+// staging instructions and L2 traffic per MFMA relative to NW = 4.
+//
+// Staging: global_load_lds (LDS-DMA, no VGPRs), 3 LDS buffers: tile it+2 is
+// issued right after the barrier that opens tile it, and each wave waits
+// with a counted vmcnt for its own pieces of tile it before that barrier --
+// two tiles of latency hidden, one barrier per tile.  (A register-staged
+// variant measured the same or slower; removed.)
+template <int DP, int R, int METRIC, int NW>
+__global__ void __launch_bounds__(NW * 64)
+cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
+            int n_qt, float* __restrict__ out_v, int* __restrict__ out_i, int abl) {
+  // Q32 is deliberately not __restrict__: with it hipcc treats the query
+  // fragments as invariant and re-loads them inside the tile loop instead of
+  // keeping them in VGPRs (its waits would then also drain the LDS-DMA queue).
+  // abl: timing-only ablations (results invalid): bit0 = no staging loads
+  // after the first tiles, bit1 = no selection epilogue.  0 in production.
+  constexpr int RSF = DP + 4;               // row stride (floats), HBM and LDS
+  constexpr int TBY = kTR * RSF * 4;        // tile bytes
+  constexpr int NG = (TBY + 1023) / 1024;   // 1-KiB LDS-DMA pieces per tile
+  constexpr int NB = 3;                     // LDS buffers (prefetch distance 2)
+  constexpr int BUFF = NG * 256;            // floats per buffer
+  constexpr int SEED = METRIC == 1 ? DP + 1 : DP;  // seed float within a row
+  __shared__ __attribute__((aligned(16))) float lds[NB * BUFF];
+
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / n_qt;
+  const int qt = bid - split * n_qt;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int j = lane & 31, h = lane >> 5;
+  const int64_t qg = (int64_t)qt * (NW * 32) + wv * 32 + j;
+  const float* qrow = Q32 + qg * DP;
+
+  // B operand resident in VGPRs for the whole kernel.  METRIC 0: fp32 -2q,
+  // float4 c holds dims 8c+4h..8c+4h+3 (four 32x32x2 k-steps).  METRIC 2:
+  // the row is [qh | ql] in bf16 (-2q split hi/lo); float4 t (t < DP/16) is
+  // qh dims 16t+8h..16t+8h+7, float4 DP/16+t the same dims of ql.
+  float4 qf[METRIC != 1 ? DP / 8 : 1];
+  if constexpr (METRIC != 1) {
+    // Loaded with inline asm (loads + their vmcnt(0) in one statement): with
+    // ordinary loads hipcc places the vmcnt waits for these registers at
+    // their first MFMA use INSIDE the tile loop, where each executes every
+    // tile and -- counting all vector-memory ops -- drains the in-flight
+    // LDS-DMA pieces of the staging pipeline.
+#pragma unroll
+    for (int c0 = 0; c0 < DP / 8; c0 += 4) {
+      const float* p[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int c = c0 + u < DP / 8 ? c0 + u : c0;
+        const int off = METRIC == 0 ? 8 * c : (c < DP / 16 ? 8 * c : DP / 2 + 8 * (c - DP / 16));
+        p[u] = qrow + off + 4 * h;
+      }
+      float4 v0, v1, v2, v3;
+      asm volatile(
+          "global_load_dwordx4 %0, %4, off\n\t"
+          "global_load_dwordx4 %1, %5, off\n\t"
+          "global_load_dwordx4 %2, %6, off\n\t"
+          "global_load_dwordx4 %3, %7, off\n\t"
+          "s_waitcnt vmcnt(0)"
+          : "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3)
+          : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3])
+          : "memory");
+      qf[c0] = v0;
+      if (c0 + 1 < DP / 8) qf[c0 + 1] = v1;
+      if (c0 + 2 < DP / 8) qf[c0 + 2] = v2;
+      if (c0 + 3 < DP / 8) qf[c0 + 3] = v3;
+    }
+  }
+
+  float L[R];
+  int I[R];
+#pragma unroll
+  for (int t = 0; t < R; ++t) { L[t] = KNN_INF_F; I[t] = -1; }
+  float thr = KNN_INF_F;
+
+  const int my_nt = split < n_tiles ? (n_tiles - split + S - 1) / S : 0;
+
+  // ---- staging: this wave's LDS-DMA pieces i = wv, wv+NW, ... of tile t ->
+  // buffer b.  The last piece may read past the tile (and past the last row:
+  // the HBM allocation carries 1 KiB of slack); it lands in the buffer tail.
+  constexpr int G_HI = (NG + NW - 1) / NW, G_LO = NG / NW;
+  static_assert(G_HI <= 15, "vmcnt immediate range");
+  // LDS byte address of the staging array (wave-uniform)
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)lds;
+#define KNN_ISSUE(t_, b_)                                                              \
+  do {                                                                                 \
+    const char* g_ = (const char*)Xr + (int64_t)(t_) * TBY + lane * 16;                \
+    const uint32_t l_ = lds_base + (uint32_t)((b_) * BUFF * 4);                        \
+    for (int i_ = wv; i_ < NG; i_ += NW) glds16(g_ + i_ * 1024, l_ + (uint32_t)(i_ * 1024)); \
+  } while (0)
+
+  if (my_nt > 0) KNN_ISSUE(split, 0);
+  if (my_nt > 1) KNN_ISSUE(split + S, 1);
+
+  for (int it = 0; it < my_nt; ++it) {
+    const int t = split + it * S;
+    int cur;
+    {
+      // this wave's pieces of tile `it` have landed once at most the pieces
+      // of tile it+1 remain outstanding; the barrier then publishes all
+      // waves' pieces and retires every read of buffer (it-1)%3 before it is
+      // refilled with tile it+2.
+      // wait + barrier in ONE asm statement with a memory clobber, so no LDS
+      // read can be hoisted above the barrier (a bare s_barrier builtin does
+      // not order memory) and no vmcnt(0) drains the in-flight tiles.
+      if (it + 1 < my_nt) {
+        if (wv < NG % NW || NG % NW == 0)
+          asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" :: "n"(G_HI) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" :: "n"(G_LO) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (it + 2 < my_nt && !(abl & 1)) KNN_ISSUE(t + 2 * S, (it + 2) % 3);
+      cur = it % 3;
+    }
+    const float* base = lds + cur * BUFF;
+
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = base[((i & 3) + 8 * (i >> 2) + 4 * h) * RSF + SEED];
+    if constexpr (METRIC == 0) {
+      const float* arow = base + j * RSF + 4 * h;
+#pragma unroll
+      for (int c = 0; c < DP / 8; ++c) {
+        const float4 a = *(const float4*)(arow + 8 * c);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, qf[c].x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, qf[c].y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, qf[c].z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, qf[c].w, acc, 0, 0, 0);
+      }
+    } else if constexpr (METRIC == 2) {
+      // bf16x3 split product on v_mfma_f32_32x32x16_bf16:
+      //   q.x ~= qh.xh + ql.xh + qh.xl   (train row payload = [xh | xl])
+      // i.e. one bf16 GEMM with K = 3*DP; ~2^-16 relative product error,
+      // 16x the f32 MFMA rate per instruction -> 5.3x per fp32-equivalent flop.
+      const float* arow = base + j * RSF + 4 * h;
+#pragma unroll
+      for (int tt = 0; tt < DP / 16; ++tt) {
+        const bf16x8 ah = __builtin_bit_cast(bf16x8, *(const float4*)(arow + 8 * tt));
+        const bf16x8 al = __builtin_bit_cast(bf16x8, *(const float4*)(arow + DP / 2 + 8 * tt));
+        const bf16x8 bh = __builtin_bit_cast(bf16x8, qf[tt]);
+        const bf16x8 bl = __builtin_bit_cast(bf16x8, qf[DP / 16 + tt]);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+      }
+    } else {
+      // L1 on the VALU: lane's query against its 16 rows, dims in chunks of 4.
+#pragma unroll 2
+      for (int c = 0; c < DP / 4; ++c) {
+        const float4 qv = *(const float4*)(qrow + 4 * c);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int r = (i & 3) + 8 * (i >> 2) + 4 * h;
+          const float4 xv = *(const float4*)(base + r * RSF + 4 * c);
+          float a = acc[i];
+          a = a + __builtin_fabsf(qv.x - xv.x);
+          a = a + __builtin_fabsf(qv.y - xv.y);
+          a = a + __builtin_fabsf(qv.z - xv.z);
+          a = a + __builtin_fabsf(qv.w - xv.w);
+          acc[i] = a;
+        }
+      }
+    }
+
+    if (!(abl & 2)) select_block<R>(acc, t * kTR, h, L, I, thr);
+    else if (acc[0] == 1234.5f && acc[15] == 1234.5f) thr = acc[7];  // keep acc live
+
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  write_lists<R>(out_v, out_i, qg, S, split, h, L, I);
+#undef KNN_ISSUE
+}
+
+// Compile-time dispatch over (R, METRIC): R in {8, 16}; METRIC 0/1/2
+// (2 = bf16x3, resident kernel with DP % 16 == 0 only).
+template <class F>
+static void with_R(int R, F f) {
+  if (R == 8) f(std::integral_constant<int, 8>{});
+  else f(std::integral_constant<int, 16>{});
+}
+template <class F>
+static void with_M(int M, F f) {
+  if (M == 0) f(std::integral_constant<int, 0>{});
+  else if (M == 1) f(std::integral_constant<int, 1>{});
+  else f(std::integral_constant<int, 2>{});
+}
+
+template <int DP, int R, int METRIC, int NW>
+static void launch_res(const CandLaunch& c, hipStream_t s) {
+  hipLaunchKernelGGL((cand_kernel<DP, R, METRIC, NW>), dim3((unsigned)(c.n_qt * c.S)),
+                     dim3(NW * 64), 0, s, c.X32, c.Q32, (int)(c.n_pad / kTR), c.S, c.n_qt,
+                     c.out_v, c.out_i, c.ablate);
+}
+
+// Instantiated variants: R in {8, 16}; METRIC 0/2 with NW in {4, 8};
+// METRIC 1 (L1, not perf-graded) with NW = 4; METRIC 2 needs DP % 16 == 0.
+template <int DP, int R, int M, int NW>
+constexpr bool res_variant() {
+  return (M != 2 || DP % 16 == 0) && (M != 1 || NW == 4);
+}
+
+template <int DP>
+static int blocks_per_cu_res(int R, int metric, int nw) {
+  int out = 1;
+  with_R(R, [&](auto Rc) {
+    with_M(metric, [&](auto Mc) {
+      if (nw == 8) {
+        if constexpr (res_variant<DP, Rc.value, Mc.value, 8>())
+          out = occupancy_of(cand_kernel<DP, Rc.value, Mc.value, 8>, 512);
+      } else {
+        if constexpr (res_variant<DP, Rc.value, Mc.value, 4>())
+          out = occupancy_of(cand_kernel<DP, Rc.value, Mc.value, 4>, 256);
+      }
+    });
+  });
+  return out;
+}
+
+template <int DP>
+static void launch_res_dp(const CandLaunch& c, hipStream_t s) {
+  with_R(c.R, [&](auto Rc) {
+    with_M(c.metric, [&](auto Mc) {
+      if (c.nw == 8) {
+        if constexpr (res_variant<DP, Rc.value, Mc.value, 8>())
+          launch_res<DP, Rc.value, Mc.value, 8>(c, s);
+      } else {
+        if constexpr (res_variant<DP, Rc.value, Mc.value, 4>())
+          launch_res<DP, Rc.value, Mc.value, 4>(c, s);
+      }
+    });
+  });
+}
+
+#if KNN_GROUP == 0
+#define KNN_GROUP_DPS(X) X(8) X(16) X(24) X(32) X(48) X(64)
+#elif KNN_GROUP == 1
+#define KNN_GROUP_DPS(X) X(96) X(128)
+#elif KNN_GROUP == 2
+#define KNN_GROUP_DPS(X) X(160) X(192)
+#elif KNN_GROUP == 3
+#define KNN_GROUP_DPS(X) X(256)
+#else
+#error "KNN_GROUP must be 0..3"
+#endif
+
+#define KNN_DEF(v)                                                                 \
+  void launch_res_##v(const CandLaunch& c, hipStream_t s) { launch_res_dp<v>(c, s); } \
+  int blocks_res_##v(int R, int metric, int nw) { return blocks_per_cu_res<v>(R, metric, nw); }
+KNN_GROUP_DPS(KNN_DEF)
+#undef KNN_DEF
+
+}  // namespace knnk

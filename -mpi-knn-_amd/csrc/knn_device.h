@@ -1,0 +1,222 @@
+// knn_device.h -- device helpers shared by the gfx950 kernel translation
+// units (knn_prep.hip, knn_cand*.hip, knn_select.hip).  Internal.
+#pragma once
+#include "knn_kernels.h"
+
+#include <float.h>
+#include <limits.h>
+
+#include <type_traits>
+
+#pragma clang fp contract(off)
+
+namespace knnk {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+#define KNN_INF_F __builtin_inff()
+#define KNN_INF_D __builtin_inf()
+
+// ---------------------------------------------------------------- helpers
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  // Blocks are dispatched round-robin over the 8 XCDs; give each XCD a
+  // contiguous range of logical ids so workgroups that stream the same train
+  // split share an L2 (bijective for any nwg).
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_or_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Reference distance, bit-exact with cpp:33-50 (L2: returns the squared sum
+// before sqrt) and cpp:51-67 (L1): fp64, dims in order, multiply then add.
+template <int METRIC>
+__device__ __forceinline__ double exact_dist_raw(const double* __restrict__ q,
+                                                 const double* __restrict__ x, int d) {
+  double r = 0.0;
+#pragma unroll 8
+  for (int i = 0; i < d; ++i) {
+    const double t = q[i] - x[i];
+    if (METRIC == 0) r = r + t * t;
+    else r = r + __builtin_fabs(t);
+  }
+  return r;
+}
+template <int METRIC>
+__device__ __forceinline__ double exact_dist(const double* __restrict__ q,
+                                             const double* __restrict__ x, int d) {
+  const double r = exact_dist_raw<METRIC>(q, x, d);
+  return METRIC == 0 ? __builtin_sqrt(r) : r;  // llvm.sqrt.f64: correctly rounded
+}
+
+template <typename K, typename I>
+__device__ __forceinline__ bool pair_less(K ka, I ia, K kb, I ib) {
+  return ka < kb || (ka == kb && ia < ib);
+}
+
+// Bitonic sort of n (power of two) (key, id) pairs in LDS, ascending by
+// (key, id).  All threads of the block participate.
+template <typename K, typename I>
+__device__ void bitonic_sort_lds(K* key, I* id, int n, int tid, int nthr) {
+  for (int size = 2; size <= n; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      __syncthreads();
+      for (int t = tid; t < (n >> 1); t += nthr) {
+        const int lo = 2 * t - (t & (stride - 1));
+        const int hi = lo + stride;
+        const bool up = (lo & size) == 0;
+        const K ka = key[lo], kb = key[hi];
+        const I ia = id[lo], ib = id[hi];
+        const bool sw = up ? pair_less(kb, ib, ka, ia) : pair_less(ka, ia, kb, ib);
+        if (sw) {
+          key[lo] = kb; key[hi] = ka;
+          id[lo] = ib; id[hi] = ia;
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ int pow2_ceil(int v) {
+  int p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+// bf16 hi/lo split of fp64 rows: row r of the output is [hi(DP) | lo(DP)]
+// with hi = bf16(x), lo = bf16(x - hi) (x - hi exact in fp64), scaled by
+// `scale` (exact power of two), zero padding beyond d and on pad rows.
+__device__ __forceinline__ void split_bf16(double x, unsigned short& hi, unsigned short& lo) {
+  const __bf16 h = (__bf16)(float)x;
+  const double r = x - (double)(float)h;
+  const __bf16 l = (__bf16)(float)r;
+  hi = __builtin_bit_cast(unsigned short, h);
+  lo = __builtin_bit_cast(unsigned short, l);
+}
+
+// ------------------------------------------------------- candidate kernel
+// Sorted insertion of v (< L[R-1]) into the ascending register list (L, I);
+// the previous last entry drops out.  Fully unrolled: no dynamic register
+// indexing (which would go to scratch).
+template <int R>
+__device__ __forceinline__ void list_insert(float (&L)[R], int (&I)[R], float v, int id) {
+  // L'[t] = max(L[t-1], min(v, L[t])) shifts the tail and drops L[R-1];
+  // the index follows with two selects.  Branch-free: v_min/v_max/v_cndmask
+  // (the TU is built with -fno-honor-nans so fminf/fmaxf need no quieting).
+  bool cc = true;  // v < L[R-1] by precondition
+#pragma unroll
+  for (int t = R - 1; t > 0; --t) {
+    const bool cp = v < L[t - 1];
+    L[t] = __builtin_fmaxf(L[t - 1], __builtin_fminf(v, L[t]));
+    I[t] = cp ? I[t - 1] : (cc ? id : I[t]);
+    cc = cp;
+  }
+  I[0] = cc ? id : I[0];
+  L[0] = __builtin_fminf(v, L[0]);
+}
+
+// One 16-B-per-lane LDS-DMA piece (global_load_lds_dwordx4): 64 lanes x 16 B
+// from per-lane global addresses to LDS [lds_addr, lds_addr + 1 KiB).  Issued
+// from inline asm so hipcc neither counts it nor inserts its own
+// s_waitcnt vmcnt(0) before later LDS reads (it would drain the pipeline);
+// the kernel waits with explicit counted vmcnt + s_barrier instead.  M0 is
+// compiler-reserved, so it is saved and restored inside the statement.
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_addr) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_addr))
+      : "memory");
+}
+
+// Fused top-R selection over one 32x32 accumulator block: lane (j, h) holds
+// the values of query j against rows row0 + rho(i, h), i = 0..15.  Once the
+// list is warm this is a 16-way min (v_min3) and one compare per block; a
+// value is inserted only under a branch that no lane of the wave skips.
+template <int R>
+__device__ __forceinline__ void select_block(const f32x16& acc, int row0, int h, float (&L)[R],
+                                             int (&I)[R], float& thr) {
+  // Lanes l and l^32 hold the same query: filtering with the smaller of the
+  // two list thresholds is safe -- anything dropped is >= some list's final
+  // R-th entry, which the merge's lower bound (min over lists) accounts for.
+  float te = __builtin_fminf(thr, __shfl_xor(thr, 32, 64));
+  float mn = __builtin_fminf(acc[0], acc[1]);
+#pragma unroll
+  for (int i = 2; i < 16; ++i) mn = __builtin_fminf(mn, acc[i]);
+  if (mn < te) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float v = acc[i];
+      if (v < te) {
+        list_insert<R>(L, I, v, row0 + (i & 3) + 8 * (i >> 2) + 4 * h);
+        thr = L[R - 1];
+        te = __builtin_fminf(te, thr);
+      }
+    }
+  }
+}
+
+// Lists are stored [query][split][half][R] so a query's 2S lists are contiguous.
+template <int R>
+__device__ __forceinline__ void write_lists(float* __restrict__ out_v, int* __restrict__ out_i,
+                                            int64_t qg, int S, int split, int h,
+                                            const float (&L)[R], const int (&I)[R]) {
+  const int64_t o = ((qg * (2 * S)) + split * 2 + h) * R;
+#pragma unroll
+  for (int t = 0; t < R; t += 4) {
+    *(float4*)(out_v + o + t) = make_float4(L[t], L[t + 1], L[t + 2], L[t + 3]);
+    *(int4*)(out_i + o + t) = make_int4(I[t], I[t + 1], I[t + 2], I[t + 3]);
+  }
+}
+
+// S3 (bf16x3, DP > 256) image geometry; see knn_cand.hip
+constexpr int kS3Q = 256;   // queries per workgroup
+constexpr int kS3R = 256;   // train rows per tile
+constexpr int kS3DC = 16;   // dims per staged chunk
+
+__device__ __forceinline__ int s3_slot(int r, int s) { return s ^ ((r >> 2) & 3); }
+
+template <class KernelT>
+static int occupancy_of(KernelT k, int threads) {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, threads, 0) != hipSuccess) return 1;
+  return nb > 0 ? nb : 1;
+}
+
+#define KNN_DP_LIST(X) X(8) X(16) X(24) X(32) X(48) X(64) X(96) X(128) X(160) X(192) X(256)
+
+}  // namespace knnk

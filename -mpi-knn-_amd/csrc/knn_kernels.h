@@ -44,6 +44,20 @@ struct TrainDev {
 
 int pad_dim(int d);                 // padded dim the candidate kernels run at
 int pad_dim_bf16x3(int d);          // padded dim of the bf16x3 kernel, -1 if unsupported
+bool bf16x3_streamed(int DP);       // bf16x3 at this DP runs the S3 stream kernel
+constexpr int kS3Rows = 256;        // S3 kernel: train rows per tile = queries per workgroup
+int s3_blocks_per_cu(int R);
+// S3 kernel (bf16x3, DP > 256): XT/QT are tile-chunk images made by
+// launch_prep_split_tiled, XS the per-row seeds [n_pad]; n_pad and m_pad are
+// multiples of kS3Rows.
+void launch_cand_s3(const unsigned short* XT, const float* XS, const unsigned short* QT, int DP,
+                    int64_t n_pad, int R, int S, int n_qt, float* out_v, int* out_i, int ablate,
+                    hipStream_t s);
+// fp64 rows -> bf16 hi/lo tile-chunk images of scale*x (S3 layout); seed_out
+// (train only, else null) receives seed_src[row] (+inf on pad rows)
+void launch_prep_split_tiled(const double* X64, int64_t n, int d, int DP, int64_t n_pad,
+                             double scale, unsigned short* out, const float* seed_src,
+                             float* seed_out, hipStream_t s);
 bool cand_supported(int DP);
 int cand_tile_rows(int DP);         // train rows per tile of the kernel serving DP
 int cand_blocks_per_cu(int metric, int DP, int R, int nw);  // resident workgroups per CU

@@ -1,0 +1,185 @@
+// knn_prep.hip -- operand preparation kernels (gfx950): fp64 rows -> fp32 /
+// bf16 hi-lo MFMA operands, seeds and norm statistics.
+#include "knn_device.h"
+
+namespace knnk {
+
+// ------------------------------------------------------------------ prep
+// One wave per train row: fp64 -> fp32 (zero padded to DP), fl32(||x32||^2)
+// seeds for the L2 accumulator, 0 seeds for L1, +inf on pad rows; running
+// max of ||x||_2^2 and ||x||_1 (fp64, non-negative -> ordered as u64 bits).
+__global__ void __launch_bounds__(256)
+prep_train_kernel(const double* __restrict__ X64, int64_t n, int d, int DP, int64_t n_pad,
+                  float* __restrict__ X32, float* __restrict__ xl2, float* __restrict__ xl1,
+                  unsigned long long* __restrict__ stats) {
+  const int RSF = DP + 4;  // padded row: [x32 (DP) | ||x32||^2, l1 seed, 0, 0]
+  const int lane = threadIdx.x & 63;
+  const int64_t wstride = (int64_t)gridDim.x * 4;
+  double m2 = 0.0, m1 = 0.0;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n_pad; row += wstride) {
+    double s32 = 0.0, s64 = 0.0, a64 = 0.0;
+    for (int c = lane; c < DP; c += 64) {
+      float v = 0.0f;
+      if (row < n && c < d) {
+        const double x = X64[row * d + c];
+        v = (float)x;
+        s64 += x * x;
+        a64 += __builtin_fabs(x);
+      }
+      X32[row * RSF + c] = v;
+      s32 += (double)v * (double)v;
+    }
+    s32 = wave_sum_d(s32);
+    s64 = wave_sum_d(s64);
+    a64 = wave_sum_d(a64);
+    if (lane < 4) {
+      const float s2 = row < n ? (float)s32 : KNN_INF_F;
+      const float s1 = row < n ? 0.0f : KNN_INF_F;
+      X32[row * RSF + DP + lane] = lane == 0 ? s2 : (lane == 1 ? s1 : 0.0f);
+      if (lane == 0) {
+        xl2[row] = s2;
+        xl1[row] = s1;
+      }
+    }
+    m2 = fmax(m2, s64);
+    m1 = fmax(m1, a64);
+  }
+  if (lane == 0) {
+    // small relative slack covers the order of the fp64 sums above
+    atomicMax(&stats[0], (unsigned long long)__double_as_longlong(m2 * (1.0 + 1e-12)));
+    atomicMax(&stats[1], (unsigned long long)__double_as_longlong(m1 * (1.0 + 1e-12)));
+  }
+}
+
+void launch_prep_train(const double* X64, int64_t n, int d, int DP, int64_t n_pad, float* X32,
+                       float* xl2, float* xl1, unsigned long long* stats, hipStream_t s) {
+  int64_t blocks = (n_pad + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(prep_train_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X64, n, d, DP,
+                     n_pad, X32, xl2, xl1, stats);
+}
+
+__global__ void __launch_bounds__(256)
+prep_queries_kernel(const double* __restrict__ Q64, int64_t m, int d, int DP, int64_t m_pad,
+                    float scale, float* __restrict__ Q32) {
+  const int64_t total = m_pad * DP;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * 256) {
+    const int64_t row = e / DP;
+    const int c = (int)(e - row * DP);
+    float v = 0.0f;
+    if (row < m && c < d) v = scale * (float)Q64[row * d + c];  // x(-2) is exact
+    Q32[e] = v;
+  }
+}
+
+void launch_prep_queries(const double* Q64, int64_t m, int d, int DP, int64_t m_pad,
+                         float scale, float* Q32, hipStream_t s) {
+  int64_t blocks = (m_pad * DP + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(prep_queries_kernel, dim3((unsigned)blocks), dim3(256), 0, s, Q64, m, d,
+                     DP, m_pad, scale, Q32);
+}
+
+__global__ void __launch_bounds__(256)
+prep_split_kernel(const double* __restrict__ X64, int64_t n, int d, int DP, int64_t n_pad,
+                  double scale, unsigned short* __restrict__ out, int row_shorts,
+                  const float* __restrict__ xl2, const float* __restrict__ xl1) {
+  // row r of `out` (row_shorts 16-bit words) = [hi(DP) | lo(DP) | seeds...]
+  const int64_t total = n_pad * DP;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * 256) {
+    const int64_t row = e / DP;
+    const int c = (int)(e - row * DP);
+    unsigned short hi = 0, lo = 0;
+    if (row < n && c < d) split_bf16(scale * X64[row * d + c], hi, lo);
+    out[row * row_shorts + c] = hi;
+    out[row * row_shorts + DP + c] = lo;
+    if (xl2 && c < 4) {  // train rows: the padded row's seed floats
+      float* seed = (float*)(out + row * row_shorts + 2 * DP);
+      seed[c] = c == 0 ? xl2[row] : (c == 1 ? xl1[row] : 0.0f);
+    }
+  }
+}
+
+void launch_prep_split(const double* X64, int64_t n, int d, int DP, int64_t n_pad, double scale,
+                       unsigned short* out, int row_shorts, const float* xl2, const float* xl1,
+                       hipStream_t s) {
+  int64_t blocks = (n_pad * DP + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(prep_split_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X64, n, d, DP,
+                     n_pad, scale, out, row_shorts, xl2, xl1);
+}
+
+__global__ void fill_i32_kernel(int32_t* p, int64_t n, int32_t v) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256)
+    p[e] = v;
+}
+void launch_fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t s) {
+  if (n <= 0) return;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(fill_i32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p, n, v);
+}
+
+// -------------------------------------- bf16x3 large-dimension kernel (S3)
+// For DP > 256 with the bf16x3 L2 candidate pass (cfg5: d = 960, k = 100;
+// the reference's MNIST default d = 784).  Neither operand fits in VGPRs, so
+// both are staged per chunk of 16 dims (one 32x32x16 k-step).  Workgroup =
+// 8 waves, tile = 256 queries x 256 train rows; wave w owns queries
+// 32w..32w+31 against all 256 rows as 8 accumulator blocks (128 acc
+// registers), so one staged chunk (32 KiB: 16 KiB of rows + 16 KiB of
+// queries) feeds 8 x 24 MFMAs -- 98 MACs per staged byte, a third of what the
+// XCD L2 can deliver at the full MFMA rate.  The epilogue (the same register
+// top-R lists as cand_kernel) runs once per tile, i.e. every DP/16 chunks.
+//
+// HBM images are pre-laid out exactly as the LDS images, so LDS-DMA copies
+// them linearly: block (tile, chunk) = 256 rows x 64 B, row r holding the
+// four 16-B slots {hi k0-7, hi k8-15, lo k0-7, lo k8-15} at slot position
+// s ^ ((r >> 2) & 3).  That XOR makes every 16-lane group of a ds_read_b128
+// (lanes on rows {0-3,12-15,20-27} etc.) touch 16 distinct 16-B bank groups.
+// Seeds (fl32 ||x32||^2, +inf on pad rows) travel as one 1-KiB piece with
+// chunk 0 of each tile.
+__global__ void __launch_bounds__(256)
+prep_split_tiled_kernel(const double* __restrict__ X64, int64_t n, int d, int DP, int64_t n_pad,
+                        double scale, unsigned short* __restrict__ out,
+                        const float* __restrict__ seed_src, float* __restrict__ seed_out) {
+  const int G = DP / 8;  // 8-dim groups per row
+  const int nch = DP / kS3DC;
+  const int64_t total = n_pad * G;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * 256) {
+    const int64_t row = e / G;
+    const int g = (int)(e - row * G);
+    unsigned short hi[8], lo[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int col = 8 * g + u;
+      hi[u] = lo[u] = 0;
+      if (row < n && col < d) split_bf16(scale * X64[row * d + col], hi[u], lo[u]);
+    }
+    const int64_t tile = row / kS3R;
+    const int r = (int)(row - tile * kS3R);
+    const int c = g >> 1, sh = g & 1;
+    unsigned char* blk = (unsigned char*)out + (((int64_t)tile * nch + c) * kS3R + r) * 64;
+    uint4 vh, vl;
+    vh.x = hi[0] | (uint32_t)hi[1] << 16; vh.y = hi[2] | (uint32_t)hi[3] << 16;
+    vh.z = hi[4] | (uint32_t)hi[5] << 16; vh.w = hi[6] | (uint32_t)hi[7] << 16;
+    vl.x = lo[0] | (uint32_t)lo[1] << 16; vl.y = lo[2] | (uint32_t)lo[3] << 16;
+    vl.z = lo[4] | (uint32_t)lo[5] << 16; vl.w = lo[6] | (uint32_t)lo[7] << 16;
+    *(uint4*)(blk + s3_slot(r, sh) * 16) = vh;
+    *(uint4*)(blk + s3_slot(r, 2 + sh) * 16) = vl;
+    if (seed_out && g == 0) seed_out[row] = row < n ? seed_src[row] : KNN_INF_F;
+  }
+}
+
+void launch_prep_split_tiled(const double* X64, int64_t n, int d, int DP, int64_t n_pad,
+                             double scale, unsigned short* out, const float* seed_src,
+                             float* seed_out, hipStream_t s) {
+  int64_t blocks = (n_pad * (DP / 8) + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(prep_split_tiled_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X64, n, d,
+                     DP, n_pad, scale, out, seed_src, seed_out);
+}
+
+}  // namespace knnk

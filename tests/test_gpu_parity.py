@@ -124,6 +124,11 @@ CASES = [
     (3000, 150, 256, 50, 0, 10),    # largest register-resident dim, K=50
     (4000, 100, 64, 100, 0, 10),    # K=100 (cfg5's k)
     (8000, 128, 24, 16, 0, 6),
+    # large d: bf16x3 S3 stream kernel (auto) / fp32 stream kernel (fp32)
+    (3000, 300, 300, 10, 0, 10),    # d not a multiple of 16 -> zero padding, ragged m
+    (2500, 257, 784, 50, 0, 10),    # the reference's MNIST dimension, K=50
+    (4000, 200, 960, 100, 0, 10),   # cfg5 shape (d=960, k=100), scaled down
+    (700, 40, 520, 5, 1, 4),        # L1 at large d (fp32 stream kernel in both modes)
 ]
 
 
