@@ -138,9 +138,13 @@ static int build_train(knn_ctx* ctx, const double* dX, const int32_t* dlab, int6
   if ((rc = ctx->xl2.ensure((size_t)n_pad * sizeof(float)))) return rc;
   if ((rc = ctx->xl1.ensure((size_t)n_pad * sizeof(float)))) return rc;
   if ((rc = ctx->stats.ensure(2 * sizeof(unsigned long long)))) return rc;
+  if ((rc = ctx->mu.ensure((size_t)d * sizeof(double)))) return rc;
+  if ((rc = ctx->mu_part.ensure((size_t)col_mean_blocks(n) * d * sizeof(double)))) return rc;
+  launch_col_mean(dX, n, d, (double*)ctx->mu_part.p, (double*)ctx->mu.p, ctx->stream);
   HIP_TRY(hipMemsetAsync(ctx->stats.p, 0, 2 * sizeof(unsigned long long), ctx->stream));
-  launch_prep_train(dX, n, d, DP, n_pad, (float*)ctx->X32.p, (float*)ctx->xl2.p,
-                    (float*)ctx->xl1.p, (unsigned long long*)ctx->stats.p, ctx->stream);
+  launch_prep_train(dX, (const double*)ctx->mu.p, n, d, DP, n_pad, (float*)ctx->X32.p,
+                    (float*)ctx->xl2.p, (float*)ctx->xl1.p, (unsigned long long*)ctx->stats.p,
+                    ctx->stream);
   HIP_TRY(hipGetLastError());
   unsigned long long st[2];
   HIP_TRY(hipMemcpyAsync(st, ctx->stats.p, sizeof st, hipMemcpyDeviceToHost, ctx->stream));
@@ -150,6 +154,7 @@ static int build_train(knn_ctx* ctx, const double* dX, const int32_t* dlab, int6
   memcpy(&x1, &st[1], 8);
   TrainDev& t = ctx->train;
   t.X64 = dX;
+  t.mu = (const double*)ctx->mu.p;
   t.lab = dlab;
   t.X32 = (const float*)ctx->X32.p;
   t.xinit_l2 = (const float*)ctx->xl2.p;
@@ -181,11 +186,11 @@ static int ensure_bf16x3(knn_ctx* ctx, hipStream_t s) {
     const int64_t n3 = (t.n + kS3Rows - 1) / kS3Rows * kS3Rows;
     if ((rc = ctx->XB.ensure((size_t)n3 * DPb * 4))) return rc;
     if ((rc = ctx->XS.ensure((size_t)n3 * sizeof(float)))) return rc;
-    launch_prep_split_tiled(t.X64, t.n, t.d, DPb, n3, 1.0, (unsigned short*)ctx->XB.p, t.xinit_l2,
+    launch_prep_split_tiled(t.X64, t.mu, t.n, t.d, DPb, n3, 1.0, (unsigned short*)ctx->XB.p, t.xinit_l2,
                             (float*)ctx->XS.p, s);
   } else {
     if ((rc = ctx->XB.ensure((size_t)t.n_pad * (DPb + 4) * sizeof(float) + 1024))) return rc;
-    launch_prep_split(t.X64, t.n, t.d, DPb, t.n_pad, 1.0, (unsigned short*)ctx->XB.p,
+    launch_prep_split(t.X64, t.mu, t.n, t.d, DPb, t.n_pad, 1.0, (unsigned short*)ctx->XB.p,
                       2 * (DPb + 4), t.xinit_l2, t.xinit_l1, s);
   }
   HIP_TRY(hipGetLastError());
@@ -346,13 +351,14 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   const bool tm = ctx->timing;
   if (tm) HIP_TRY(hipEventRecord(ctx->ev[0], s));
   if (s3)
-    launch_prep_split_tiled(dQ, m, t.d, DP, m_pad, -2.0, (unsigned short*)ctx->Q32.p, nullptr,
+    launch_prep_split_tiled(dQ, t.mu, m, t.d, DP, m_pad, -2.0, (unsigned short*)ctx->Q32.p, nullptr,
                             nullptr, s);
   else if (kmetric == 2)
-    launch_prep_split(dQ, m, t.d, DP, m_pad, -2.0, (unsigned short*)ctx->Q32.p, 2 * DP, nullptr,
+    launch_prep_split(dQ, t.mu, m, t.d, DP, m_pad, -2.0, (unsigned short*)ctx->Q32.p, 2 * DP, nullptr,
                       nullptr, s);
   else
-    launch_prep_queries(dQ, m, t.d, DP, m_pad, metric == 0 ? -2.0f : 1.0f, (float*)ctx->Q32.p, s);
+    launch_prep_queries(dQ, t.mu, m, t.d, DP, m_pad, metric == 0 ? -2.0f : 1.0f,
+                        (float*)ctx->Q32.p, s);
   if (tm) HIP_TRY(hipEventRecord(ctx->ev[1], s));
   CandLaunch cl{};
   cl.metric = kmetric;

@@ -33,13 +33,14 @@ struct Sink {
 // Train-set side state resident in HBM.
 struct TrainDev {
   const double* X64;     // [n][d] fp64 (reference values)
+  const double* mu;      // [d] train column means: the candidate pass's centre
   const int32_t* lab;    // [n]
   const float* X32;      // [n_pad][DP+4] fp32 padded rows (payload | seeds), zero padded
   const float* xinit_l2; // [n_pad] fl32(||x32||^2); +inf on pad rows
   const float* xinit_l1; // [n_pad] 0; +inf on pad rows
   int64_t n, n_pad;
   int d, DP;
-  double x2max, x1max;   // max ||x||_2^2, max ||x||_1 over the train rows
+  double x2max, x1max;   // max ||x - mu||_2^2, max ||x - mu||_1 over the train rows
 };
 
 int pad_dim(int d);                 // padded dim the candidate kernels run at
@@ -55,9 +56,9 @@ void launch_cand_s3(const unsigned short* XT, const float* XS, const unsigned sh
                     hipStream_t s);
 // fp64 rows -> bf16 hi/lo tile-chunk images of scale*x (S3 layout); seed_out
 // (train only, else null) receives seed_src[row] (+inf on pad rows)
-void launch_prep_split_tiled(const double* X64, int64_t n, int d, int DP, int64_t n_pad,
-                             double scale, unsigned short* out, const float* seed_src,
-                             float* seed_out, hipStream_t s);
+void launch_prep_split_tiled(const double* X64, const double* mu, int64_t n, int d, int DP,
+                             int64_t n_pad, double scale, unsigned short* out,
+                             const float* seed_src, float* seed_out, hipStream_t s);
 bool cand_supported(int DP);
 int cand_tile_rows(int DP);         // train rows per tile of the kernel serving DP
 int cand_blocks_per_cu(int metric, int DP, int R, int nw);  // resident workgroups per CU
@@ -75,10 +76,15 @@ struct CandLaunch {
   int nw;       // resident kernel: waves (x32 queries) per workgroup, 4 or 8
 };
 
-void launch_prep_train(const double* X64, int64_t n, int d, int DP, int64_t n_pad, float* X32,
-                       float* xl2, float* xl1, unsigned long long* stats, hipStream_t s);
-void launch_prep_queries(const double* Q64, int64_t m, int d, int DP, int64_t m_pad,
-                         float scale, float* Q32, hipStream_t s);
+// Candidate-pass operands are centred on the train column means mu (see knn_prep.hip).
+int col_mean_blocks(int64_t n);  // rows of the `partial` scratch (x d doubles)
+void launch_col_mean(const double* X64, int64_t n, int d, double* partial, double* mu,
+                     hipStream_t s);
+void launch_prep_train(const double* X64, const double* mu, int64_t n, int d, int DP,
+                       int64_t n_pad, float* X32, float* xl2, float* xl1,
+                       unsigned long long* stats, hipStream_t s);
+void launch_prep_queries(const double* Q64, const double* mu, int64_t m, int d, int DP,
+                         int64_t m_pad, float scale, float* Q32, hipStream_t s);
 void launch_cand(const CandLaunch& c, hipStream_t s);
 void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int R,
                          const TrainDev& t, const double* Q64, int64_t m, int W, int C,
@@ -96,9 +102,9 @@ void launch_fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t s);
 // fp64 rows -> [hi(DP) | lo(DP)] bf16 rows of scale*x (candidate metric 2 = L2 via bf16x3)
 // rows of `out` are row_shorts 16-bit words; xl2/xl1 (train only, else null)
 // fill the padded row's seed floats after the 2*DP bf16 payload
-void launch_prep_split(const double* X64, int64_t n, int d, int DP, int64_t n_pad, double scale,
-                       unsigned short* out, int row_shorts, const float* xl2, const float* xl1,
-                       hipStream_t s);
+void launch_prep_split(const double* X64, const double* mu, int64_t n, int d, int DP,
+                       int64_t n_pad, double scale, unsigned short* out, int row_shorts,
+                       const float* xl2, const float* xl1, hipStream_t s);
 
 // Min-max normalisation (knn_normalize.hip, cpp:229-306).  R = rows per
 // grid sweep; `partial` holds 2*d*R doubles.  launch_minmax folds the set's

@@ -5,13 +5,60 @@
 namespace knnk {
 
 // ------------------------------------------------------------------ prep
-// One wave per train row: fp64 -> fp32 (zero padded to DP), fl32(||x32||^2)
-// seeds for the L2 accumulator, 0 seeds for L1, +inf on pad rows; running
-// max of ||x||_2^2 and ||x||_1 (fp64, non-negative -> ordered as u64 bits).
+// Every candidate-pass operand is centred on the train mean mu: distances
+// are translation invariant (||q - x|| = ||(q - mu) - (x - mu)||), while the
+// candidate pass's rounding error scales with ||x||^2 and ||q||.||x|| -- on
+// min-max normalised data centring shrinks those ~20x, which is what lets
+// the certification pass at d = 960.  mu only shifts the
+// operands; the exact re-rank always uses the caller's fp64 rows.
+
+// Column means, deterministic: block b sums rows [b*rpb, (b+1)*rpb) of every
+// dim in row order (coalesced across threads), then one pass adds the
+// per-block sums in block order.
 __global__ void __launch_bounds__(256)
-prep_train_kernel(const double* __restrict__ X64, int64_t n, int d, int DP, int64_t n_pad,
-                  float* __restrict__ X32, float* __restrict__ xl2, float* __restrict__ xl1,
-                  unsigned long long* __restrict__ stats) {
+col_sum_kernel(const double* __restrict__ X64, int64_t n, int d, int64_t rpb,
+               double* __restrict__ partial) {
+  const int64_t r0 = (int64_t)blockIdx.x * rpb;
+  const int64_t r1 = r0 + rpb < n ? r0 + rpb : n;
+  for (int c = threadIdx.x; c < d; c += 256) {
+    double s = 0.0;
+    for (int64_t r = r0; r < r1; ++r) s += X64[r * d + c];
+    partial[(int64_t)blockIdx.x * d + c] = s;
+  }
+}
+
+__global__ void __launch_bounds__(256)
+col_mean_kernel(const double* __restrict__ partial, int nb, int d, int64_t n,
+                double* __restrict__ mu) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= d) return;
+  double s = 0.0;
+  for (int b = 0; b < nb; ++b) s += partial[(int64_t)b * d + c];
+  mu[c] = s / (double)n;
+}
+
+int col_mean_blocks(int64_t n) {
+  const int64_t nb = (n + 1023) / 1024;
+  return (int)(nb < 2048 ? (nb > 0 ? nb : 1) : 2048);
+}
+
+void launch_col_mean(const double* X64, int64_t n, int d, double* partial, double* mu,
+                     hipStream_t s) {
+  const int nb = col_mean_blocks(n);
+  const int64_t rpb = (n + nb - 1) / nb;
+  hipLaunchKernelGGL(col_sum_kernel, dim3(nb), dim3(256), 0, s, X64, n, d, rpb, partial);
+  hipLaunchKernelGGL(col_mean_kernel, dim3((d + 255) / 256), dim3(256), 0, s, partial, nb, d, n,
+                     mu);
+}
+
+// One wave per train row: fp64 x - mu -> fp32 (zero padded to DP),
+// fl32(||x32||^2) seeds for the L2 accumulator, 0 seeds for L1, +inf on pad
+// rows; running max of ||x - mu||_2^2 and ||x - mu||_1 (fp64, non-negative
+// -> ordered as u64 bits).
+__global__ void __launch_bounds__(256)
+prep_train_kernel(const double* __restrict__ X64, const double* __restrict__ mu, int64_t n, int d,
+                  int DP, int64_t n_pad, float* __restrict__ X32, float* __restrict__ xl2,
+                  float* __restrict__ xl1, unsigned long long* __restrict__ stats) {
   const int RSF = DP + 4;  // padded row: [x32 (DP) | ||x32||^2, l1 seed, 0, 0]
   const int lane = threadIdx.x & 63;
   const int64_t wstride = (int64_t)gridDim.x * 4;
@@ -21,7 +68,7 @@ prep_train_kernel(const double* __restrict__ X64, int64_t n, int d, int DP, int6
     for (int c = lane; c < DP; c += 64) {
       float v = 0.0f;
       if (row < n && c < d) {
-        const double x = X64[row * d + c];
+        const double x = X64[row * d + c] - mu[c];
         v = (float)x;
         s64 += x * x;
         a64 += __builtin_fabs(x);
@@ -51,39 +98,40 @@ prep_train_kernel(const double* __restrict__ X64, int64_t n, int d, int DP, int6
   }
 }
 
-void launch_prep_train(const double* X64, int64_t n, int d, int DP, int64_t n_pad, float* X32,
-                       float* xl2, float* xl1, unsigned long long* stats, hipStream_t s) {
+void launch_prep_train(const double* X64, const double* mu, int64_t n, int d, int DP,
+                       int64_t n_pad, float* X32, float* xl2, float* xl1,
+                       unsigned long long* stats, hipStream_t s) {
   int64_t blocks = (n_pad + 3) / 4;
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(prep_train_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X64, n, d, DP,
-                     n_pad, X32, xl2, xl1, stats);
+  hipLaunchKernelGGL(prep_train_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X64, mu, n, d,
+                     DP, n_pad, X32, xl2, xl1, stats);
 }
 
 __global__ void __launch_bounds__(256)
-prep_queries_kernel(const double* __restrict__ Q64, int64_t m, int d, int DP, int64_t m_pad,
-                    float scale, float* __restrict__ Q32) {
+prep_queries_kernel(const double* __restrict__ Q64, const double* __restrict__ mu, int64_t m,
+                    int d, int DP, int64_t m_pad, float scale, float* __restrict__ Q32) {
   const int64_t total = m_pad * DP;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * 256) {
     const int64_t row = e / DP;
     const int c = (int)(e - row * DP);
     float v = 0.0f;
-    if (row < m && c < d) v = scale * (float)Q64[row * d + c];  // x(-2) is exact
+    if (row < m && c < d) v = scale * (float)(Q64[row * d + c] - mu[c]);  // x(-2) is exact
     Q32[e] = v;
   }
 }
 
-void launch_prep_queries(const double* Q64, int64_t m, int d, int DP, int64_t m_pad,
-                         float scale, float* Q32, hipStream_t s) {
+void launch_prep_queries(const double* Q64, const double* mu, int64_t m, int d, int DP,
+                         int64_t m_pad, float scale, float* Q32, hipStream_t s) {
   int64_t blocks = (m_pad * DP + 255) / 256;
   if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL(prep_queries_kernel, dim3((unsigned)blocks), dim3(256), 0, s, Q64, m, d,
+  hipLaunchKernelGGL(prep_queries_kernel, dim3((unsigned)blocks), dim3(256), 0, s, Q64, mu, m, d,
                      DP, m_pad, scale, Q32);
 }
 
 __global__ void __launch_bounds__(256)
-prep_split_kernel(const double* __restrict__ X64, int64_t n, int d, int DP, int64_t n_pad,
-                  double scale, unsigned short* __restrict__ out, int row_shorts,
+prep_split_kernel(const double* __restrict__ X64, const double* __restrict__ mu, int64_t n, int d,
+                  int DP, int64_t n_pad, double scale, unsigned short* __restrict__ out, int row_shorts,
                   const float* __restrict__ xl2, const float* __restrict__ xl1) {
   // row r of `out` (row_shorts 16-bit words) = [hi(DP) | lo(DP) | seeds...]
   const int64_t total = n_pad * DP;
@@ -92,7 +140,7 @@ prep_split_kernel(const double* __restrict__ X64, int64_t n, int d, int DP, int6
     const int64_t row = e / DP;
     const int c = (int)(e - row * DP);
     unsigned short hi = 0, lo = 0;
-    if (row < n && c < d) split_bf16(scale * X64[row * d + c], hi, lo);
+    if (row < n && c < d) split_bf16(scale * (X64[row * d + c] - mu[c]), hi, lo);
     out[row * row_shorts + c] = hi;
     out[row * row_shorts + DP + c] = lo;
     if (xl2 && c < 4) {  // train rows: the padded row's seed floats
@@ -102,12 +150,12 @@ prep_split_kernel(const double* __restrict__ X64, int64_t n, int d, int DP, int6
   }
 }
 
-void launch_prep_split(const double* X64, int64_t n, int d, int DP, int64_t n_pad, double scale,
-                       unsigned short* out, int row_shorts, const float* xl2, const float* xl1,
-                       hipStream_t s) {
+void launch_prep_split(const double* X64, const double* mu, int64_t n, int d, int DP,
+                       int64_t n_pad, double scale, unsigned short* out, int row_shorts,
+                       const float* xl2, const float* xl1, hipStream_t s) {
   int64_t blocks = (n_pad * DP + 255) / 256;
   if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL(prep_split_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X64, n, d, DP,
+  hipLaunchKernelGGL(prep_split_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X64, mu, n, d, DP,
                      n_pad, scale, out, row_shorts, xl2, xl1);
 }
 
@@ -122,27 +170,12 @@ void launch_fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t s) {
   hipLaunchKernelGGL(fill_i32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p, n, v);
 }
 
-// -------------------------------------- bf16x3 large-dimension kernel (S3)
-// For DP > 256 with the bf16x3 L2 candidate pass (cfg5: d = 960, k = 100;
-// the reference's MNIST default d = 784).  Neither operand fits in VGPRs, so
-// both are staged per chunk of 16 dims (one 32x32x16 k-step).  Workgroup =
-// 8 waves, tile = 256 queries x 256 train rows; wave w owns queries
-// 32w..32w+31 against all 256 rows as 8 accumulator blocks (128 acc
-// registers), so one staged chunk (32 KiB: 16 KiB of rows + 16 KiB of
-// queries) feeds 8 x 24 MFMAs -- 98 MACs per staged byte, a third of what the
-// XCD L2 can deliver at the full MFMA rate.  The epilogue (the same register
-// top-R lists as cand_kernel) runs once per tile, i.e. every DP/16 chunks.
-//
-// HBM images are pre-laid out exactly as the LDS images, so LDS-DMA copies
-// them linearly: block (tile, chunk) = 256 rows x 64 B, row r holding the
-// four 16-B slots {hi k0-7, hi k8-15, lo k0-7, lo k8-15} at slot position
-// s ^ ((r >> 2) & 3).  That XOR makes every 16-lane group of a ds_read_b128
-// (lanes on rows {0-3,12-15,20-27} etc.) touch 16 distinct 16-B bank groups.
-// Seeds (fl32 ||x32||^2, +inf on pad rows) travel as one 1-KiB piece with
-// chunk 0 of each tile.
+// ------------------------------- S3 images (bf16x3, DP > 256; knn_cand.hip)
+// Tile-chunk images: block (tile, chunk of 16 dims) = 256 rows x 64 B, the
+// four 16-B slots of row r at slot position s ^ ((r >> 2) & 3).
 __global__ void __launch_bounds__(256)
-prep_split_tiled_kernel(const double* __restrict__ X64, int64_t n, int d, int DP, int64_t n_pad,
-                        double scale, unsigned short* __restrict__ out,
+prep_split_tiled_kernel(const double* __restrict__ X64, const double* __restrict__ mu, int64_t n,
+                        int d, int DP, int64_t n_pad, double scale, unsigned short* __restrict__ out,
                         const float* __restrict__ seed_src, float* __restrict__ seed_out) {
   const int G = DP / 8;  // 8-dim groups per row
   const int nch = DP / kS3DC;
@@ -156,7 +189,7 @@ prep_split_tiled_kernel(const double* __restrict__ X64, int64_t n, int d, int DP
     for (int u = 0; u < 8; ++u) {
       const int col = 8 * g + u;
       hi[u] = lo[u] = 0;
-      if (row < n && col < d) split_bf16(scale * X64[row * d + col], hi[u], lo[u]);
+      if (row < n && col < d) split_bf16(scale * (X64[row * d + col] - mu[col]), hi[u], lo[u]);
     }
     const int64_t tile = row / kS3R;
     const int r = (int)(row - tile * kS3R);
@@ -173,12 +206,12 @@ prep_split_tiled_kernel(const double* __restrict__ X64, int64_t n, int d, int DP
   }
 }
 
-void launch_prep_split_tiled(const double* X64, int64_t n, int d, int DP, int64_t n_pad,
-                             double scale, unsigned short* out, const float* seed_src,
-                             float* seed_out, hipStream_t s) {
+void launch_prep_split_tiled(const double* X64, const double* mu, int64_t n, int d, int DP,
+                             int64_t n_pad, double scale, unsigned short* out,
+                             const float* seed_src, float* seed_out, hipStream_t s) {
   int64_t blocks = (n_pad * (DP / 8) + 255) / 256;
   if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL(prep_split_tiled_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X64, n, d,
+  hipLaunchKernelGGL(prep_split_tiled_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X64, mu, n, d,
                      DP, n_pad, scale, out, seed_src, seed_out);
 }
 

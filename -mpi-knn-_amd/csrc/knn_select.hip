@@ -121,7 +121,7 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
   } else {
     double qa = 0.0;
     for (int c = lane; c < d; c += 64) {
-      const double x = qrow[c];
+      const double x = qrow[c] - t.mu[c];  // centred like the candidate operands
       qa += METRIC == 0 ? x * x : __builtin_fabs(x);
     }
     qa = wave_sum_d(qa) * (1.0 + 1e-12);
