@@ -256,8 +256,10 @@ static void choose_geometry(knn_ctx* ctx, int metric, int DP, int nw, int n_qt, 
                             int& S_out, int& R_out) {
   const int S_hi = (int)std::max<int64_t>(1, std::min<int64_t>(64, n_tiles));
   int bestS = 1, bestR = 8;
-  for (int R : {8, 16}) {
-    if (ctx->tune_R && R != ctx->tune_R) continue;
+  for (int R : {4, 8, 16}) {
+    // R = 4 only on request (resident kernel; tuning experiments)
+    if (ctx->tune_R ? R != ctx->tune_R : R == 4) continue;
+    if (R == 4 && (DP > 256 || metric == 1)) continue;
     const int64_t slots = (int64_t)cand_blocks_per_cu(metric, DP, R, nw) * ctx->cu_count;
     const int S_lo = std::min(S_hi, std::max(1, (C + 2 * R - 1) / (2 * R)));
     auto eff_of = [&](int S) {
@@ -640,8 +642,8 @@ int knn_last_candidate_path(knn_ctx* ctx) { return ctx ? ctx->last_kmetric : -1;
 int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value) {
   if (!ctx || !key) return knn_fail(KNN_ERR_ARG, "null argument");
   if (!strcmp(key, "R")) {
-    if (value != 0 && value != 8 && value != 16)
-      return knn_fail(KNN_ERR_ARG, "R must be 0 (auto), 8 or 16");
+    if (value != 0 && value != 4 && value != 8 && value != 16)
+      return knn_fail(KNN_ERR_ARG, "R must be 0 (auto), 4, 8 or 16");
     ctx->tune_R = (int)value;
   } else if (!strcmp(key, "nw")) {
     if (value != 0 && value != 4 && value != 8) return knn_fail(KNN_ERR_ARG, "nw must be 0, 4 or 8");

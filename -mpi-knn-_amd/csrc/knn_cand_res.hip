@@ -3,7 +3,16 @@
 // many (DP, R, metric, waves) instantiations build in parallel.
 #include "knn_device.h"
 
+#ifndef KNN_RES_NB
+#define KNN_RES_NB 3  // staging buffers of the resident kernel (experiments: -DKNN_RES_NB=4)
+#endif
+
 namespace knnk {
+
+template <int N>
+__device__ __forceinline__ void wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
 
 // Train rows in HBM (X32 for fp32/L1, XB for bf16x3) share one padded row
 // format of RSF = DP + 4 floats: [payload (DP floats) | ||x32||^2, l1 seed,
@@ -45,7 +54,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   constexpr int RSF = DP + 4;               // row stride (floats), HBM and LDS
   constexpr int TBY = kTR * RSF * 4;        // tile bytes
   constexpr int NG = (TBY + 1023) / 1024;   // 1-KiB LDS-DMA pieces per tile
-  constexpr int NB = 3;                     // LDS buffers (prefetch distance 2)
+  constexpr int NB = KNN_RES_NB;            // LDS buffers (prefetch distance NB - 1)
   constexpr int BUFF = NG * 256;            // floats per buffer
   constexpr int SEED = METRIC == 1 ? DP + 1 : DP;  // seed float within a row
   __shared__ __attribute__((aligned(16))) float lds[NB * BUFF];
@@ -108,7 +117,8 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   // buffer b.  The last piece may read past the tile (and past the last row:
   // the HBM allocation carries 1 KiB of slack); it lands in the buffer tail.
   constexpr int G_HI = (NG + NW - 1) / NW, G_LO = NG / NW;
-  static_assert(G_HI <= 15, "vmcnt immediate range");
+  constexpr int PD = NB - 1;  // prefetch distance in tiles
+  static_assert(G_HI * (PD - 1) <= 63, "vmcnt range");
   // LDS byte address of the staging array (wave-uniform)
   const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)lds;
 #define KNN_ISSUE(t_, b_)                                                              \
@@ -118,31 +128,32 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
     for (int i_ = wv; i_ < NG; i_ += NW) glds16(g_ + i_ * 1024, l_ + (uint32_t)(i_ * 1024)); \
   } while (0)
 
-  if (my_nt > 0) KNN_ISSUE(split, 0);
-  if (my_nt > 1) KNN_ISSUE(split + S, 1);
+#pragma unroll
+  for (int p = 0; p < PD; ++p)
+    if (my_nt > p) KNN_ISSUE(split + p * S, p);
 
+  const bool g_hi = wv < NG % NW || NG % NW == 0;
+  int cur = 0, nxt = PD;  // buffer of tile it, buffer that tile it+PD goes to
   for (int it = 0; it < my_nt; ++it) {
     const int t = split + it * S;
-    int cur;
     {
       // this wave's pieces of tile `it` have landed once at most the pieces
-      // of tile it+1 remain outstanding; the barrier then publishes all
-      // waves' pieces and retires every read of buffer (it-1)%3 before it is
-      // refilled with tile it+2.
+      // of the (up to PD-1) later tiles already issued remain outstanding;
+      // the barrier then publishes all waves' pieces and retires every read
+      // of buffer (it-1)%NB before it is refilled with tile it+PD.
       // wait + barrier in ONE asm statement with a memory clobber, so no LDS
       // read can be hoisted above the barrier (a bare s_barrier builtin does
       // not order memory) and no vmcnt(0) drains the in-flight tiles.
-      if (it + 1 < my_nt) {
-        if (wv < NG % NW || NG % NW == 0)
-          asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" :: "n"(G_HI) : "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" :: "n"(G_LO) : "memory");
+      const int ahead = min(PD - 1, my_nt - 1 - it);
+      if (ahead >= 2 && PD >= 3) {
+        if (g_hi) wait_barrier<2 * G_HI>(); else wait_barrier<2 * G_LO>();
+      } else if (ahead == 1) {
+        if (g_hi) wait_barrier<G_HI>(); else wait_barrier<G_LO>();
       } else {
-        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        wait_barrier<0>();
       }
       __builtin_amdgcn_sched_barrier(0);
-      if (it + 2 < my_nt && !(abl & 1)) KNN_ISSUE(t + 2 * S, (it + 2) % 3);
-      cur = it % 3;
+      if (it + PD < my_nt && !(abl & 1)) KNN_ISSUE(t + PD * S, nxt);
     }
     const float* base = lds + cur * BUFF;
 
@@ -196,6 +207,8 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
 
     if (!(abl & 2)) select_block<R>(acc, t * kTR, h, L, I, thr);
     else if (acc[0] == 1234.5f && acc[15] == 1234.5f) thr = acc[7];  // keep acc live
+    if (++cur == NB) cur = 0;
+    if (++nxt == NB) nxt = 0;
 
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -204,11 +217,12 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
 #undef KNN_ISSUE
 }
 
-// Compile-time dispatch over (R, METRIC): R in {8, 16}; METRIC 0/1/2
+// Compile-time dispatch over (R, METRIC): R in {4, 8, 16}; METRIC 0/1/2
 // (2 = bf16x3, resident kernel with DP % 16 == 0 only).
 template <class F>
 static void with_R(int R, F f) {
-  if (R == 8) f(std::integral_constant<int, 8>{});
+  if (R == 4) f(std::integral_constant<int, 4>{});
+  else if (R == 8) f(std::integral_constant<int, 8>{});
   else f(std::integral_constant<int, 16>{});
 }
 template <class F>
@@ -225,11 +239,12 @@ static void launch_res(const CandLaunch& c, hipStream_t s) {
                      c.out_v, c.out_i, c.ablate);
 }
 
-// Instantiated variants: R in {8, 16}; METRIC 0/2 with NW in {4, 8};
-// METRIC 1 (L1, not perf-graded) with NW = 4; METRIC 2 needs DP % 16 == 0.
+// Instantiated variants: R in {4, 8, 16}; METRIC 0/2 with NW in {4, 8};
+// METRIC 1 (L1, not perf-graded) with NW = 4 and R in {8, 16}; METRIC 2
+// needs DP % 16 == 0.
 template <int DP, int R, int M, int NW>
 constexpr bool res_variant() {
-  return (M != 2 || DP % 16 == 0) && (M != 1 || NW == 4);
+  return (M != 2 || DP % 16 == 0) && (M != 1 || (NW == 4 && R != 4));
 }
 
 template <int DP>

@@ -173,7 +173,12 @@ __device__ __forceinline__ void select_block(const f32x16& acc, int row0, int h,
   // Lanes l and l^32 hold the same query: filtering with the smaller of the
   // two list thresholds is safe -- anything dropped is >= some list's final
   // R-th entry, which the merge's lower bound (min over lists) accounts for.
-  float te = __builtin_fminf(thr, __shfl_xor(thr, 32, 64));
+  // v_permlane32_swap of thr with itself: r[0] = lower half, r[1] = upper
+  // half of every lane pair, so min(r[0], r[1]) = min over lanes l, l^32
+  // (one VALU op instead of an LDS ds_bpermute round trip).
+  const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(thr), __float_as_uint(thr),
+                                                   false, false);
+  float te = __builtin_fminf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
   float mn = __builtin_fminf(acc[0], acc[1]);
 #pragma unroll
   for (int i = 2; i < 16; ++i) mn = __builtin_fminf(mn, acc[i]);

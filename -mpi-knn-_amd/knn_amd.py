@@ -19,6 +19,9 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libknn_amd.so")
+# experiment builds (tools/build_variant.sh) are selected by file name under lib/
+if os.environ.get("KNN_AMD_VARIANT"):
+    LIB_PATH = os.path.join(HERE, "lib", "libknn_amd_%s.so" % os.environ["KNN_AMD_VARIANT"])
 DRIVER_PATH = os.path.join(HERE, "bin", "knn_mpi_amd")
 
 L2, L1 = 0, 1

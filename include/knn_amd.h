@@ -172,7 +172,7 @@ int knn_set_precision(knn_ctx* ctx, int mode);
 int knn_last_candidate_path(knn_ctx* ctx);
 
 /* Tuning overrides for experiments (0 = automatic): "R" list entries per
- * lane (8, 16), "S" train splits per query tile (1..64), "nw" waves per
+ * lane (4, 8, 16), "S" train splits per query tile (1..64), "nw" waves per
  * candidate workgroup (4 or 8; 32 queries per wave), "ablate" (timing-only
  * kernel ablations; results invalid). */
 int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value);
