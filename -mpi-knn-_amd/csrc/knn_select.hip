@@ -54,122 +54,237 @@ __device__ void finish_partial(int64_t q, const double* dk, const int* di, const
 }
 
 // --------------------------------------------- merge + exact re-rank
-// One wave per query.  Dynamic LDS: dk[C2] f64 | di[C2] | ls[C2] | uk[U2] f32 | ui[U2].
-template <int METRIC>
-__global__ void __launch_bounds__(64)
-merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, int U, int U2,
-                    int R, TrainDev t, const double* __restrict__ Q64, int W, int C, int C2,
+// One block per query (NT = 64 or 256 threads).
+//  1. wave 0 holds the union of the 2S lists in registers (EPL per lane),
+//     finds the W-th smallest proxy v_W by a 32-step radix select on the
+//     order-preserving key bits (ballot counts, no sort), and selects every
+//     row with proxy <= v_W + 2E: only those can beat the W-th exact
+//     distance (|proxy + ||q'||^2 - d^2| <= E for every row), so the re-rank
+//     set adapts to the certified error instead of a fixed 2W.
+//     LB = min(first unselected proxy, min over lists of the R-th entry) is a
+//     lower bound on the proxy of every row not re-ranked.
+//  2. exact fp64 reference distances of the selected rows: rows are read
+//     coalesced (16 lanes per 128-B row piece) into an LDS tile of squared
+//     differences, then each thread adds its candidate's terms in dimension
+//     order -- bit-exact with cpp:33-50 / cpp:51-67 (sequential, no FMA).
+//  3. sort (dist, idx), certify LB + ||q'||^2 - E > d_W^2, vote / output.
+// Dynamic LDS: qv[d] f64 (d <= kMergeLdsDim) | dk[C2] f64 | tb[NT][17] f64 |
+// di[C2] | ls[C2].
+constexpr int kMergeLdsDim = 4096;
+__device__ __forceinline__ uint32_t f2key(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return u ^ ((u >> 31) ? 0xFFFFFFFFu : 0x80000000u);
+}
+__device__ __forceinline__ float key2f(uint32_t k) {
+  return __uint_as_float((k >> 31) ? (k ^ 0x80000000u) : ~k);
+}
+__device__ __forceinline__ int lanes_below(unsigned long long mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+}
+
+template <int METRIC, int NT, int EPL>
+__global__ void __launch_bounds__(NT)
+merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, int U, int R,
+                    TrainDev t, const double* __restrict__ Q64, int W, int Cmax, int C2,
                     double f_err, Sink sink, int* __restrict__ rescan_q,
                     int* __restrict__ rescan_cnt) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  double* dk = (double*)smem;
-  int* di = (int*)(dk + C2);
-  int* ls = di + C2;
-  float* uk = (float*)(ls + C2);
-  int* ui = (int*)(uk + U2);
-  const int64_t q = blockIdx.x;
-  const int lane = threadIdx.x;
+  __shared__ int s_cn, s_cert;
+  __shared__ float s_lb;
+  __shared__ double s_qa, s_e;
   const int d = t.d;
+  // the query row is staged in LDS up to kMergeLdsDim dims, else read in place
+  const bool q_in_lds = d <= kMergeLdsDim;
+  double* dk = (double*)smem + (q_in_lds ? d : 0);
+  double* tb = dk + C2;
+  int* di = (int*)(tb + NT * 17);
+  int* ls = di + C2;
+  const int64_t q = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
 
-  // 1. union of the 2S lists; min over lists of their worst kept entry
-  const float* lv = cv + q * U;
-  const int* li = ci + q * U;
-  float mlr = KNN_INF_F;
-  for (int e = lane; e < U2; e += 64) {
-    float v = KNN_INF_F;
-    int id = INT_MAX;
-    if (e < U) {
-      v = lv[e];
-      if (v < KNN_INF_F) id = li[e];
-      if ((e % R) == R - 1) mlr = fminf(mlr, v);
-    }
-    uk[e] = v;
-    ui[e] = id;
-  }
-  mlr = wave_min(mlr);
-  bitonic_sort_lds(uk, ui, U2, lane, 64);
-  int nv = 0;
-  for (int e = lane; e < U2; e += 64) nv += (uk[e] < KNN_INF_F);
-  nv = wave_sum_i(nv);
-
-  // 2. best C by the fp32 proxy; lower bound of every row not re-ranked
-  const int Cn = min(C, nv);
-  const float T = Cn < nv ? uk[Cn] : KNN_INF_F;
-  const float LBa = fminf(T, mlr);
-
-  // 3. exact fp64 distances for the C best, sorted by (dist, idx)
   const double* qrow = Q64 + q * d;
-  for (int c = lane; c < C2; c += 64) {
-    double v = KNN_INF_D;
-    int id = INT_MAX;
-    if (c < Cn) {
-      id = ui[c];
-      v = exact_dist<METRIC>(qrow, t.X64 + (int64_t)id * d, d);
-    }
-    dk[c] = v;
-    di[c] = id;
-  }
-  bitonic_sort_lds(dk, di, C2, lane, 64);
+  const double* qv = q_in_lds ? (const double*)smem : qrow;
+  if (q_in_lds)
+    for (int c = tid; c < d; c += NT) ((double*)smem)[c] = qrow[c];
+  __syncthreads();
 
-  // 4. certification: every excluded row has proxy >= LBa, so its exact
-  //    distance is >= the bound below (rigorous fp32 error bound f_err).
-  bool cert;
-  if (!(LBa < KNN_INF_F)) {
-    cert = true;  // every row was re-ranked exactly
-  } else if (Cn < W) {
-    cert = false;
-  } else {
+  if (tid < 64) {
+    // error bound of this query's proxies (the candidate operands are centred)
     double qa = 0.0;
     for (int c = lane; c < d; c += 64) {
-      const double x = qrow[c] - t.mu[c];  // centred like the candidate operands
+      const double x = qv[c] - t.mu[c];
       qa += METRIC == 0 ? x * x : __builtin_fabs(x);
     }
     qa = wave_sum_d(qa) * (1.0 + 1e-12);
-    const double dw = dk[W - 1];
-    if (METRIC == 0) {
-      const double E = f_err * (t.x2max + 2.1 * __builtin_sqrt(qa) * __builtin_sqrt(t.x2max)) + 1e-30;
-      const double bound = ((double)LBa + qa * (1.0 - 2e-12) - E) * (1.0 - 1e-12);
-      cert = bound > dw * dw * (1.0 + 1e-12);
-    } else {
-      const double E = f_err * (qa + t.x1max) + 1e-30;
-      const double bound = ((double)LBa - E) * (1.0 - 1e-12);
-      cert = bound > dw * (1.0 + 1e-12);
+    const double E =
+        (METRIC == 0 ? f_err * (t.x2max + 2.1 * __builtin_sqrt(qa) * __builtin_sqrt(t.x2max))
+                     : f_err * (qa + t.x1max)) + 1e-30;
+    // union in registers; min over full lists of their R-th (worst kept) entry
+    const float* lv = cv + q * U;
+    const int* li = ci + q * U;
+    float v[EPL];
+    int id[EPL];
+    float mlr = KNN_INF_F;
+    int nv = 0;
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) {
+      const int x = lane + 64 * e;
+      v[e] = KNN_INF_F;
+      id[e] = -1;
+      if (x < U) {
+        v[e] = lv[x];
+        id[e] = li[x];
+        if (x % R == R - 1) mlr = fminf(mlr, v[e]);
+      }
+      nv += __popcll(__ballot(v[e] < KNN_INF_F));
+    }
+    mlr = wave_min(mlr);
+    double tsel = KNN_INF_D;  // select proxies <= tsel
+    if (nv > W) {
+      uint32_t pre = 0;  // radix select: key of the W-th smallest proxy
+      for (int b = 31; b >= 0; --b) {
+        const uint32_t T = pre | ((1u << b) - 1u);
+        int cnt = 0;
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) cnt += __popcll(__ballot(f2key(v[e]) <= T));
+        if (cnt < W) pre |= 1u << b;
+      }
+      const double vw = (double)key2f(pre);
+      tsel = vw + 2.0 * E + 1e-9 * (__builtin_fabs(vw) + qa + E) + 1e-300;
+    }
+    float lbx = KNN_INF_F;
+    int cn = 0;
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) {
+      const bool valid = v[e] < KNN_INF_F;
+      const bool sel = valid && (double)v[e] <= tsel;
+      if (valid && !sel) lbx = fminf(lbx, v[e]);
+      const unsigned long long mk = __ballot(sel);
+      if (sel) {
+        const int pos = cn + lanes_below(mk);
+        if (pos < Cmax) di[pos] = id[e];
+      }
+      cn += __popcll(mk);
+    }
+    lbx = wave_min(lbx);
+    if (lane == 0) {
+      s_cn = cn;
+      s_lb = fminf(lbx, mlr);
+      s_qa = qa;
+      s_e = E;
     }
   }
-  if (!cert) {
-    if (lane == 0) {
-      const int s = atomicAdd(rescan_cnt, 1);
-      rescan_q[s] = (int)q;
-    }
+  __syncthreads();
+  const int cn = s_cn;
+  if (cn > Cmax) {  // re-rank set beyond this launch's capacity: exact rescan
+    if (tid == 0) rescan_q[atomicAdd(rescan_cnt, 1)] = (int)q;
     return;
   }
 
-  // 5. outputs
-  const int need = sink.mode == MODE_SINGLE ? sink.k : sink.w;
-  for (int c = lane; c < need && c < Cn; c += 64) ls[c] = t.lab[di[c]];
+  // exact distances, NT candidates per batch, 16 dims per LDS tile
+  for (int b0 = 0; b0 < cn; b0 += NT) {
+    const int nb = min(NT, cn - b0);
+    double r = 0.0;
+    for (int c0 = 0; c0 < d; c0 += 16) {
+      const int nd = min(16, d - c0);
+      for (int e = tid; e < nb * 16; e += NT) {
+        const int c = e >> 4, j = e & 15;
+        double val = 0.0;
+        if (j < nd) {
+          const double x = t.X64[(int64_t)di[b0 + c] * d + c0 + j];
+          const double tq = qv[c0 + j] - x;
+          val = METRIC == 0 ? tq * tq : __builtin_fabs(tq);
+        }
+        tb[c * 17 + j] = val;
+      }
+      __syncthreads();
+      if (tid < nb) {
+        const double* row = tb + tid * 17;
+        if (nd == 16) {
+#pragma unroll
+          for (int j = 0; j < 16; ++j) r = r + row[j];
+        } else {
+          for (int j = 0; j < nd; ++j) r = r + row[j];
+        }
+      }
+      __syncthreads();
+    }
+    if (tid < nb) dk[b0 + tid] = METRIC == 0 ? __builtin_sqrt(r) : r;  // correctly rounded
+  }
+  for (int c = tid; c < C2; c += NT) {
+    if (c >= cn) {
+      dk[c] = KNN_INF_D;
+      di[c] = INT_MAX;
+    }
+  }
+  bitonic_sort_lds(dk, di, C2, tid, NT);
+
+  // certification: every row not re-ranked has proxy >= LB, hence exact
+  // distance >= the bound below (rigorous error bound E)
+  if (tid == 0) {
+    const float LB = s_lb;
+    bool cert;
+    if (!(LB < KNN_INF_F)) {
+      cert = true;  // nothing was left out: every row was re-ranked exactly
+    } else if (cn < W) {
+      cert = false;
+    } else {
+      const double dw = dk[W - 1], qa = s_qa, E = s_e;
+      if (METRIC == 0) {
+        const double bound = ((double)LB + qa * (1.0 - 2e-12) - E) * (1.0 - 1e-12);
+        cert = bound > dw * dw * (1.0 + 1e-12);
+      } else {
+        const double bound = ((double)LB - E) * (1.0 - 1e-12);
+        cert = bound > dw * (1.0 + 1e-12);
+      }
+    }
+    s_cert = cert;
+    if (!cert) rescan_q[atomicAdd(rescan_cnt, 1)] = (int)q;
+  }
   __syncthreads();
-  if (sink.mode == MODE_SINGLE)
-    finish_single(q, dk, di, ls, Cn, sink.k, sink.idx_off, 0, sink);
-  else
-    finish_partial(q, dk, di, ls, Cn, sink.w, sink.idx_off, sink);
+  if (!s_cert) return;
+
+  const int need = sink.mode == MODE_SINGLE ? sink.k : sink.w;
+  for (int c = tid; c < need && c < cn; c += NT) ls[c] = t.lab[di[c]];
+  __syncthreads();
+  if (tid < 64) {
+    if (sink.mode == MODE_SINGLE)
+      finish_single(q, dk, di, ls, cn, sink.k, sink.idx_off, 0, sink);
+    else
+      finish_partial(q, dk, di, ls, cn, sink.w, sink.idx_off, sink);
+  }
+}
+
+template <int METRIC, int NT, int EPL>
+static void launch_mr(const float* cv, const int* ci, int U, int R, const TrainDev& t,
+                      const double* Q64, int64_t m, int W, int Cmax, int C2, double f_err,
+                      const Sink& sink, int* rescan_q, int* rescan_cnt, hipStream_t s) {
+  const size_t lds = (size_t)(t.d <= kMergeLdsDim ? t.d : 0) * 8 + (size_t)C2 * 8 +
+                     (size_t)NT * 17 * 8 + (size_t)C2 * 8;
+  hipLaunchKernelGGL((merge_rerank_kernel<METRIC, NT, EPL>), dim3((unsigned)m), dim3(NT), lds, s,
+                     cv, ci, U, R, t, Q64, W, Cmax, C2, f_err, sink, rescan_q, rescan_cnt);
 }
 
 void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int R,
                          const TrainDev& t, const double* Q64, int64_t m, int W, int C,
                          double f_err, const Sink& sink, int* rescan_q, int* rescan_cnt,
                          hipStream_t s) {
-  const int U = NL * R;
-  int U2 = 1;
-  while (U2 < U) U2 <<= 1;
+  if (m <= 0) return;
+  const int U = NL * R;  // <= 2 * 64 * 16 (choose_geometry bounds S and R)
   int C2 = 1;
   while (C2 < C) C2 <<= 1;
-  const size_t lds = (size_t)C2 * (8 + 4 + 4) + (size_t)U2 * 8;
-  if (metric == 0)
-    hipLaunchKernelGGL((merge_rerank_kernel<0>), dim3((unsigned)m), dim3(64), lds, s, cv, ci, U,
-                       U2, R, t, Q64, W, C, C2, f_err, sink, rescan_q, rescan_cnt);
-  else
-    hipLaunchKernelGGL((merge_rerank_kernel<1>), dim3((unsigned)m), dim3(64), lds, s, cv, ci, U,
-                       U2, R, t, Q64, W, C, C2, f_err, sink, rescan_q, rescan_cnt);
+  const bool big = C2 > 64, wide = U > 1024;
+#define KNN_MR(M_, NT_, EPL_) \
+  launch_mr<M_, NT_, EPL_>(cv, ci, U, R, t, Q64, m, W, C, C2, f_err, sink, rescan_q, rescan_cnt, s)
+  if (metric == 0) {
+    if (big) { if (wide) KNN_MR(0, 256, 32); else KNN_MR(0, 256, 16); }
+    else { if (wide) KNN_MR(0, 64, 32); else KNN_MR(0, 64, 16); }
+  } else {
+    if (big) { if (wide) KNN_MR(1, 256, 32); else KNN_MR(1, 256, 16); }
+    else { if (wide) KNN_MR(1, 64, 32); else KNN_MR(1, 64, 16); }
+  }
+#undef KNN_MR
 }
 
 // ------------------------------------------------------ exact rescan path
