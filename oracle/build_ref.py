@@ -13,7 +13,8 @@ oracle/ref_dump.h) straight into the image's MPICH compiler wrapper
 of the reference source is written anywhere; only the binary lands in
 oracle/_ref/ (git-ignored).
 
-Usage (python):  build_ref(cfg, instrument=True) -> path to binary
+Usage (python):  build_ref(cfg, instrument=True, timing=False) -> path to binary
+(timing=True adds a timer around the test-query loop, see sed_script)
 CLI:             python oracle/build_ref.py dim=16 K=5 N_train=10000 ...
 """
 import hashlib
@@ -37,7 +38,7 @@ def _c(v):
     return str(int(v))
 
 
-def sed_script(cfg, instrument):
+def sed_script(cfg, instrument, timing=False):
     s = []
     # cpp:108-116 -- the constant block (each line is "\t<name> = <value>; //...").
     for name, default in DEFAULTS.items():
@@ -48,6 +49,15 @@ def sed_script(cfg, instrument):
               "-e", r"s/d2\[j\]\.label = Train_label\[j\];/&  d2[j].idx = j;/",  # cpp:362
               "-e", r's/sort(d1, d1 + N_train, Comp);/& KNN_DUMP(d1, "val", myid * batch_val + i);/',
               "-e", r's/sort(d2, d2 + N_train, Comp);/& KNN_DUMP(d2, "test", myid * batch_test + i);/']
+    if timing:
+        # wall time of the test-query loop alone (cpp:352-382), max over ranks
+        # via barriers, printed by rank 0: the compute-only rate of the
+        # reference, without its CSV parse and MPI_Bcast of the train set
+        s += ["-e", r"s/^\(\s*\)train_data_dis\* d2;/\1MPI_Barrier(MPI_COMM_WORLD); "
+                    r"double knn_tq0 = MPI_Wtime(); train_data_dis* d2;/",
+              "-e", r"s/^\(\s*\)MPI_Gather(Test_label_buffer/\1MPI_Barrier(MPI_COMM_WORLD); "
+                    r"if (!myid) printf(\"KNN_TEST_LOOP_SECONDS %.6f\\n\", MPI_Wtime() - knn_tq0); "
+                    r"MPI_Gather(Test_label_buffer/"]
     return s
 
 
@@ -55,17 +65,18 @@ def ref_available():
     return os.path.exists(REF) and os.path.exists(MPICXX)
 
 
-def build_ref(cfg=None, instrument=True, force=False):
+def build_ref(cfg=None, instrument=True, force=False, timing=False):
     full = dict(DEFAULTS)
     full.update(cfg or {})
-    tag = hashlib.sha1(repr(sorted(full.items())).encode() + bytes([instrument])).hexdigest()[:12]
+    flags = bytes([instrument]) + (b"t" if timing else b"")
+    tag = hashlib.sha1(repr(sorted(full.items())).encode() + flags).hexdigest()[:12]
     os.makedirs(OUT, exist_ok=True)
     exe = os.path.join(OUT, "knn_ref_" + tag)
     if os.path.exists(exe) and not force:
         return exe
     if not ref_available():
         raise FileNotFoundError("reference source or MPICH wrapper missing")
-    sed = subprocess.run(["sed"] + sed_script(full, instrument) + [REF],
+    sed = subprocess.run(["sed"] + sed_script(full, instrument, timing) + [REF],
                          check=True, capture_output=True)
     src = sed.stdout
     # every substitution must have hit exactly once
@@ -75,6 +86,8 @@ def build_ref(cfg=None, instrument=True, force=False):
             raise RuntimeError("constant substitution failed for " + name)
     if instrument and src.count(b"KNN_DUMP(") != 2:
         raise RuntimeError("instrumentation substitution failed")
+    if timing and src.count(b"KNN_TEST_LOOP_SECONDS") != 1:
+        raise RuntimeError("timing substitution failed")
     env = dict(os.environ, MPICH_CXX="g++")
     cmd = [MPICXX, "-O2", "-w", "-x", "c++"]
     if instrument:
