@@ -87,7 +87,10 @@ int knn_create(knn_ctx** out, int device) {
   HIP_TRY(hipSetDevice(device));
   knn_ctx* c = new knn_ctx();
   c->device = device;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  // a blocking stream: ordered after work the caller queued on the legacy
+  // default stream (e.g. torch producing the device inputs), so device
+  // pointers handed to *_device calls with stream = NULL are safe to read
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamDefault) != hipSuccess) {
     delete c;
     return knn_fail(KNN_ERR_DEVICE, "hipStreamCreate failed");
   }

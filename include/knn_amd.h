@@ -39,7 +39,8 @@
  * (cpp:127-129).  One host thread per context; contexts are independent.
  * "Host" pointers are ordinary CPU memory; "_device" variants take device
  * pointers on the context's GPU and an optional hipStream_t (NULL = the
- * context's own stream).
+ * context's own stream, which is ordered after work on the device's legacy
+ * default stream; work on other streams must be synchronised by the caller).
  */
 #ifndef KNN_AMD_H
 #define KNN_AMD_H

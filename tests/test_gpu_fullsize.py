@@ -1,0 +1,213 @@
+"""Parity at BASELINE.json's full sizes, through the C ABI.
+
+configs[1] (cfg2: 1M train x 10k queries, d=128, k=10) in full; configs[2]'s
+per-GPU shard of the 1M-query job; configs[4] (cfg5: 1M x d=960, k=100) with
+2,000 of its queries; configs[3]'s train-sharded decomposition (two shards +
+k-way merge) at 10M rows.  The oracle (oracle/knn_oracle.cpp, pinned to the
+reference's own outputs) finishes only a few of these queries in seconds, so
+the checks are:
+  * oracle, bit for bit (labels, neighbour indices, fp64 distances), on a
+    sample of queries;
+  * for every checked query, size-independent properties:
+      - each reported distance IS the reference formula for that train row
+        (cpp:33-50: (q_i - x_i)^2 added sequentially in fp64, then sqrt),
+        recomputed on the host in the same operation order -- bit-exact;
+      - distances ascending, indices distinct;
+      - the label is the reference's first-to-max vote (cpp:324-337) over
+        the reported neighbours' labels;
+  * optimality against an independent fp64 brute force on the GPU
+    (fp64 GEMM form) on a query sample: the reported k distances equal the
+    k smallest distances over ALL train rows to within 1e-10 relative (that
+    brute force's own rounding error is ~1e-14 relative here).
+Data: bench.synth (Gaussian mixture on the 8-bit grid k/256), seeded."""
+import numpy as np
+import pytest
+import torch
+
+import bench
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def knn():
+    mod = bench.load_knn()
+    if mod.lib().knn_device_count() < 1:
+        pytest.fail("no HIP device visible: the KNN path has no CPU fallback")
+    return mod
+
+
+def classify(knn, clf, Q, k):
+    m = Q.shape[0]
+    lab = torch.empty(m, dtype=torch.int32, device=DEV)
+    idx = torch.empty((m, k), dtype=torch.int64, device=DEV)
+    dist = torch.empty((m, k), dtype=torch.float64, device=DEV)
+    flags = torch.empty(m, dtype=torch.int32, device=DEV)
+    clf.classify_device(Q.data_ptr(), m, k, knn.L2, lab.data_ptr(), idx.data_ptr(),
+                        dist.data_ptr(), flags.data_ptr())
+    clf.sync()
+    return lab.cpu().numpy(), idx.cpu().numpy(), dist.cpu().numpy(), flags.cpu().numpy()
+
+
+def ref_distances(X, Q, idx):
+    """cpp:33-50 on the host for (query, reported row) pairs: same operation order."""
+    Xn = X.cpu().numpy() if torch.is_tensor(X) else X
+    Qn = Q.cpu().numpy() if torch.is_tensor(Q) else Q
+    rows = Xn[idx]                       # [m, k, d]
+    r = np.zeros(idx.shape, np.float64)
+    for j in range(Qn.shape[1]):
+        t = Qn[:, None, j] - rows[:, :, j]
+        r = r + t * t
+    return np.sqrt(r)
+
+
+def vote(nlab, k):
+    """cpp:324-337 over each row of neighbour labels."""
+    out = np.empty(nlab.shape[0], np.int32)
+    for q in range(nlab.shape[0]):
+        cnt, best, bl = {}, 0, -1
+        for t in range(k):
+            lb = int(nlab[q, t])
+            cnt[lb] = cnt.get(lb, 0) + 1
+            if cnt[lb] > best:
+                best, bl = cnt[lb], lb
+        out[q] = bl
+    return out
+
+
+def brute_force_kdist(X, Q, k, chunk=1 << 18):
+    """Independent fp64 top-k distances over all rows: ||q||^2 + ||x||^2 - 2 q.x
+    on the fp64 GEMM (hipBLAS), |error| ~ 1e-16 (||q||^2 + ||x||^2), i.e.
+    ~1e-14 relative at these distances.  (torch.cdist's non-GEMM mode is not
+    used: it returned zeros for some elements on this stack.)"""
+    qn = (Q * Q).sum(1, keepdim=True)
+    best = None
+    for c0 in range(0, X.shape[0], chunk):
+        Xc = X[c0:c0 + chunk]
+        D2 = qn + (Xc * Xc).sum(1)[None, :] - 2.0 * (Q @ Xc.T)
+        d = torch.topk(D2.clamp_(min=0.0), min(k, D2.shape[1]), dim=1, largest=False).values
+        best = d if best is None else torch.topk(torch.cat([best, d], 1), k, dim=1,
+                                                 largest=False).values
+    return best.sqrt().cpu().numpy()
+
+
+def check_properties(X, lab_all, Q, k, got, idx, dist, sample):
+    # reported distances are the reference's, bit for bit
+    want_d = ref_distances(X, Q[sample], idx[sample])
+    bad = np.nonzero(want_d.view(np.int64) != dist[sample].view(np.int64))
+    assert bad[0].size == 0, "distance not bit-exact at %d (query, pos) pairs, e.g. %s" % (
+        bad[0].size, [(int(sample[a]), int(b), int(idx[sample[a], b]), float(dist[sample[a], b]),
+                       float(want_d[a, b])) for a, b in list(zip(*bad))[:4]])
+    assert (np.diff(dist[sample], axis=1) >= 0).all(), "neighbours not ascending"
+    srt = np.sort(idx[sample], axis=1)
+    assert (np.diff(srt, axis=1) > 0).all(), "repeated neighbour"
+    labs = lab_all[idx[sample]]
+    np.testing.assert_array_equal(got[sample], vote(labs, k))
+
+
+def check_oracle(X, lab_all, Q, k, got, idx, dist, qs):
+    want, widx, wdist = oracle.knn(X.cpu().numpy(), lab_all, Q[qs].cpu().numpy(), k, True,
+                                   int(lab_all.max()) + 1, n_out=k, nthreads=16)
+    np.testing.assert_array_equal(got[qs], want)
+    assert (dist[qs].view(np.int64) == wdist.view(np.int64)).all()
+    # indices: identical except inside runs of exactly equal distances
+    for a, q in enumerate(qs):
+        if not (idx[q] == widx[a]).all():
+            for t in np.nonzero(idx[q] != widx[a])[0]:
+                assert (dist[q] == dist[q][t]).sum() > 1, "query %d: index differs without a tie" % q
+
+
+def check_optimal(X, Q, k, dist, qs):
+    bf = brute_force_kdist(X, Q[qs], k)
+    np.testing.assert_allclose(dist[qs], bf, rtol=1e-10, atol=0)
+
+
+def test_cfg2_full(knn):
+    n, m, d, k, C = 1_000_000, 10_000, 128, 10, 10
+    X, lab, Q, _ = bench.synth(n, m, d, C, 1234, 5678, DEV)
+    torch.cuda.synchronize()
+    clf = knn.Classifier(0)
+    clf.set_train_device(X.data_ptr(), lab.data_ptr(), n, d, C, keep=(X, lab))
+    got, idx, dist, flags = classify(knn, clf, Q, k)
+    lab_all = lab.cpu().numpy()
+    check_properties(X, lab_all, Q, k, got, idx, dist, np.arange(m))
+    check_oracle(X, lab_all, Q, k, got, idx, dist, np.arange(0, m, m // 32))
+    check_optimal(X, Q, k, dist, np.arange(0, m, m // 512))
+    # the fp32 candidate path gives the same exact answer
+    clf.set_precision(knn.PRECISION_FP32)
+    got32, idx32, dist32, _ = classify(knn, clf, Q, k)
+    np.testing.assert_array_equal(got32, got)
+    assert (dist32.view(np.int64) == dist.view(np.int64)).all()
+    clf.close()
+
+
+def test_cfg3_shard_1m_queries(knn):
+    """configs[2]: one GPU's 1M-query shard against the 1M-row train set."""
+    n, m, d, k, C = 1_000_000, 1_000_000, 128, 10, 10
+    X, lab, Q, _ = bench.synth(n, m, d, C, 1234, 91011, DEV)
+    torch.cuda.synchronize()
+    clf = knn.Classifier(0)
+    clf.set_train_device(X.data_ptr(), lab.data_ptr(), n, d, C, keep=(X, lab))
+    got, idx, dist, flags = classify(knn, clf, Q, k)
+    lab_all = lab.cpu().numpy()
+    rng = np.random.default_rng(3)
+    sample = np.sort(rng.choice(m, 20_000, replace=False))
+    check_properties(X, lab_all, Q, k, got, idx, dist, sample)
+    check_oracle(X, lab_all, Q, k, got, idx, dist, sample[::1250])
+    check_optimal(X, Q, k, dist, sample[::40])
+    clf.close()
+
+
+def test_cfg5_d960_k100(knn):
+    n, m, d, k, C = 1_000_000, 2_000, 960, 100, 10
+    X, lab, Q, _ = bench.synth(n, m, d, C, 4321, 8765, DEV)
+    torch.cuda.synchronize()
+    clf = knn.Classifier(0)
+    clf.set_train_device(X.data_ptr(), lab.data_ptr(), n, d, C, keep=(X, lab))
+    got, idx, dist, flags = classify(knn, clf, Q, k)
+    assert clf.last_candidate_path() == 2, "cfg5 should run the bf16x3 candidate pass"
+    lab_all = lab.cpu().numpy()
+    sample = np.arange(0, m, 4)
+    check_properties(X, lab_all, Q, k, got, idx, dist, sample)
+    check_oracle(X, lab_all, Q, k, got, idx, dist, np.arange(0, m, m // 8))
+    check_optimal(X, Q, k, dist, np.arange(0, m, m // 128))
+    clf.close()
+
+
+def test_cfg4_train_sharded_merge(knn):
+    """configs[3]'s decomposition (per-shard exact top-(k+1), all-gather layout,
+    k-way merge + vote) with two shards of a 10M x 96 train set on one GPU."""
+    n, m, d, k, C = 10_000_000, 2_000, 96, 10, 10
+    X, lab, Q, _ = bench.synth(n, m, d, C, 2468, 1357, DEV)
+    torch.cuda.synchronize()
+    w = k + 1
+    half = n // 2
+    gd = torch.empty((2, m, w), dtype=torch.float64, device=DEV)
+    gi = torch.empty((2, m, w), dtype=torch.int64, device=DEV)
+    gl = torch.empty((2, m, w), dtype=torch.int32, device=DEV)
+    ctxs = [knn.Classifier(0), knn.Classifier(0)]
+    for p, c in enumerate(ctxs):
+        Xs, Ls = X[p * half:(p + 1) * half], lab[p * half:(p + 1) * half]
+        c.set_train_device(Xs.data_ptr(), Ls.data_ptr(), half, d, C, idx_offset=p * half,
+                           keep=(Xs, Ls))
+        c.search_partial_device(Q.data_ptr(), m, w, knn.L2, gd[p].data_ptr(), gi[p].data_ptr(),
+                                gl[p].data_ptr())
+        c.sync()
+    ol = torch.empty(m, dtype=torch.int32, device=DEV)
+    oi = torch.empty((m, k), dtype=torch.int64, device=DEV)
+    od = torch.empty((m, k), dtype=torch.float64, device=DEV)
+    of = torch.empty(m, dtype=torch.int32, device=DEV)
+    torch.cuda.synchronize()
+    ctxs[0].merge_vote_device(gd.data_ptr(), gi.data_ptr(), gl.data_ptr(), 2, m, w, k,
+                              ol.data_ptr(), oi.data_ptr(), od.data_ptr(), of.data_ptr())
+    ctxs[0].sync()
+    got, idx, dist = ol.cpu().numpy(), oi.cpu().numpy(), od.cpu().numpy()
+    lab_all = lab.cpu().numpy()
+    check_properties(X, lab_all, Q, k, got, idx, dist, np.arange(m))
+    check_oracle(X, lab_all, Q, k, got, idx, dist, np.arange(0, m, m // 8))
+    check_optimal(X, Q, k, dist, np.arange(0, m, m // 128))
+    for c in ctxs:
+        c.close()
