@@ -344,6 +344,10 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   if ((rc = ctx->Q32.ensure((size_t)m_pad * DP * sizeof(float)))) return rc;
   if ((rc = ctx->cand_v.ensure((size_t)m_pad * NL * R * sizeof(float)))) return rc;
   if ((rc = ctx->cand_i.ensure((size_t)m_pad * NL * R * sizeof(int)))) return rc;
+  // per-query global thresholds of the resident candidate kernel
+  // (tuning switch "ablate" bit 2 turns the exchange off; results stay exact)
+  const bool use_gthr = DP <= 256 && !(ctx->tune_ablate & 4);
+  if (use_gthr && (rc = ctx->gthr.ensure((size_t)m_pad * 4 * sizeof(uint32_t)))) return rc;
   if ((rc = ctx->rescan_q.ensure((size_t)m * sizeof(int) + 16))) return rc;
   if ((rc = ctx->rescan_cnt.ensure(16))) return rc;
 
@@ -379,6 +383,8 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   cl.out_i = (int*)ctx->cand_i.p;
   cl.ablate = ctx->tune_ablate;
   cl.nw = nw;
+  cl.gthr = use_gthr ? (uint32_t*)ctx->gthr.p : nullptr;
+  if (use_gthr) launch_fill_i32((int32_t*)ctx->gthr.p, m_pad * 4, (int32_t)kGthrInit, s);
   if (s3)
     launch_cand_s3((const unsigned short*)ctx->XB.p, (const float*)ctx->XS.p,
                    (const unsigned short*)ctx->Q32.p, DP, n_pad3, R, S, n_qt, cl.out_v, cl.out_i,
@@ -389,7 +395,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   if (tm) HIP_TRY(hipEventRecord(ctx->ev[2], s));
   HIP_TRY(hipMemsetAsync(ctx->rescan_cnt.p, 0, sizeof(int), s));
   launch_merge_rerank(metric, (const float*)ctx->cand_v.p, (const int*)ctx->cand_i.p, NL, R, t, dQ,
-                      m, W, C, err_factor(kmetric, DP), sink, (int*)ctx->rescan_q.p,
+                      m, W, C, err_factor(kmetric, DP), cl.gthr, sink, (int*)ctx->rescan_q.p,
                       (int*)ctx->rescan_cnt.p, s);
   HIP_TRY(hipGetLastError());
   if (tm) HIP_TRY(hipEventRecord(ctx->ev[3], s));

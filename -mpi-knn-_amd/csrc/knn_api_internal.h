@@ -38,13 +38,13 @@ struct knn_ctx {
   // train-side HBM
   DevBuf X64_own, lab_own, X32, xl2, xl1, stats, XB, XS, mu, mu_part;
   // per-classify workspace
-  DevBuf Q64, Q32, cand_v, cand_i, rescan_q, rescan_cnt, ra_k, ra_i, rb_k, rb_i;
+  DevBuf Q64, Q32, cand_v, cand_i, gthr, rescan_q, rescan_cnt, ra_k, ra_i, rb_k, rb_i;
   // host-API outputs
   DevBuf o_lab, o_idx, o_dist, o_flags;
   // normalisation: per-thread partial max/min, bounds, host-API staging
   DevBuf nrm_part, nrm_mm, nrm_X;
   std::vector<DevBuf*> all_bufs() {
-    return {&X64_own, &lab_own, &X32, &xl2, &xl1, &stats, &XB, &XS, &mu, &mu_part, &Q64, &Q32, &cand_v, &cand_i,
+    return {&X64_own, &lab_own, &X32, &xl2, &xl1, &stats, &XB, &XS, &mu, &mu_part, &Q64, &Q32, &cand_v, &cand_i, &gthr,
             &rescan_q, &rescan_cnt, &ra_k, &ra_i, &rb_k, &rb_i, &o_lab, &o_idx, &o_dist,
             &o_flags, &nrm_part, &nrm_mm, &nrm_X};
   }

@@ -182,10 +182,10 @@ cand_stream_kernel(const float* __restrict__ X32, const float* __restrict__ xini
       }
     }
     if (c == nch - 1) {
-      select_block<R>(acc0, t * TRS + 0, h, L, I, thr);
-      select_block<R>(acc1, t * TRS + 32, h, L, I, thr);
-      select_block<R>(acc2, t * TRS + 64, h, L, I, thr);
-      select_block<R>(acc3, t * TRS + 96, h, L, I, thr);
+      select_block<R>(acc0, t * TRS + 0, h, L, I, thr, KNN_INF_F);
+      select_block<R>(acc1, t * TRS + 32, h, L, I, thr, KNN_INF_F);
+      select_block<R>(acc2, t * TRS + 64, h, L, I, thr, KNN_INF_F);
+      select_block<R>(acc3, t * TRS + 96, h, L, I, thr, KNN_INF_F);
     }
     if (more) KNN_SSTORE(st + 1, (st + 1) & 1);
     __syncthreads();
@@ -314,7 +314,8 @@ cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* 
     if (c == nch - 1) {
       if (!(abl & 2)) {
 #pragma unroll
-        for (int bb = 0; bb < 8; ++bb) select_block<R>(acc[bb], t * kS3R + 32 * bb, h, L, I, thr);
+        for (int bb = 0; bb < 8; ++bb)
+          select_block<R>(acc[bb], t * kS3R + 32 * bb, h, L, I, thr, KNN_INF_F);
       } else if (acc[0][0] == 1234.5f && acc[7][15] == 1234.5f) {
         thr = acc[3][7];  // keep the accumulators live
       }

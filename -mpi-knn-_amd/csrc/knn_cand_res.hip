@@ -14,6 +14,16 @@ __device__ __forceinline__ void wait_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
+// The wait count plus `extra` younger exchange ops (see cand_kernel).
+template <int BASE>
+__device__ __forceinline__ void wait_barrier_x(int extra) {
+  if (extra == 2) wait_barrier<BASE + 2>();
+  else if (extra == 1) wait_barrier<BASE + 1>();
+  else wait_barrier<BASE>();
+}
+
+constexpr int kPubEvery = 8;  // tiles between global-threshold exchanges
+
 // Train rows in HBM (X32 for fp32/L1, XB for bf16x3) share one padded row
 // format of RSF = DP + 4 floats: [payload (DP floats) | ||x32||^2, l1 seed,
 // 0, 0], where payload is DP fp32 values or [hi(DP) | lo(DP)] bf16.  A tile
@@ -45,7 +55,8 @@ __device__ __forceinline__ void wait_barrier() {
 template <int DP, int R, int METRIC, int NW>
 __global__ void __launch_bounds__(NW * 64)
 cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
-            int n_qt, float* __restrict__ out_v, int* __restrict__ out_i, int abl) {
+            int n_qt, float* __restrict__ out_v, int* __restrict__ out_i, int abl,
+            uint32_t* gthr) {
   // Q32 is deliberately not __restrict__: with it hipcc treats the query
   // fragments as invariant and re-loads them inside the tile loop instead of
   // keeping them in VGPRs (its waits would then also drain the LDS-DMA queue).
@@ -111,6 +122,31 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   for (int t = 0; t < R; ++t) { L[t] = KNN_INF_F; I[t] = -1; }
   float thr = KNN_INF_F;
 
+  // Global per-query threshold.  The query's lists are spread over S
+  // workgroups; they form 4 groups by split % 4, and slot g of gthr[query]
+  // holds the min over group g's published list thresholds (order-preserving
+  // keys, atomicMin).  Each slot is a list's R-th entry, so group g has a list
+  // with R rows at or below it, and tq = max over the 4 slots has >= 4R
+  // distinct rows at or below it: any row above tq is outside the query's 4R
+  // best and may be dropped.  The merge bounds dropped rows by the final tq.
+  // Lists then stop filling with rows only a cold list would keep -- the
+  // insertions (64 independent lists per wave) that dominate the epilogue.
+  // The 4 slots come back by LDS-DMA into this wave's 1-KiB area of gls
+  // (16 B per lane) and are read after the next barrier: a plain load into
+  // VGPRs would be consumed (or copied) by compiler code before it lands.
+  __shared__ __attribute__((aligned(16))) u32x4 gls[NW * 64];
+  const uint32_t gls_addr =
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) u32x4*)gls + wv * 1024;
+  // An exchange at tile e issues (after that tile's DMA pieces) an atomic
+  // (only if some lane improved) and the slot fetch; the barriers of tiles
+  // e+1 .. e+PD-1 leave those x ops in flight (counted wait + x), the
+  // barrier of tile e+PD retires them and the slots are read after it -- no
+  // barrier ever waits on a (contended) atomic.
+  const uint32_t goff = (uint32_t)(qg * 16);  // byte offset of gthr[query][0]
+  float tq = KNN_INF_F;
+  uint32_t last_pub = kKeyInf;
+  int x_ops = 0, x_age = -1;  // ops of the pending exchange, tiles since it
+
   const int my_nt = split < n_tiles ? (n_tiles - split + S - 1) / S : 0;
 
   // ---- staging: this wave's LDS-DMA pieces i = wv, wv+NW, ... of tile t ->
@@ -145,15 +181,43 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       // read can be hoisted above the barrier (a bare s_barrier builtin does
       // not order memory) and no vmcnt(0) drains the in-flight tiles.
       const int ahead = min(PD - 1, my_nt - 1 - it);
+      if (x_age >= 0) ++x_age;
+      const int extra = (x_age >= 1 && x_age <= PD - 1) ? x_ops : 0;
       if (ahead >= 2 && PD >= 3) {
-        if (g_hi) wait_barrier<2 * G_HI>(); else wait_barrier<2 * G_LO>();
+        if (g_hi) wait_barrier_x<2 * G_HI>(extra); else wait_barrier_x<2 * G_LO>(extra);
       } else if (ahead == 1) {
-        if (g_hi) wait_barrier<G_HI>(); else wait_barrier<G_LO>();
+        if (g_hi) wait_barrier_x<G_HI>(extra); else wait_barrier_x<G_LO>(extra);
       } else {
-        wait_barrier<0>();
+        wait_barrier_x<0>(extra);
       }
       __builtin_amdgcn_sched_barrier(0);
       if (it + PD < my_nt && !(abl & 1)) KNN_ISSUE(t + PD * S, nxt);
+      if (gthr) {
+        if (x_age == PD) {
+          const u32x4 gv = gls[wv * 64 + lane];
+          tq = key2f(max(max(gv.x, gv.y), max(gv.z, gv.w)));
+          x_age = -1;
+        }
+        if ((it & (kPubEvery - 1)) == kPubEvery - 1 && it + PD < my_nt) {
+          // publish the better of the lane pair's two list thresholds (one
+          // lane per pair, only when it improved), fetch the query's 4 slots
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(thr),
+                                                           __float_as_uint(thr), false, false);
+          const uint32_t pk = f2key(fminf(__uint_as_float(sw[0]), __uint_as_float(sw[1])));
+          const bool pub = h == 0 && pk < last_pub;
+          x_ops = 1;
+          if (__ballot(pub)) {
+            if (pub)
+              asm volatile("global_atomic_umin %0, %1, %2" ::"v"(goff), "v"(pk),
+                           "s"(gthr + (split & 3))
+                           : "memory");
+            x_ops = 2;
+          }
+          if (pub) last_pub = pk;
+          glds16((const char*)gthr + goff, gls_addr);
+          x_age = 0;
+        }
+      }
     }
     const float* base = lds + cur * BUFF;
 
@@ -205,7 +269,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       }
     }
 
-    if (!(abl & 2)) select_block<R>(acc, t * kTR, h, L, I, thr);
+    if (!(abl & 2)) select_block<R>(acc, t * kTR, h, L, I, thr, tq);
     else if (acc[0] == 1234.5f && acc[15] == 1234.5f) thr = acc[7];  // keep acc live
     if (++cur == NB) cur = 0;
     if (++nxt == NB) nxt = 0;
@@ -236,7 +300,7 @@ template <int DP, int R, int METRIC, int NW>
 static void launch_res(const CandLaunch& c, hipStream_t s) {
   hipLaunchKernelGGL((cand_kernel<DP, R, METRIC, NW>), dim3((unsigned)(c.n_qt * c.S)),
                      dim3(NW * 64), 0, s, c.X32, c.Q32, (int)(c.n_pad / kTR), c.S, c.n_qt,
-                     c.out_v, c.out_i, c.ablate);
+                     c.out_v, c.out_i, c.ablate, c.gthr);
 }
 
 // Instantiated variants: R in {4, 8, 16}; METRIC 0/2 with NW in {4, 8};

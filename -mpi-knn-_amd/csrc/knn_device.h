@@ -13,6 +13,7 @@
 namespace knnk {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 #define KNN_INF_F __builtin_inff()
@@ -163,13 +164,26 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_addr) {
       : "memory");
 }
 
+// Order-preserving float <-> uint32 keys (unsigned compares order like the
+// floats; +inf -> 0xFF800000).
+__device__ __forceinline__ uint32_t f2key(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return u ^ ((u >> 31) ? 0xFFFFFFFFu : 0x80000000u);
+}
+__device__ __forceinline__ float key2f(uint32_t k) {
+  return __uint_as_float((k >> 31) ? (k ^ 0x80000000u) : ~k);
+}
+constexpr uint32_t kKeyInf = 0xFF800000u;  // f2key(+inf)
+
 // Fused top-R selection over one 32x32 accumulator block: lane (j, h) holds
 // the values of query j against rows row0 + rho(i, h), i = 0..15.  Once the
 // list is warm this is a 16-way min (v_min3) and one compare per block; a
 // value is inserted only under a branch that no lane of the wave skips.
+// tq: an extra filter bound valid for the whole query (the global per-query
+// threshold of cand_kernel, +inf elsewhere).
 template <int R>
 __device__ __forceinline__ void select_block(const f32x16& acc, int row0, int h, float (&L)[R],
-                                             int (&I)[R], float& thr) {
+                                             int (&I)[R], float& thr, float tq) {
   // Lanes l and l^32 hold the same query: filtering with the smaller of the
   // two list thresholds is safe -- anything dropped is >= some list's final
   // R-th entry, which the merge's lower bound (min over lists) accounts for.
@@ -178,7 +192,7 @@ __device__ __forceinline__ void select_block(const f32x16& acc, int row0, int h,
   // (one VALU op instead of an LDS ds_bpermute round trip).
   const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(thr), __float_as_uint(thr),
                                                    false, false);
-  float te = __builtin_fminf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+  float te = __builtin_fminf(__builtin_fminf(__uint_as_float(sw[0]), __uint_as_float(sw[1])), tq);
   float mn = __builtin_fminf(acc[0], acc[1]);
 #pragma unroll
   for (int i = 2; i < 16; ++i) mn = __builtin_fminf(mn, acc[i]);

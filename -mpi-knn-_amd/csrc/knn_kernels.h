@@ -74,7 +74,9 @@ struct CandLaunch {
   int* out_i;
   int ablate;   // timing-only ablation bits (0 in production)
   int nw;       // resident kernel: waves (x32 queries) per workgroup, 4 or 8
+  uint32_t* gthr;  // resident kernel: per-query global thresholds [m_pad][4] (keys)
 };
+constexpr uint32_t kGthrInit = 0xFF800000u;  // order-preserving key of +inf
 
 // Candidate-pass operands are centred on the train column means mu (see knn_prep.hip).
 int col_mean_blocks(int64_t n);  // rows of the `partial` scratch (x d doubles)
@@ -86,10 +88,12 @@ void launch_prep_train(const double* X64, const double* mu, int64_t n, int d, in
 void launch_prep_queries(const double* Q64, const double* mu, int64_t m, int d, int DP,
                          int64_t m_pad, float scale, float* Q32, hipStream_t s);
 void launch_cand(const CandLaunch& c, hipStream_t s);
+// gthr: the candidate kernel's per-query global thresholds ([m_pad][4] keys)
+// or null when the kernel kept none
 void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int R,
                          const TrainDev& t, const double* Q64, int64_t m, int W, int C,
-                         double f_err, const Sink& sink, int* rescan_q, int* rescan_cnt,
-                         hipStream_t s);
+                         double f_err, const uint32_t* gthr, const Sink& sink, int* rescan_q,
+                         int* rescan_cnt, hipStream_t s);
 void launch_rescan(int metric, const TrainDev& t, const double* Q64, const int* rescan_q,
                    int f0, int nf, int W, double* pa_k, int* pa_i, double* pb_k, int* pb_i,
                    const Sink& sink, hipStream_t s);

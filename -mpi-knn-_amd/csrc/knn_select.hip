@@ -61,8 +61,9 @@ __device__ void finish_partial(int64_t q, const double* dk, const int* di, const
 //     row with proxy <= v_W + 2E: only those can beat the W-th exact
 //     distance (|proxy + ||q'||^2 - d^2| <= E for every row), so the re-rank
 //     set adapts to the certified error instead of a fixed 2W.
-//     LB = min(first unselected proxy, min over lists of the R-th entry) is a
-//     lower bound on the proxy of every row not re-ranked.
+//     LB = min(first unselected proxy, min over lists of the R-th entry,
+//     the query's final global threshold) is a lower bound on the proxy of
+//     every row not re-ranked.
 //  2. exact fp64 reference distances of the selected rows: rows are read
 //     coalesced (16 lanes per 128-B row piece) into an LDS tile of squared
 //     differences, then each thread adds its candidate's terms in dimension
@@ -71,13 +72,6 @@ __device__ void finish_partial(int64_t q, const double* dk, const int* di, const
 // Dynamic LDS: qv[d] f64 (d <= kMergeLdsDim) | dk[C2] f64 | tb[NT][17] f64 |
 // di[C2] | ls[C2].
 constexpr int kMergeLdsDim = 4096;
-__device__ __forceinline__ uint32_t f2key(float f) {
-  const uint32_t u = __float_as_uint(f);
-  return u ^ ((u >> 31) ? 0xFFFFFFFFu : 0x80000000u);
-}
-__device__ __forceinline__ float key2f(uint32_t k) {
-  return __uint_as_float((k >> 31) ? (k ^ 0x80000000u) : ~k);
-}
 __device__ __forceinline__ int lanes_below(unsigned long long mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                    __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
@@ -87,8 +81,8 @@ template <int METRIC, int NT, int EPL>
 __global__ void __launch_bounds__(NT)
 merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, int U, int R,
                     TrainDev t, const double* __restrict__ Q64, int W, int Cmax, int C2,
-                    double f_err, Sink sink, int* __restrict__ rescan_q,
-                    int* __restrict__ rescan_cnt) {
+                    double f_err, const uint32_t* __restrict__ gthr, Sink sink,
+                    int* __restrict__ rescan_q, int* __restrict__ rescan_cnt) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int s_cn, s_cert;
   __shared__ float s_lb;
@@ -168,9 +162,16 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
       cn += __popcll(mk);
     }
     lbx = wave_min(lbx);
+    // the candidate kernel also filtered with the query's global threshold
+    // (cand_kernel): rows it dropped have proxy >= its final value
+    float tq = KNN_INF_F;
+    if (gthr) {
+      const uint32_t* g = gthr + q * 4;
+      tq = key2f(max(max(g[0], g[1]), max(g[2], g[3])));
+    }
     if (lane == 0) {
       s_cn = cn;
-      s_lb = fminf(lbx, mlr);
+      s_lb = fminf(fminf(lbx, mlr), tq);
       s_qa = qa;
       s_e = E;
     }
@@ -259,24 +260,26 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
 template <int METRIC, int NT, int EPL>
 static void launch_mr(const float* cv, const int* ci, int U, int R, const TrainDev& t,
                       const double* Q64, int64_t m, int W, int Cmax, int C2, double f_err,
-                      const Sink& sink, int* rescan_q, int* rescan_cnt, hipStream_t s) {
+                      const uint32_t* gthr, const Sink& sink, int* rescan_q, int* rescan_cnt,
+                      hipStream_t s) {
   const size_t lds = (size_t)(t.d <= kMergeLdsDim ? t.d : 0) * 8 + (size_t)C2 * 8 +
                      (size_t)NT * 17 * 8 + (size_t)C2 * 8;
   hipLaunchKernelGGL((merge_rerank_kernel<METRIC, NT, EPL>), dim3((unsigned)m), dim3(NT), lds, s,
-                     cv, ci, U, R, t, Q64, W, Cmax, C2, f_err, sink, rescan_q, rescan_cnt);
+                     cv, ci, U, R, t, Q64, W, Cmax, C2, f_err, gthr, sink, rescan_q, rescan_cnt);
 }
 
 void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int R,
                          const TrainDev& t, const double* Q64, int64_t m, int W, int C,
-                         double f_err, const Sink& sink, int* rescan_q, int* rescan_cnt,
-                         hipStream_t s) {
+                         double f_err, const uint32_t* gthr, const Sink& sink, int* rescan_q,
+                         int* rescan_cnt, hipStream_t s) {
   if (m <= 0) return;
   const int U = NL * R;  // <= 2 * 64 * 16 (choose_geometry bounds S and R)
   int C2 = 1;
   while (C2 < C) C2 <<= 1;
   const bool big = C2 > 64, wide = U > 1024;
 #define KNN_MR(M_, NT_, EPL_) \
-  launch_mr<M_, NT_, EPL_>(cv, ci, U, R, t, Q64, m, W, C, C2, f_err, sink, rescan_q, rescan_cnt, s)
+  launch_mr<M_, NT_, EPL_>(cv, ci, U, R, t, Q64, m, W, C, C2, f_err, gthr, sink, rescan_q, \
+                           rescan_cnt, s)
   if (metric == 0) {
     if (big) { if (wide) KNN_MR(0, 256, 32); else KNN_MR(0, 256, 16); }
     else { if (wide) KNN_MR(0, 64, 32); else KNN_MR(0, 64, 16); }
