@@ -255,8 +255,8 @@ int knn_set_train_device(knn_ctx* ctx, const double* dX, const int32_t* dlabels,
 // kernel (occupancy x CUs): a mostly-empty final round costs up to a whole
 // workgroup duration.  The union of the 2S lists must hold the C re-rank
 // candidates; R grows to 16 when the expected per-list share of C is large.
-static void choose_geometry(knn_ctx* ctx, int metric, int DP, int nw, int n_qt, int64_t n_tiles, int C,
-                            int& S_out, int& R_out) {
+static void choose_geometry(knn_ctx* ctx, int metric, int DP, int nw, int n_qt, int64_t n_tiles,
+                            int W, int C, int& S_out, int& R_out) {
   const int S_hi = (int)std::max<int64_t>(1, std::min<int64_t>(64, n_tiles));
   int bestS = 1, bestR = 8;
   for (int R : {4, 8, 16}) {
@@ -281,9 +281,12 @@ static void choose_geometry(knn_ctx* ctx, int metric, int DP, int nw, int n_qt, 
     if (ctx->tune_S) bS = std::min(ctx->tune_S, S_hi);
     bestS = bS;
     bestR = R;
-    // expected share of the C re-rank candidates per list (2S lists): R = 8
-    // when <= 2, else 16 (certification catches the rest)
-    if (ctx->tune_R || C <= 4 * bS) break;
+    // R = 8 when the expected share of the top W per list (2S lists) is at
+    // most 2: a list overflow (-> certification fails) is then rare and the
+    // fast rescan absorbs it.  Without a fast rescan (d > kRescanFastMaxDP a
+    // rescan is a full exact scan) R = 16 unless the share is at most 1/2.
+    const bool fast_rescan = DP <= kRescanFastMaxDP;
+    if (ctx->tune_R || (fast_rescan ? W <= 4 * bS : W <= bS)) break;
   }
   S_out = bestS;
   R_out = bestR;
@@ -338,7 +341,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   int C = (int)std::min<int64_t>(t.n, std::max(2 * W, W + 16));
   C = std::min(C, kMaxUnion);
   int S = 1, R = 8;
-  choose_geometry(ctx, kmetric, DP, nw, n_qt, n_tiles, C, S, R);
+  choose_geometry(ctx, kmetric, DP, nw, n_qt, n_tiles, W, C, S, R);
   const int NL = 2 * S;
   C = std::min(C, NL * R);
   if ((rc = ctx->Q32.ensure((size_t)m_pad * DP * sizeof(float)))) return rc;
@@ -349,6 +352,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   const bool use_gthr = DP <= 256 && !(ctx->tune_ablate & 4);
   if (use_gthr && (rc = ctx->gthr.ensure((size_t)m_pad * 4 * sizeof(uint32_t)))) return rc;
   if ((rc = ctx->rescan_q.ensure((size_t)m * sizeof(int) + 16))) return rc;
+  if ((rc = ctx->rescan_tau.ensure((size_t)m * sizeof(double) + 16))) return rc;
   if ((rc = ctx->rescan_cnt.ensure(16))) return rc;
 
   ctx->last_kmetric = kmetric;
@@ -396,13 +400,14 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   HIP_TRY(hipMemsetAsync(ctx->rescan_cnt.p, 0, sizeof(int), s));
   launch_merge_rerank(metric, (const float*)ctx->cand_v.p, (const int*)ctx->cand_i.p, NL, R, t, dQ,
                       m, W, C, err_factor(kmetric, DP), cl.gthr, sink, (int*)ctx->rescan_q.p,
-                      (int*)ctx->rescan_cnt.p, s);
+                      (double*)ctx->rescan_tau.p, (int*)ctx->rescan_cnt.p, s);
   HIP_TRY(hipGetLastError());
   if (tm) HIP_TRY(hipEventRecord(ctx->ev[3], s));
   HIP_TRY(hipMemcpyAsync(ctx->h_count, ctx->rescan_cnt.p, sizeof(int), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   const int nflag = ctx->h_count[0];
   ctx->last_rescan = nflag;
+  ctx->last_slow_rescan = 0;
   if (tm) {
     float ms;
     for (int p = 0; p < 3; p++) {
@@ -412,19 +417,53 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
     ctx->phase_ms[3] = 0.0;
   }
   if (nflag > 0) {
-    const size_t per = rescan_scratch_entries(t.n, W);
-    int64_t batch = (int64_t)((256ull << 20) / (per * 12 + 1));
-    batch = std::max<int64_t>(1, std::min<int64_t>(batch, 4096));
-    batch = std::min<int64_t>(batch, nflag);
-    if ((rc = ctx->ra_k.ensure(per * batch * sizeof(double)))) return rc;
-    if ((rc = ctx->ra_i.ensure(per * batch * sizeof(int)))) return rc;
-    if ((rc = ctx->rb_k.ensure(per * batch * sizeof(double)))) return rc;
-    if ((rc = ctx->rb_i.ensure(per * batch * sizeof(int)))) return rc;
-    for (int f0 = 0; f0 < nflag; f0 += (int)batch) {
-      const int nf = (int)std::min<int64_t>(batch, nflag - f0);
-      launch_rescan(metric, t, dQ, (const int*)ctx->rescan_q.p, f0, nf, W, (double*)ctx->ra_k.p,
-                    (int*)ctx->ra_i.p, (double*)ctx->rb_k.p, (int*)ctx->rb_i.p, sink, s);
+    // fast filtered rescan (one pass over the fp32 train copy per 64 failed
+    // queries, d <= kRescanFastMaxDP); what it cannot finish goes to the full
+    // exact scan below
+    const bool fast = t.DP <= kRescanFastMaxDP;
+    const int fb = std::min(nflag, 4096);
+    if ((rc = ctx->fr_cnt.ensure((size_t)fb * sizeof(int)))) return rc;
+    if ((rc = ctx->fr_buf.ensure((size_t)fb * kRescanCap * sizeof(int)))) return rc;
+    if ((rc = ctx->fr_q.ensure((size_t)fb * (t.DP + 1) * sizeof(float)))) return rc;
+    if ((rc = ctx->slow_q.ensure((size_t)nflag * sizeof(int) + 16))) return rc;
+    // rescan_cnt is reused as the count of queries for the full scan (still
+    // nflag, with every failed query, when there is no fast path)
+    if (fast) HIP_TRY(hipMemsetAsync(ctx->rescan_cnt.p, 0, sizeof(int), s));
+    else
+      HIP_TRY(hipMemcpyAsync(ctx->slow_q.p, ctx->rescan_q.p, (size_t)nflag * sizeof(int),
+                             hipMemcpyDeviceToDevice, s));
+    for (int f0 = 0; fast && f0 < nflag; f0 += fb) {
+      const int nf = std::min(fb, nflag - f0);
+      HIP_TRY(hipMemsetAsync(ctx->fr_cnt.p, 0, (size_t)nf * sizeof(int), s));
+      launch_rescan_fast(metric, t, dQ, (const int*)ctx->rescan_q.p,
+                         (const double*)ctx->rescan_tau.p, f0, nf, W, err_factor(metric, t.DP),
+                         (float*)ctx->fr_q.p, (float*)ctx->fr_q.p + (size_t)fb * t.DP,
+                         (int*)ctx->fr_cnt.p, (int*)ctx->fr_buf.p, sink, (int*)ctx->slow_q.p,
+                         (int*)ctx->rescan_cnt.p, s);
       HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipMemcpyAsync(ctx->h_count, ctx->rescan_cnt.p, sizeof(int), hipMemcpyDeviceToHost,
+                           s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const int nslow = ctx->h_count[0];
+    ctx->last_slow_rescan = nslow;
+    if (getenv("KNN_DEBUG_RESCAN"))
+      fprintf(stderr, "[knn] %d queries not certified, %d sent to the full scan\n", nflag, nslow);
+    if (nslow > 0) {
+      const size_t per = rescan_scratch_entries(t.n, W);
+      int64_t batch = (int64_t)((256ull << 20) / (per * 12 + 1));
+      batch = std::max<int64_t>(1, std::min<int64_t>(batch, 4096));
+      batch = std::min<int64_t>(batch, nslow);
+      if ((rc = ctx->ra_k.ensure(per * batch * sizeof(double)))) return rc;
+      if ((rc = ctx->ra_i.ensure(per * batch * sizeof(int)))) return rc;
+      if ((rc = ctx->rb_k.ensure(per * batch * sizeof(double)))) return rc;
+      if ((rc = ctx->rb_i.ensure(per * batch * sizeof(int)))) return rc;
+      for (int f0 = 0; f0 < nslow; f0 += (int)batch) {
+        const int nf = (int)std::min<int64_t>(batch, nslow - f0);
+        launch_rescan(metric, t, dQ, (const int*)ctx->slow_q.p, f0, nf, W, (double*)ctx->ra_k.p,
+                      (int*)ctx->ra_i.p, (double*)ctx->rb_k.p, (int*)ctx->rb_i.p, sink, s);
+        HIP_TRY(hipGetLastError());
+      }
     }
     if (tm) {
       HIP_TRY(hipEventRecord(ctx->ev[4], s));

@@ -21,7 +21,8 @@ struct knn_ctx {
   bool trained = false;
   int class_cnt = 0;
   int64_t idx_off = 0;
-  int64_t last_rescan = 0;
+  int64_t last_rescan = 0;       // queries that failed certification
+  int64_t last_slow_rescan = 0;  // of those, queries the fast rescan passed on to the full scan
   int cu_count = 0;
   int precision = 0;     // KNN_PRECISION_*
   int DPb = 0;           // padded dim of the bf16x3 copy (0 = not built)
@@ -38,13 +39,14 @@ struct knn_ctx {
   // train-side HBM
   DevBuf X64_own, lab_own, X32, xl2, xl1, stats, XB, XS, mu, mu_part;
   // per-classify workspace
-  DevBuf Q64, Q32, cand_v, cand_i, gthr, rescan_q, rescan_cnt, ra_k, ra_i, rb_k, rb_i;
+  DevBuf Q64, Q32, cand_v, cand_i, gthr, rescan_q, rescan_tau, rescan_cnt, ra_k, ra_i, rb_k,
+      rb_i, fr_cnt, fr_buf, fr_q, slow_q;
   // host-API outputs
   DevBuf o_lab, o_idx, o_dist, o_flags;
   // normalisation: per-thread partial max/min, bounds, host-API staging
   DevBuf nrm_part, nrm_mm, nrm_X;
   std::vector<DevBuf*> all_bufs() {
-    return {&X64_own, &lab_own, &X32, &xl2, &xl1, &stats, &XB, &XS, &mu, &mu_part, &Q64, &Q32, &cand_v, &cand_i, &gthr,
+    return {&X64_own, &lab_own, &X32, &xl2, &xl1, &stats, &XB, &XS, &mu, &mu_part, &Q64, &Q32, &cand_v, &cand_i, &gthr, &rescan_tau, &fr_cnt, &fr_buf, &fr_q, &slow_q,
             &rescan_q, &rescan_cnt, &ra_k, &ra_i, &rb_k, &rb_i, &o_lab, &o_idx, &o_dist,
             &o_flags, &nrm_part, &nrm_mm, &nrm_X};
   }

@@ -90,10 +90,22 @@ void launch_prep_queries(const double* Q64, const double* mu, int64_t m, int d, 
 void launch_cand(const CandLaunch& c, hipStream_t s);
 // gthr: the candidate kernel's per-query global thresholds ([m_pad][4] keys)
 // or null when the kernel kept none
+// failed queries are appended to rescan_q with rescan_tau = the W-th exact
+// distance among their re-ranked rows (+inf if unknown)
 void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int R,
                          const TrainDev& t, const double* Q64, int64_t m, int W, int C,
                          double f_err, const uint32_t* gthr, const Sink& sink, int* rescan_q,
-                         int* rescan_cnt, hipStream_t s);
+                         double* rescan_tau, int* rescan_cnt, hipStream_t s);
+constexpr int kRescanCap = 1024;  // rows a fast rescan may append per query
+constexpr int kRescanFastMaxDP = 256;  // fast rescan: resident-kernel dimensions
+// Fast rescan of failed queries [f0, f0+nf): scratch qf[nf * t.DP], thr[nf],
+// cnt[nf] (zeroed by the caller), buf[nf * kRescanCap]; queries it cannot
+// finish land in slow_q/slow_cnt (for launch_rescan).  f_err: the fp32
+// candidate error factor of t.DP.
+void launch_rescan_fast(int metric, const TrainDev& t, const double* Q64, const int* rescan_q,
+                        const double* tau, int f0, int nf, int W, double f_err, float* qf,
+                        float* thr, int* cnt, int* buf, const Sink& sink, int* slow_q,
+                        int* slow_cnt, hipStream_t s);
 void launch_rescan(int metric, const TrainDev& t, const double* Q64, const int* rescan_q,
                    int f0, int nf, int W, double* pa_k, int* pa_i, double* pb_k, int* pb_i,
                    const Sink& sink, hipStream_t s);

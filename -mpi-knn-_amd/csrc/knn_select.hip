@@ -2,6 +2,8 @@
 // the exact rescan path and the train-sharded k-way merge (gfx950).
 #include "knn_device.h"
 
+#include <algorithm>
+
 namespace knnk {
 
 // ------------------------------------------------ finish: vote / outputs
@@ -77,12 +79,62 @@ __device__ __forceinline__ int lanes_below(unsigned long long mask) {
                                    __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
 }
 
+// Exact fp64 distances of rows di[0..cn) to the query row qv, in the
+// reference's operation order: rows are read coalesced (16 lanes per 128-B
+// row piece) into an LDS tile of squared (L1: absolute) differences, then
+// thread c adds its candidate's terms in dimension order -- bit-exact with
+// cpp:33-50 / cpp:51-67 (sequential, no FMA; sqrt correctly rounded).
+// Pads [cn, C2) with (+inf, INT_MAX) and sorts (dist, idx) ascending.
+// All NT threads; tb holds NT x 17 doubles.
+template <int METRIC, int NT>
+__device__ void exact_sorted(const TrainDev& t, const double* qv, int* di, double* dk, double* tb,
+                             int cn, int C2, int tid) {
+  const int d = t.d;
+  for (int b0 = 0; b0 < cn; b0 += NT) {
+    const int nb = min(NT, cn - b0);
+    double r = 0.0;
+    for (int c0 = 0; c0 < d; c0 += 16) {
+      const int nd = min(16, d - c0);
+      for (int e = tid; e < nb * 16; e += NT) {
+        const int c = e >> 4, j = e & 15;
+        double val = 0.0;
+        if (j < nd) {
+          const double x = t.X64[(int64_t)di[b0 + c] * d + c0 + j];
+          const double tq = qv[c0 + j] - x;
+          val = METRIC == 0 ? tq * tq : __builtin_fabs(tq);
+        }
+        tb[c * 17 + j] = val;
+      }
+      __syncthreads();
+      if (tid < nb) {
+        const double* row = tb + tid * 17;
+        if (nd == 16) {
+#pragma unroll
+          for (int j = 0; j < 16; ++j) r = r + row[j];
+        } else {
+          for (int j = 0; j < nd; ++j) r = r + row[j];
+        }
+      }
+      __syncthreads();
+    }
+    if (tid < nb) dk[b0 + tid] = METRIC == 0 ? __builtin_sqrt(r) : r;  // correctly rounded
+  }
+  for (int c = tid; c < C2; c += NT) {
+    if (c >= cn) {
+      dk[c] = KNN_INF_D;
+      di[c] = INT_MAX;
+    }
+  }
+  bitonic_sort_lds(dk, di, C2, tid, NT);
+}
+
 template <int METRIC, int NT, int EPL>
 __global__ void __launch_bounds__(NT)
 merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, int U, int R,
                     TrainDev t, const double* __restrict__ Q64, int W, int Cmax, int C2,
                     double f_err, const uint32_t* __restrict__ gthr, Sink sink,
-                    int* __restrict__ rescan_q, int* __restrict__ rescan_cnt) {
+                    int* __restrict__ rescan_q, double* __restrict__ rescan_tau,
+                    int* __restrict__ rescan_cnt) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int s_cn, s_cert;
   __shared__ float s_lb;
@@ -179,47 +231,15 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
   __syncthreads();
   const int cn = s_cn;
   if (cn > Cmax) {  // re-rank set beyond this launch's capacity: exact rescan
-    if (tid == 0) rescan_q[atomicAdd(rescan_cnt, 1)] = (int)q;
+    if (tid == 0) {
+      const int f = atomicAdd(rescan_cnt, 1);
+      rescan_q[f] = (int)q;
+      rescan_tau[f] = KNN_INF_D;
+    }
     return;
   }
 
-  // exact distances, NT candidates per batch, 16 dims per LDS tile
-  for (int b0 = 0; b0 < cn; b0 += NT) {
-    const int nb = min(NT, cn - b0);
-    double r = 0.0;
-    for (int c0 = 0; c0 < d; c0 += 16) {
-      const int nd = min(16, d - c0);
-      for (int e = tid; e < nb * 16; e += NT) {
-        const int c = e >> 4, j = e & 15;
-        double val = 0.0;
-        if (j < nd) {
-          const double x = t.X64[(int64_t)di[b0 + c] * d + c0 + j];
-          const double tq = qv[c0 + j] - x;
-          val = METRIC == 0 ? tq * tq : __builtin_fabs(tq);
-        }
-        tb[c * 17 + j] = val;
-      }
-      __syncthreads();
-      if (tid < nb) {
-        const double* row = tb + tid * 17;
-        if (nd == 16) {
-#pragma unroll
-          for (int j = 0; j < 16; ++j) r = r + row[j];
-        } else {
-          for (int j = 0; j < nd; ++j) r = r + row[j];
-        }
-      }
-      __syncthreads();
-    }
-    if (tid < nb) dk[b0 + tid] = METRIC == 0 ? __builtin_sqrt(r) : r;  // correctly rounded
-  }
-  for (int c = tid; c < C2; c += NT) {
-    if (c >= cn) {
-      dk[c] = KNN_INF_D;
-      di[c] = INT_MAX;
-    }
-  }
-  bitonic_sort_lds(dk, di, C2, tid, NT);
+  exact_sorted<METRIC, NT>(t, qv, di, dk, tb, cn, C2, tid);
 
   // certification: every row not re-ranked has proxy >= LB, hence exact
   // distance >= the bound below (rigorous error bound E)
@@ -241,7 +261,13 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
       }
     }
     s_cert = cert;
-    if (!cert) rescan_q[atomicAdd(rescan_cnt, 1)] = (int)q;
+    if (!cert) {
+      // the W-th exact distance among the re-ranked rows bounds the true
+      // W-th from above: the fast rescan keeps every row that can reach it
+      const int f = atomicAdd(rescan_cnt, 1);
+      rescan_q[f] = (int)q;
+      rescan_tau[f] = cn >= W ? dk[W - 1] : KNN_INF_D;
+    }
   }
   __syncthreads();
   if (!s_cert) return;
@@ -260,18 +286,19 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
 template <int METRIC, int NT, int EPL>
 static void launch_mr(const float* cv, const int* ci, int U, int R, const TrainDev& t,
                       const double* Q64, int64_t m, int W, int Cmax, int C2, double f_err,
-                      const uint32_t* gthr, const Sink& sink, int* rescan_q, int* rescan_cnt,
-                      hipStream_t s) {
+                      const uint32_t* gthr, const Sink& sink, int* rescan_q,
+                      double* rescan_tau, int* rescan_cnt, hipStream_t s) {
   const size_t lds = (size_t)(t.d <= kMergeLdsDim ? t.d : 0) * 8 + (size_t)C2 * 8 +
                      (size_t)NT * 17 * 8 + (size_t)C2 * 8;
   hipLaunchKernelGGL((merge_rerank_kernel<METRIC, NT, EPL>), dim3((unsigned)m), dim3(NT), lds, s,
-                     cv, ci, U, R, t, Q64, W, Cmax, C2, f_err, gthr, sink, rescan_q, rescan_cnt);
+                     cv, ci, U, R, t, Q64, W, Cmax, C2, f_err, gthr, sink, rescan_q, rescan_tau,
+                     rescan_cnt);
 }
 
 void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int R,
                          const TrainDev& t, const double* Q64, int64_t m, int W, int C,
                          double f_err, const uint32_t* gthr, const Sink& sink, int* rescan_q,
-                         int* rescan_cnt, hipStream_t s) {
+                         double* rescan_tau, int* rescan_cnt, hipStream_t s) {
   if (m <= 0) return;
   const int U = NL * R;  // <= 2 * 64 * 16 (choose_geometry bounds S and R)
   int C2 = 1;
@@ -279,7 +306,7 @@ void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int
   const bool big = C2 > 64, wide = U > 1024;
 #define KNN_MR(M_, NT_, EPL_) \
   launch_mr<M_, NT_, EPL_>(cv, ci, U, R, t, Q64, m, W, C, C2, f_err, gthr, sink, rescan_q, \
-                           rescan_cnt, s)
+                           rescan_tau, rescan_cnt, s)
   if (metric == 0) {
     if (big) { if (wide) KNN_MR(0, 256, 32); else KNN_MR(0, 256, 16); }
     else { if (wide) KNN_MR(0, 64, 32); else KNN_MR(0, 64, 16); }
@@ -288,6 +315,209 @@ void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int
     else { if (wide) KNN_MR(1, 64, 32); else KNN_MR(1, 64, 16); }
   }
 #undef KNN_MR
+}
+
+// ------------------------------------------------- fast rescan (filtered)
+// Queries whose candidate set was not certified (a list overflowed near the
+// top, heavy ties).  tau = the W-th exact distance among the query's
+// re-ranked rows, >= the true W-th.  rescan_filter streams the fp32 train
+// copy once per kFiltQ such queries (lane = train row, queries broadcast
+// from LDS) and appends every row whose centred fp32 proxy --
+// an fmaf chain with the candidate pass's certified error bound -- is within
+// reach of tau; the appended set therefore holds every row with exact
+// distance <= tau, i.e. the exact top-W with all its ties.  rescan_finish
+// re-ranks it exactly.  Unknown tau or more than kRescanCap rows: the full
+// exact scan below.
+constexpr int kFiltQ = 16;  // failed queries per filter block (LDS broadcasts)
+
+// Block = NWB waves, wave w owns the 64 consecutive train rows starting at
+// blockIdx.x*64*NWB + 64w (lane = row).  The wave copies its rows (the
+// padded fp32 X32 layout, odd 16-B stride -> conflict-free ds_read_b128) into
+// LDS by LDS-DMA, then runs kFiltQ accumulators per lane against the block's
+// queries, read as LDS broadcasts.
+// One wave per failed query: the centred fp32 query row (x -2 for L2, the
+// candidate pass's operand) and the proxy threshold every row with exact
+// distance <= tau passes (fp32 fmaf-chain error bound f_err of t.DP).
+template <int METRIC>
+__global__ void __launch_bounds__(64)
+rescan_prep_kernel(TrainDev t, const double* __restrict__ Q64, const int* __restrict__ rescan_q,
+                   const double* __restrict__ tau, int f0, double f_err, float* __restrict__ qf,
+                   float* __restrict__ thr) {
+  const int s = blockIdx.x, lane = threadIdx.x, d = t.d, DP = t.DP;
+  const double* qr = Q64 + (int64_t)rescan_q[f0 + s] * d;
+  double qa = 0.0;
+  for (int i = lane; i < DP; i += 64) {
+    float v = 0.0f;
+    if (i < d) {
+      const double x = qr[i] - t.mu[i];
+      qa += METRIC == 0 ? x * x : __builtin_fabs(x);
+      v = (float)x * (METRIC == 0 ? -2.0f : 1.0f);
+    }
+    qf[(int64_t)s * DP + i] = v;
+  }
+  qa = wave_sum_d(qa) * (1.0 + 1e-12);
+  if (lane == 0) {
+    const double tq = tau[f0 + s];
+    double T;
+    if (METRIC == 0) {
+      const double E =
+          f_err * (t.x2max + 2.1 * __builtin_sqrt(qa) * __builtin_sqrt(t.x2max)) + 1e-30;
+      T = tq * tq * (1.0 + 1e-12) - qa * (1.0 - 2e-12) + E;
+    } else {
+      const double E = f_err * (qa + t.x1max) + 1e-30;
+      T = tq * (1.0 + 1e-12) + E;
+    }
+    // round T up to a float (the order-preserving key's successor is the next float up)
+    float tf = (float)T;
+    if ((double)tf < T && tf < KNN_INF_F) tf = key2f(f2key(tf) + 1u);
+    thr[s] = tq < KNN_INF_D ? tf : -KNN_INF_F;  // unknown tau: nothing passes, full scan
+  }
+}
+
+template <int METRIC>
+__global__ void __launch_bounds__(256)
+rescan_filter_kernel(TrainDev t, const float* __restrict__ qf, const float* __restrict__ thr,
+                     int nf, int* __restrict__ cnt, int* __restrict__ buf) {
+  extern __shared__ __attribute__((aligned(16))) float fsm[];
+  const int DP = t.DP, RSF = DP + 4;
+  const int NWB = blockDim.x >> 6;
+  float* qs = fsm;                          // [kFiltQ][DP] centred queries (x -2 for L2)
+  float* thr_s = qs + kFiltQ * DP;          // [kFiltQ] proxy thresholds
+  float* rows = thr_s + kFiltQ;             // [NWB][64][RSF]
+  __shared__ int s_dummy;
+  (void)s_dummy;
+  const int g0 = blockIdx.y * kFiltQ;
+  const int nfg = min(kFiltQ, nf - g0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t row0 = ((int64_t)blockIdx.x * NWB + wv) * 64;
+  const bool active = row0 < t.n_pad;
+
+  // this wave's 64 rows -> LDS (X32 carries 1 KiB of slack past the last row)
+  float* my_rows = rows + (size_t)wv * 64 * RSF;
+  if (active) {
+    const int bytes = 64 * RSF * 4;
+    const char* src = (const char*)(t.X32 + row0 * RSF) + lane * 16;
+    const uint32_t dst = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)my_rows;
+    for (int p = 0; p * 1024 < bytes; ++p) glds16(src + p * 1024, dst + p * 1024);
+  }
+  for (int e = tid; e < kFiltQ * DP; e += blockDim.x) {
+    const int qi = e / DP;
+    qs[e] = qi < nfg ? qf[(int64_t)g0 * DP + e] : 0.0f;
+  }
+  if (tid < kFiltQ) thr_s[tid] = tid < nfg ? thr[g0 + tid] : -KNN_INF_F;  // absent: no row passes
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (!active) return;
+
+  const float* xr = my_rows + lane * RSF;
+  const float seed = xr[METRIC == 0 ? DP : DP + 1];  // +inf on pad rows: never passes
+  float acc[kFiltQ];
+#pragma unroll
+  for (int qi = 0; qi < kFiltQ; ++qi) acc[qi] = seed;
+  for (int c = 0; c < DP / 4; ++c) {
+    const float4 x4 = *(const float4*)(xr + 4 * c);
+#pragma unroll
+    for (int qi = 0; qi < kFiltQ; ++qi) {
+      const float4 q4 = *(const float4*)(qs + qi * DP + 4 * c);
+      float a = acc[qi];
+      if (METRIC == 0) {  // the candidate pass's fp32 model: an fmaf chain
+        a = __builtin_fmaf(q4.x, x4.x, a);
+        a = __builtin_fmaf(q4.y, x4.y, a);
+        a = __builtin_fmaf(q4.z, x4.z, a);
+        a = __builtin_fmaf(q4.w, x4.w, a);
+      } else {
+        a = a + __builtin_fabsf(q4.x - x4.x);
+        a = a + __builtin_fabsf(q4.y - x4.y);
+        a = a + __builtin_fabsf(q4.z - x4.z);
+        a = a + __builtin_fabsf(q4.w - x4.w);
+      }
+      acc[qi] = a;
+    }
+  }
+#pragma unroll
+  for (int qi = 0; qi < kFiltQ; ++qi) {
+    if (acc[qi] <= thr_s[qi]) {
+      const int pos = atomicAdd(&cnt[g0 + qi], 1);
+      if (pos < kRescanCap) buf[(int64_t)(g0 + qi) * kRescanCap + pos] = (int)(row0 + lane);
+    }
+  }
+}
+
+// One block per fast-rescanned query: exact re-rank of its appended rows.
+// Dynamic LDS: qv[d] | dk[kRescanCap] | tb[NT][17] | di[kRescanCap] | ls[kRescanCap].
+template <int METRIC, int NT>
+__global__ void __launch_bounds__(NT)
+rescan_finish_fast_kernel(TrainDev t, const double* __restrict__ Q64,
+                          const int* __restrict__ rescan_q, const double* __restrict__ tau, int f0,
+                          int W, const int* __restrict__ cnt, const int* __restrict__ buf,
+                          Sink sink, int* __restrict__ slow_q, int* __restrict__ slow_cnt) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int d = t.d;
+  const bool q_in_lds = d <= 1024;  // keeps the block's LDS under 64 KiB
+  double* dk = (double*)smem + (q_in_lds ? d : 0);
+  double* tb = dk + kRescanCap;
+  int* di = (int*)(tb + NT * 17);
+  int* ls = di + kRescanCap;
+  const int s = blockIdx.x, tid = threadIdx.x;
+  const int64_t q = rescan_q[f0 + s];
+  const int c = cnt[s];
+  const int need_rows = (int)min((int64_t)W, t.n);
+  if (!(tau[f0 + s] < KNN_INF_D) || c > kRescanCap || c < need_rows) {
+    if (tid == 0) slow_q[atomicAdd(slow_cnt, 1)] = (int)q;
+    return;
+  }
+  const double* qrow = Q64 + q * d;
+  const double* qv = q_in_lds ? (const double*)smem : qrow;
+  if (q_in_lds)
+    for (int i = tid; i < d; i += NT) ((double*)smem)[i] = qrow[i];
+  for (int i = tid; i < c; i += NT) di[i] = buf[(int64_t)s * kRescanCap + i];
+  __syncthreads();
+  int C2 = 1;
+  while (C2 < c) C2 <<= 1;
+  exact_sorted<METRIC, NT>(t, qv, di, dk, tb, c, C2, tid);
+  const int need = sink.mode == MODE_SINGLE ? sink.k : sink.w;
+  for (int i = tid; i < need && i < c; i += NT) ls[i] = t.lab[di[i]];
+  __syncthreads();
+  if (tid < 64) {
+    if (sink.mode == MODE_SINGLE)
+      finish_single(q, dk, di, ls, c, sink.k, sink.idx_off, 1 /*KNN_FLAG_EXACT_RESCAN*/, sink);
+    else
+      finish_partial(q, dk, di, ls, c, sink.w, sink.idx_off, sink);
+  }
+}
+
+void launch_rescan_fast(int metric, const TrainDev& t, const double* Q64, const int* rescan_q,
+                        const double* tau, int f0, int nf, int W, double f_err, float* qf,
+                        float* thr, int* cnt, int* buf, const Sink& sink, int* slow_q,
+                        int* slow_cnt, hipStream_t s) {
+  if (nf <= 0) return;
+  if (metric == 0)
+    hipLaunchKernelGGL(rescan_prep_kernel<0>, dim3((unsigned)nf), dim3(64), 0, s, t, Q64,
+                       rescan_q, tau, f0, f_err, qf, thr);
+  else
+    hipLaunchKernelGGL(rescan_prep_kernel<1>, dim3((unsigned)nf), dim3(64), 0, s, t, Q64,
+                       rescan_q, tau, f0, f_err, qf, thr);
+  // waves per block: as many 64-row tiles as fit beside the queries in ~150 KiB
+  const size_t tile = (size_t)64 * (t.DP + 4) * 4, qbytes = (size_t)kFiltQ * (t.DP + 1) * 4;
+  const int nwb = (int)std::max<size_t>(1, std::min<size_t>(4, (150 * 1024 - qbytes) / tile));
+  const int64_t rpb = 64 * nwb;
+  const dim3 fg((unsigned)((t.n_pad + rpb - 1) / rpb), (unsigned)((nf + kFiltQ - 1) / kFiltQ));
+  const size_t flds = qbytes + nwb * tile;
+  if (metric == 0)
+    hipLaunchKernelGGL(rescan_filter_kernel<0>, fg, dim3(64 * nwb), flds, s, t, qf, thr, nf, cnt,
+                       buf);
+  else
+    hipLaunchKernelGGL(rescan_filter_kernel<1>, fg, dim3(64 * nwb), flds, s, t, qf, thr, nf, cnt,
+                       buf);
+  const size_t lds = (size_t)(t.d <= 1024 ? t.d : 0) * 8 + (size_t)kRescanCap * 8 +
+                     (size_t)256 * 17 * 8 + (size_t)kRescanCap * 8;
+  if (metric == 0)
+    hipLaunchKernelGGL((rescan_finish_fast_kernel<0, 256>), dim3((unsigned)nf), dim3(256), lds, s,
+                       t, Q64, rescan_q, tau, f0, W, cnt, buf, sink, slow_q, slow_cnt);
+  else
+    hipLaunchKernelGGL((rescan_finish_fast_kernel<1, 256>), dim3((unsigned)nf), dim3(256), lds, s,
+                       t, Q64, rescan_q, tau, f0, W, cnt, buf, sink, slow_q, slow_cnt);
 }
 
 // ------------------------------------------------------ exact rescan path

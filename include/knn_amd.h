@@ -174,8 +174,9 @@ int knn_last_candidate_path(knn_ctx* ctx);
 
 /* Tuning overrides for experiments (0 = automatic): "R" list entries per
  * lane (4, 8, 16), "S" train splits per query tile (1..64), "nw" waves per
- * candidate workgroup (4 or 8; 32 queries per wave), "ablate" (timing-only
- * kernel ablations; results invalid). */
+ * candidate workgroup (4 or 8; 32 queries per wave), "ablate" (bits 0/1:
+ * timing-only kernel ablations, results invalid; bit 2: no per-query global
+ * threshold exchange in the resident kernel, results stay exact). */
 int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value);
 
 /* Synchronise the context's stream. */

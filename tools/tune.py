@@ -35,6 +35,7 @@ def main():
     out = torch.empty(a.m, dtype=torch.int32, device=dev)
     ref = None
     res = {v: [] for v in a.variants}
+    tot = {}
     info = {}
     prec = {"auto": knn.PRECISION_AUTO, "fp32": knn.PRECISION_FP32, "bf16x3": knn.PRECISION_BF16X3}
     for r in range(a.rounds + 1):
@@ -56,11 +57,13 @@ def main():
                 info[v] = (clf.last_geometry(), clf.last_rescan_count(), bool(torch.equal(ref, out)))
                 continue
             res[v].append(clf.last_phase_ms(knn.PHASE_CANDIDATE))
+            tot.setdefault(v, []).append(sum(clf.last_phase_ms(p) for p in range(4)))
     flops = 2.0 * a.n * a.d * a.m
     for v in a.variants:
         ms = np.median(res[v])
-        print("%-14s cand %8.3f ms (min %8.3f)  %7.1f TF/s  %s rescans=%d same_labels=%s"
-              % (v, ms, np.min(res[v]), flops / ms / 1e9, info[v][0], info[v][1], info[v][2]))
+        print("%-14s cand %8.3f ms (min %8.3f)  %7.1f TF/s  all phases %8.3f ms  %s rescans=%d "
+              "same_labels=%s" % (v, ms, np.min(res[v]), flops / ms / 1e9, np.median(tot[v]),
+                                  info[v][0], info[v][1], info[v][2]))
 
 
 if __name__ == "__main__":
