@@ -387,7 +387,7 @@ int cand_blocks_per_cu(int metric, int DP, int R, int nw) {
   return out;
 }
 
-int cand_tile_rows(int DP) { return DP <= 256 ? kTR : 128; }
+int cand_tile_rows(int DP) { return DP <= 256 ? kResTileRows : 128; }
 
 void launch_cand(const CandLaunch& c, hipStream_t s) {
 #define KNN_CASE(v)                \

@@ -3,9 +3,17 @@
 // many (DP, R, metric, waves) instantiations build in parallel.
 #include "knn_device.h"
 
+// Staging geometry (build-time; tools/build_variant.sh overrides for A/B):
+// 2 LDS buffers of 64-row tiles (two 32-row MFMA sub-tiles per barrier).
+// Measured against 3 buffers of 32-row tiles: -5.5 % (bf16x3) / -3 % (fp32).
 #ifndef KNN_RES_NB
-#define KNN_RES_NB 3  // staging buffers of the resident kernel (experiments: -DKNN_RES_NB=4)
+#define KNN_RES_NB 2
 #endif
+#ifndef KNN_RES_TPB
+#define KNN_RES_TPB 2
+#endif
+static_assert(KNN_RES_TPB * knnk::kTR == knnk::kResTileRows || KNN_RES_TPB != 2,
+              "default tile rows must match kResTileRows");
 
 namespace knnk {
 
@@ -52,8 +60,12 @@ constexpr int kPubEvery = 8;  // tiles between global-threshold exchanges
 // with a counted vmcnt for its own pieces of tile it before that barrier --
 // two tiles of latency hidden, one barrier per tile.  (A register-staged
 // variant measured the same or slower; removed.)
+// waves_per_eu(4): 4 waves per SIMD (<= 128 VGPRs), so two 8-wave workgroups
+// share a CU and one's barrier/epilogue gaps are filled by the other's MFMAs
+// (not for R = 16 lists or DP > 160, whose registers do not fit: spills).
 template <int DP, int R, int METRIC, int NW>
 __global__ void __launch_bounds__(NW * 64)
+__attribute__((amdgpu_waves_per_eu(DP <= 160 && R <= 8 ? 4 : 1)))
 cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
             int n_qt, float* __restrict__ out_v, int* __restrict__ out_i, int abl,
             uint32_t* gthr) {
@@ -63,7 +75,8 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   // abl: timing-only ablations (results invalid): bit0 = no staging loads
   // after the first tiles, bit1 = no selection epilogue.  0 in production.
   constexpr int RSF = DP + 4;               // row stride (floats), HBM and LDS
-  constexpr int TBY = kTR * RSF * 4;        // tile bytes
+  constexpr int TPB = KNN_RES_TPB;          // 32-row sub-tiles per staged tile
+  constexpr int TBY = kTR * TPB * RSF * 4;  // tile bytes
   constexpr int NG = (TBY + 1023) / 1024;   // 1-KiB LDS-DMA pieces per tile
   constexpr int NB = KNN_RES_NB;            // LDS buffers (prefetch distance NB - 1)
   constexpr int BUFF = NG * 256;            // floats per buffer
@@ -219,7 +232,9 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
         }
       }
     }
-    const float* base = lds + cur * BUFF;
+#pragma unroll
+    for (int sub = 0; sub < TPB; ++sub) {
+    const float* base = lds + cur * BUFF + sub * kTR * RSF;
 
     f32x16 acc;
 #pragma unroll
@@ -269,8 +284,9 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       }
     }
 
-    if (!(abl & 2)) select_block<R>(acc, t * kTR, h, L, I, thr, tq);
+    if (!(abl & 2)) select_block<R>(acc, (t * TPB + sub) * kTR, h, L, I, thr, tq);
     else if (acc[0] == 1234.5f && acc[15] == 1234.5f) thr = acc[7];  // keep acc live
+    }
     if (++cur == NB) cur = 0;
     if (++nxt == NB) nxt = 0;
 
@@ -299,7 +315,8 @@ static void with_M(int M, F f) {
 template <int DP, int R, int METRIC, int NW>
 static void launch_res(const CandLaunch& c, hipStream_t s) {
   hipLaunchKernelGGL((cand_kernel<DP, R, METRIC, NW>), dim3((unsigned)(c.n_qt * c.S)),
-                     dim3(NW * 64), 0, s, c.X32, c.Q32, (int)(c.n_pad / kTR), c.S, c.n_qt,
+                     dim3(NW * 64), 0, s, c.X32, c.Q32, (int)(c.n_pad / (kTR * KNN_RES_TPB)), c.S,
+                     c.n_qt,
                      c.out_v, c.out_i, c.ablate, c.gthr);
 }
 

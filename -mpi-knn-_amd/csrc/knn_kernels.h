@@ -7,7 +7,8 @@
 namespace knnk {
 
 constexpr int kQPB = 128;        // queries per candidate workgroup (4 waves x 32)
-constexpr int kTR = 32;          // train rows per LDS tile
+constexpr int kTR = 32;          // train rows per MFMA sub-tile of the resident kernel
+constexpr int kResTileRows = 64; // resident kernel: train rows per staged tile (2 sub-tiles)
 constexpr int kMaxUnion = 1024;  // max candidates kept per query across all lists
 constexpr int kSortN = 2048;     // rows per exact-rescan chunk / reduce block
 constexpr int kMaxK = 1000;      // largest k served (k+1 <= kMaxUnion)
