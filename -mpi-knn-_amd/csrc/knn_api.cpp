@@ -259,12 +259,14 @@ static void choose_geometry(knn_ctx* ctx, int metric, int DP, int nw, int n_qt, 
                             int W, int C, int& S_out, int& R_out) {
   const int S_hi = (int)std::max<int64_t>(1, std::min<int64_t>(64, n_tiles));
   int bestS = 1, bestR = 8;
+  const int lps = metric == 3 ? 4 : 2;  // lists per query per split
   for (int R : {4, 8, 16}) {
-    // R = 4 only on request (resident kernel; tuning experiments)
-    if (ctx->tune_R ? R != ctx->tune_R : R == 4) continue;
+    // kernel metric 3 (16x16x32 layout) has R = 4 only; elsewhere R = 4 only on
+    // request (resident kernel; tuning experiments)
+    if (metric == 3 ? R != 4 : (ctx->tune_R ? R != ctx->tune_R : R == 4)) continue;
     if (R == 4 && (DP > 256 || metric == 1)) continue;
     const int64_t slots = (int64_t)cand_blocks_per_cu(metric, DP, R, nw) * ctx->cu_count;
-    const int S_lo = std::min(S_hi, std::max(1, (C + 2 * R - 1) / (2 * R)));
+    const int S_lo = std::min(S_hi, std::max(1, (C + lps * R - 1) / (lps * R)));
     auto eff_of = [&](int S) {
       const int64_t wg = (int64_t)n_qt * S;
       const int64_t rounds = (wg + slots - 1) / slots;
@@ -286,7 +288,7 @@ static void choose_geometry(knn_ctx* ctx, int metric, int DP, int nw, int n_qt, 
     // fast rescan absorbs it.  Without a fast rescan (d > kRescanFastMaxDP a
     // rescan is a full exact scan) R = 16 unless the share is at most 1/2.
     const bool fast_rescan = DP <= kRescanFastMaxDP;
-    if (ctx->tune_R || (fast_rescan ? W <= 4 * bS : W <= bS)) break;
+    if (ctx->tune_R || metric == 3 || (fast_rescan ? W <= 4 * bS : W <= bS)) break;
   }
   S_out = bestS;
   R_out = bestR;
@@ -302,7 +304,7 @@ static void choose_geometry(knn_ctx* ctx, int metric, int DP, int nw, int n_qt, 
 //     representation error (~3 * 2^-18 relative per product, x2 for -2q).
 static double err_factor(int kmetric, int DP) {
   const double u = std::ldexp(1.0, -24);
-  if (kmetric == 2) {
+  if (kmetric == 2 || kmetric == 3) {  // bf16x3 on either MFMA shape
     const double u2 = std::ldexp(1.0, -23);
     const int n = 3 * DP + 1;
     return (n * u2 / (1.0 - n * u2) + std::ldexp(1.0, -15)) * 1.02;
@@ -330,8 +332,14 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   // staged tile) when there are enough queries, else 4; the large-d fp32
   // stream kernel always takes 128 queries, the bf16x3 one (S3) 256
   const bool s3 = kmetric == 2 && bf16x3_streamed(DP);
+  // bf16x3 on the 16x16x32 MFMA layout (resident kernel, 8 waves, DP % 32 ==
+  // 0): kernel metric 3, R = 4 lists, 4 lists per split.  Tuning key
+  // "mfma16": -1 auto (on for batches of >= 4096 queries), 0 off, 1 on.
+  const bool m16 = ctx->tune_m16 < 0 ? m >= 4096 : ctx->tune_m16 > 0;
+  if (kmetric == 2 && !s3 && m16 && DP % 32 == 0) kmetric = 3;
   int nw = 4;
   if (DP <= 256 && kmetric != 1) nw = ctx->tune_nw ? ctx->tune_nw : (m >= 4096 ? 8 : 4);
+  if (kmetric == 3) nw = 8;
   if (s3) nw = 8;
   const int qpb = s3 ? kS3Rows : (DP <= 256 ? 32 * nw : kQPB);
   const int n_qt = (int)((m + qpb - 1) / qpb);
@@ -342,7 +350,8 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   C = std::min(C, kMaxUnion);
   int S = 1, R = 8;
   choose_geometry(ctx, kmetric, DP, nw, n_qt, n_tiles, W, C, S, R);
-  const int NL = 2 * S;
+  if (kmetric == 3) R = 4;
+  const int NL = (kmetric == 3 ? 4 : 2) * S;
   C = std::min(C, NL * R);
   if ((rc = ctx->Q32.ensure((size_t)m_pad * DP * sizeof(float)))) return rc;
   if ((rc = ctx->cand_v.ensure((size_t)m_pad * NL * R * sizeof(float)))) return rc;
@@ -366,7 +375,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   if (s3)
     launch_prep_split_tiled(dQ, t.mu, m, t.d, DP, m_pad, -2.0, (unsigned short*)ctx->Q32.p, nullptr,
                             nullptr, s);
-  else if (kmetric == 2)
+  else if (kmetric == 2 || kmetric == 3)
     launch_prep_split(dQ, t.mu, m, t.d, DP, m_pad, -2.0, (unsigned short*)ctx->Q32.p, 2 * DP, nullptr,
                       nullptr, s);
   else
@@ -689,7 +698,10 @@ int knn_last_candidate_path(knn_ctx* ctx) { return ctx ? ctx->last_kmetric : -1;
 
 int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value) {
   if (!ctx || !key) return knn_fail(KNN_ERR_ARG, "null argument");
-  if (!strcmp(key, "R")) {
+  if (!strcmp(key, "mfma16")) {
+    if (value < -1 || value > 1) return knn_fail(KNN_ERR_ARG, "mfma16 must be -1, 0 or 1");
+    ctx->tune_m16 = (int)value;
+  } else if (!strcmp(key, "R")) {
     if (value != 0 && value != 4 && value != 8 && value != 16)
       return knn_fail(KNN_ERR_ARG, "R must be 0 (auto), 4, 8 or 16");
     ctx->tune_R = (int)value;

@@ -29,6 +29,7 @@ struct knn_ctx {
   int tune_R = 0, tune_S = 0;  // 0 = automatic
   int tune_ablate = 0;         // timing-only kernel ablations
   int tune_nw = 0;             // resident kernel waves per workgroup (0 = auto)
+  int tune_m16 = -1;           // bf16x3 on the 16x16x32 MFMA layout: -1 auto, 0 off, 1 on
   int last_nw = 0;
   int last_kmetric = -1; // candidate path of the last search (0 fp32 L2, 1 L1, 2 bf16x3)
   knnk::TrainDev train{};

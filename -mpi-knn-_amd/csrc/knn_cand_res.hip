@@ -91,6 +91,11 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   const int j = lane & 31, h = lane >> 5;
   const int64_t qg = (int64_t)qt * (NW * 32) + wv * 32 + j;
   const float* qrow = Q32 + qg * DP;
+  // METRIC 3 (bf16x3 on 16x16x32): lane l holds queries wv*32 + qb*16 + (l&15),
+  // qb = 0, 1, against rows 4*(l>>4) + i of each 16-row block
+  constexpr bool M16 = METRIC == 3;
+  const int c16 = lane & 15, g16 = lane >> 4;
+  const int64_t qb0 = (int64_t)qt * (NW * 32) + wv * 32 + c16;  // query of block 0 (+16: block 1)
 
   // B operand resident in VGPRs for the whole kernel.  METRIC 0: fp32 -2q,
   // float4 c holds dims 8c+4h..8c+4h+3 (four 32x32x2 k-steps).  METRIC 2:
@@ -109,8 +114,14 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int c = c0 + u < DP / 8 ? c0 + u : c0;
-        const int off = METRIC == 0 ? 8 * c : (c < DP / 16 ? 8 * c : DP / 2 + 8 * (c - DP / 16));
-        p[u] = qrow + off + 4 * h;
+        if constexpr (M16) {
+          // c = (qb*2 + part)*(DP/32) + ks: dims 32ks + 8*g16 .. +7 of part
+          const int ks = c % (DP / 32), pp = (c / (DP / 32)) & 1, qb = c / (DP / 16);
+          p[u] = Q32 + (qb0 + 16 * qb) * DP + pp * (DP / 2) + 16 * ks + 4 * g16;
+        } else {
+          const int off = METRIC == 0 ? 8 * c : (c < DP / 16 ? 8 * c : DP / 2 + 8 * (c - DP / 16));
+          p[u] = qrow + off + 4 * h;
+        }
       }
       float4 v0, v1, v2, v3;
       asm volatile(
@@ -129,11 +140,16 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
     }
   }
 
-  float L[R];
-  int I[R];
+  constexpr int NQL = M16 ? 2 : 1;  // queries (lists) per lane
+  float L[NQL][R];
+  int I[NQL][R];
+  float thr[NQL];
 #pragma unroll
-  for (int t = 0; t < R; ++t) { L[t] = KNN_INF_F; I[t] = -1; }
-  float thr = KNN_INF_F;
+  for (int b = 0; b < NQL; ++b) {
+#pragma unroll
+    for (int t = 0; t < R; ++t) { L[b][t] = KNN_INF_F; I[b][t] = -1; }
+    thr[b] = KNN_INF_F;
+  }
 
   // Global per-query threshold.  The query's lists are spread over S
   // workgroups; they form 4 groups by split % 4, and slot g of gthr[query]
@@ -155,8 +171,13 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   // e+1 .. e+PD-1 leave those x ops in flight (counted wait + x), the
   // barrier of tile e+PD retires them and the slots are read after it -- no
   // barrier ever waits on a (contended) atomic.
-  const uint32_t goff = (uint32_t)(qg * 16);  // byte offset of gthr[query][0]
-  float tq = KNN_INF_F;
+  // byte offset of gthr[query][0]: the lane's query, or for METRIC 3 query
+  // (l & 31) of the wave (lanes 0-15 block 0, 16-31 block 1; 32-63 repeat)
+  const uint32_t goff =
+      M16 ? (uint32_t)(((int64_t)qt * (NW * 32) + wv * 32 + (lane & 31)) * 16) : (uint32_t)(qg * 16);
+  float tq[NQL];
+#pragma unroll
+  for (int b = 0; b < NQL; ++b) tq[b] = KNN_INF_F;
   uint32_t last_pub = kKeyInf;
   int x_ops = 0, x_age = -1;  // ops of the pending exchange, tiles since it
 
@@ -207,17 +228,28 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       if (it + PD < my_nt && !(abl & 1)) KNN_ISSUE(t + PD * S, nxt);
       if (gthr) {
         if (x_age == PD) {
-          const u32x4 gv = gls[wv * 64 + lane];
-          tq = key2f(max(max(gv.x, gv.y), max(gv.z, gv.w)));
+#pragma unroll
+          for (int b = 0; b < NQL; ++b) {
+            const u32x4 gv = gls[wv * 64 + (M16 ? 16 * b + c16 : lane)];
+            tq[b] = key2f(max(max(gv.x, gv.y), max(gv.z, gv.w)));
+          }
           x_age = -1;
         }
         if ((it & (kPubEvery - 1)) == kPubEvery - 1 && it + PD < my_nt) {
-          // publish the better of the lane pair's two list thresholds (one
-          // lane per pair, only when it improved), fetch the query's 4 slots
-          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(thr),
-                                                           __float_as_uint(thr), false, false);
-          const uint32_t pk = f2key(fminf(__uint_as_float(sw[0]), __uint_as_float(sw[1])));
-          const bool pub = h == 0 && pk < last_pub;
+          // publish the best list threshold of the query's lanes in this wave
+          // (one lane per query, only when it improved), fetch its 4 slots
+          uint32_t pk;
+          bool pub;
+          if constexpr (M16) {
+            const float m0 = quad_min(thr[0]), m1 = quad_min(thr[1]);
+            pk = f2key(g16 == 0 ? m0 : m1);
+            pub = g16 < 2 && pk < last_pub;
+          } else {
+            const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(thr[0]),
+                                                             __float_as_uint(thr[0]), false, false);
+            pk = f2key(fminf(__uint_as_float(sw[0]), __uint_as_float(sw[1])));
+            pub = h == 0 && pk < last_pub;
+          }
           x_ops = 1;
           if (__ballot(pub)) {
             if (pub)
@@ -236,6 +268,46 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
     for (int sub = 0; sub < TPB; ++sub) {
     const float* base = lds + cur * BUFF + sub * kTR * RSF;
 
+    if constexpr (M16) {
+      // bf16x3 on v_mfma_f32_16x16x32_bf16: 2 row blocks x 2 query blocks of
+      // 16; lane l: A = row rb*16 + (l&15), B = query qb*16 + (l&15), k-group
+      // l>>4; D = rows rb*16 + 4(l>>4) + i, column l&15
+      f32x4 acc[2][2];
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float sd = base[(rb * 16 + 4 * g16 + i) * RSF + SEED];
+          acc[rb][0][i] = sd;
+          acc[rb][1][i] = sd;
+        }
+      }
+#pragma unroll
+      for (int ks = 0; ks < DP / 32; ++ks) {
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          const float* ar = base + (rb * 16 + c16) * RSF + 16 * ks + 4 * g16;
+          const bf16x8 ah = __builtin_bit_cast(bf16x8, *(const float4*)ar);
+          const bf16x8 al = __builtin_bit_cast(bf16x8, *(const float4*)(ar + DP / 2));
+#pragma unroll
+          for (int qb = 0; qb < 2; ++qb) {
+            const bf16x8 bh = __builtin_bit_cast(bf16x8, qf[(qb * 2 + 0) * (DP / 32) + ks]);
+            const bf16x8 bl = __builtin_bit_cast(bf16x8, qf[(qb * 2 + 1) * (DP / 32) + ks]);
+            acc[rb][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc[rb][qb], 0, 0, 0);
+            acc[rb][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc[rb][qb], 0, 0, 0);
+            acc[rb][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc[rb][qb], 0, 0, 0);
+          }
+        }
+      }
+      const int row0 = (t * TPB + sub) * kTR + 4 * g16;
+      if (!(abl & 2)) {
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+          select_quad<R>(acc[0][qb], acc[1][qb], row0, L[qb], I[qb], thr[qb], tq[qb]);
+      } else if (acc[0][0][0] == 1234.5f && acc[1][1][3] == 1234.5f) {
+        thr[0] = acc[0][1][2];  // keep the accumulators live
+      }
+    } else {
     f32x16 acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = base[((i & 3) + 8 * (i >> 2) + 4 * h) * RSF + SEED];
@@ -284,8 +356,9 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       }
     }
 
-    if (!(abl & 2)) select_block<R>(acc, (t * TPB + sub) * kTR, h, L, I, thr, tq);
-    else if (acc[0] == 1234.5f && acc[15] == 1234.5f) thr = acc[7];  // keep acc live
+    if (!(abl & 2)) select_block<R>(acc, (t * TPB + sub) * kTR, h, L[0], I[0], thr[0], tq[0]);
+    else if (acc[0] == 1234.5f && acc[15] == 1234.5f) thr[0] = acc[7];  // keep acc live
+    }
     }
     if (++cur == NB) cur = 0;
     if (++nxt == NB) nxt = 0;
@@ -293,7 +366,20 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-  write_lists<R>(out_v, out_i, qg, S, split, h, L, I);
+  if constexpr (M16) {
+    // 4 lists per query per split (lane groups l>>4): [query][4S][R]
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      const int64_t o = ((qb0 + 16 * qb) * (4 * S) + split * 4 + g16) * R;
+#pragma unroll
+      for (int t = 0; t < R; t += 4) {
+        *(float4*)(out_v + o + t) = make_float4(L[qb][t], L[qb][t + 1], L[qb][t + 2], L[qb][t + 3]);
+        *(int4*)(out_i + o + t) = make_int4(I[qb][t], I[qb][t + 1], I[qb][t + 2], I[qb][t + 3]);
+      }
+    }
+  } else {
+    write_lists<R>(out_v, out_i, qg, S, split, h, L[0], I[0]);
+  }
 #undef KNN_ISSUE
 }
 
@@ -309,7 +395,8 @@ template <class F>
 static void with_M(int M, F f) {
   if (M == 0) f(std::integral_constant<int, 0>{});
   else if (M == 1) f(std::integral_constant<int, 1>{});
-  else f(std::integral_constant<int, 2>{});
+  else if (M == 2) f(std::integral_constant<int, 2>{});
+  else f(std::integral_constant<int, 3>{});
 }
 
 template <int DP, int R, int METRIC, int NW>
@@ -325,7 +412,8 @@ static void launch_res(const CandLaunch& c, hipStream_t s) {
 // needs DP % 16 == 0.
 template <int DP, int R, int M, int NW>
 constexpr bool res_variant() {
-  return (M != 2 || DP % 16 == 0) && (M != 1 || (NW == 4 && R != 4));
+  return (M != 2 || DP % 16 == 0) && (M != 1 || (NW == 4 && R != 4)) &&
+         (M != 3 || (DP % 32 == 0 && R == 4 && NW == 8));
 }
 
 template <int DP>

@@ -14,6 +14,7 @@ namespace knnk {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 #define KNN_INF_F __builtin_inff()
@@ -202,6 +203,39 @@ __device__ __forceinline__ void select_block(const f32x16& acc, int row0, int h,
       const float v = acc[i];
       if (v < te) {
         list_insert<R>(L, I, v, row0 + (i & 3) + 8 * (i >> 2) + 4 * h);
+        thr = L[R - 1];
+        te = __builtin_fminf(te, thr);
+      }
+    }
+  }
+}
+
+// min over the 4 lanes l&15 + 16r (r = 0..3) that hold the same query in the
+// 16x16 MFMA layout
+__device__ __forceinline__ float quad_min(float x) {
+  const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false,
+                                                   false);
+  x = __builtin_fminf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+  return __builtin_fminf(x, __shfl_xor(x, 16, 64));
+}
+
+// Top-R selection for the 16x16 layout: 8 values of one query (rows row0 + i
+// of block a, row0 + 16 + i of block b), threshold shared by the query's 4
+// lanes (each keeps its own list; the merge's bound is the min over lists).
+template <int R>
+__device__ __forceinline__ void select_quad(const f32x4& a, const f32x4& b, int row0,
+                                            float (&L)[R], int (&I)[R], float& thr, float tq) {
+  float te = __builtin_fminf(quad_min(thr), tq);
+  const float mn = __builtin_fminf(__builtin_fminf(__builtin_fminf(a[0], a[1]),
+                                                   __builtin_fminf(a[2], a[3])),
+                                   __builtin_fminf(__builtin_fminf(b[0], b[1]),
+                                                   __builtin_fminf(b[2], b[3])));
+  if (mn < te) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float v = i < 4 ? a[i] : b[i - 4];
+      if (v < te) {
+        list_insert<R>(L, I, v, row0 + (i < 4 ? i : 16 + i - 4));
         thr = L[R - 1];
         te = __builtin_fminf(te, thr);
       }

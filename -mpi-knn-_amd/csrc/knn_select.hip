@@ -321,14 +321,13 @@ void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int
 // Queries whose candidate set was not certified (a list overflowed near the
 // top, heavy ties).  tau = the W-th exact distance among the query's
 // re-ranked rows, >= the true W-th.  rescan_filter streams the fp32 train
-// copy once per kFiltQ such queries (lane = train row, queries broadcast
+// copy once per 4 or 16 such queries (lane = train row, queries broadcast
 // from LDS) and appends every row whose centred fp32 proxy --
 // an fmaf chain with the candidate pass's certified error bound -- is within
 // reach of tau; the appended set therefore holds every row with exact
 // distance <= tau, i.e. the exact top-W with all its ties.  rescan_finish
 // re-ranks it exactly.  Unknown tau or more than kRescanCap rows: the full
 // exact scan below.
-constexpr int kFiltQ = 16;  // failed queries per filter block (LDS broadcasts)
 
 // Block = NWB waves, wave w owns the 64 consecutive train rows starting at
 // blockIdx.x*64*NWB + 64w (lane = row).  The wave copies its rows (the
@@ -374,7 +373,7 @@ rescan_prep_kernel(TrainDev t, const double* __restrict__ Q64, const int* __rest
   }
 }
 
-template <int METRIC>
+template <int METRIC, int kFiltQ>  // kFiltQ: failed queries per block (LDS broadcasts)
 __global__ void __launch_bounds__(256)
 rescan_filter_kernel(TrainDev t, const float* __restrict__ qf, const float* __restrict__ thr,
                      int nf, int* __restrict__ cnt, int* __restrict__ buf) {
@@ -498,18 +497,23 @@ void launch_rescan_fast(int metric, const TrainDev& t, const double* Q64, const 
   else
     hipLaunchKernelGGL(rescan_prep_kernel<1>, dim3((unsigned)nf), dim3(64), 0, s, t, Q64,
                        rescan_q, tau, f0, f_err, qf, thr);
-  // waves per block: as many 64-row tiles as fit beside the queries in ~150 KiB
-  const size_t tile = (size_t)64 * (t.DP + 4) * 4, qbytes = (size_t)kFiltQ * (t.DP + 1) * 4;
+  // queries per block: 4 for a handful of failed queries (list overflows),
+  // else 16; waves per block: as many 64-row tiles as fit in ~150 KiB
+  const int fq = nf <= 4 ? 4 : 16;
+  const size_t tile = (size_t)64 * (t.DP + 4) * 4, qbytes = (size_t)fq * (t.DP + 1) * 4;
   const int nwb = (int)std::max<size_t>(1, std::min<size_t>(4, (150 * 1024 - qbytes) / tile));
   const int64_t rpb = 64 * nwb;
-  const dim3 fg((unsigned)((t.n_pad + rpb - 1) / rpb), (unsigned)((nf + kFiltQ - 1) / kFiltQ));
+  const dim3 fg((unsigned)((t.n_pad + rpb - 1) / rpb), (unsigned)((nf + fq - 1) / fq));
   const size_t flds = qbytes + nwb * tile;
-  if (metric == 0)
-    hipLaunchKernelGGL(rescan_filter_kernel<0>, fg, dim3(64 * nwb), flds, s, t, qf, thr, nf, cnt,
-                       buf);
-  else
-    hipLaunchKernelGGL(rescan_filter_kernel<1>, fg, dim3(64 * nwb), flds, s, t, qf, thr, nf, cnt,
-                       buf);
+#define KNN_FILT(M_, Q_)                                                                      \
+  hipLaunchKernelGGL((rescan_filter_kernel<M_, Q_>), fg, dim3(64 * nwb), flds, s, t, qf, thr, nf, \
+                     cnt, buf)
+  if (metric == 0) {
+    if (fq == 4) KNN_FILT(0, 4); else KNN_FILT(0, 16);
+  } else {
+    if (fq == 4) KNN_FILT(1, 4); else KNN_FILT(1, 16);
+  }
+#undef KNN_FILT
   const size_t lds = (size_t)(t.d <= 1024 ? t.d : 0) * 8 + (size_t)kRescanCap * 8 +
                      (size_t)256 * 17 * 8 + (size_t)kRescanCap * 8;
   if (metric == 0)

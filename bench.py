@@ -318,7 +318,7 @@ def main():
                     % (n, m, d, k, C))
         parallelism = "train-sharded tp%d" % world
 
-    bf16 = main_r["path"] == 2
+    bf16 = main_r["path"] in (2, 3)
     peak = PEAK_BF16_TFLOPS if bf16 else PEAK_FP32_TFLOPS
     mfma_mult = 3.0 if bf16 else 1.0  # MFMA flops issued per algorithmic flop
     achieved = flops / main_r["t_cand"] / 1e12

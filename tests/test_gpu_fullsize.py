@@ -136,7 +136,12 @@ def test_cfg2_full(knn):
     check_properties(X, lab_all, Q, k, got, idx, dist, np.arange(m))
     check_oracle(X, lab_all, Q, k, got, idx, dist, np.arange(0, m, m // 32))
     check_optimal(X, Q, k, dist, np.arange(0, m, m // 512))
-    # the fp32 candidate path gives the same exact answer
+    # the other candidate paths give the same exact answer
+    clf.set_tuning("mfma16", 0)  # bf16x3 on 32x32x16
+    got16, idx16, dist16, _ = classify(knn, clf, Q, k)
+    np.testing.assert_array_equal(got16, got)
+    assert (dist16.view(np.int64) == dist.view(np.int64)).all()
+    clf.set_tuning("mfma16", -1)
     clf.set_precision(knn.PRECISION_FP32)
     got32, idx32, dist32, _ = classify(knn, clf, Q, k)
     np.testing.assert_array_equal(got32, got)

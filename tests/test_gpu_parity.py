@@ -34,12 +34,14 @@ def knn():
     return mod
 
 
-@pytest.fixture(scope="module", params=["auto", "fp32"])
+@pytest.fixture(scope="module", params=["auto", "fp32", "m16"])
 def clf(knn, request):
     """Every parity test runs with the default candidate path (bf16x3 for L2
-    where supported) and with the fp32 path forced."""
+    where supported), with the fp32 path forced, and with bf16x3 on the
+    16x16x32 MFMA layout forced (the default only for >= 4096 queries)."""
     c = knn.Classifier(0)
-    c.set_precision(knn.PRECISION_AUTO if request.param == "auto" else knn.PRECISION_FP32)
+    c.set_precision(knn.PRECISION_FP32 if request.param == "fp32" else knn.PRECISION_AUTO)
+    c.set_tuning("mfma16", 1 if request.param == "m16" else 0)
     yield c
     c.close()
 
