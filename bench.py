@@ -344,8 +344,10 @@ def main():
                 "SIFT-like; fp64 inputs)",
         "config": {"workload": workload, "n_train": n, "queries": m, "dim": d, "k": k,
                    "parallelism": parallelism,
-                   "candidate_pass": ("bf16x3 split (qh.xh+ql.xh+qh.xl) on MFMA 32x32x16 bf16"
-                                      if bf16 else "fp32 MFMA 32x32x2") + " + fused top-R per lane",
+                   "candidate_pass": ("bf16x3 split (qh.xh+ql.xh+qh.xl) on MFMA %s bf16"
+                                      % ("16x16x32" if main_r["path"] == 3 else "32x32x16")
+                                      if bf16 else "fp32 MFMA 32x32x2")
+                                     + " + fused top-R per lane, certified bound",
                    "rerank": "fp64 exact (reference arithmetic), certified; labels exact",
                    "geometry": geom, "rescanned_queries": main_r["resc"]},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
