@@ -106,6 +106,7 @@ int knn_create(knn_ctx** out, int device) {
   if (const char* e = getenv("KNN_PRECISION")) {
     if (!strcmp(e, "fp32")) c->precision = KNN_PRECISION_FP32;
     else if (!strcmp(e, "bf16x3")) c->precision = KNN_PRECISION_BF16X3;
+    else if (!strcmp(e, "fp16")) c->precision = KNN_PRECISION_FP16;
   }
   *out = c;
   return KNN_OK;
@@ -140,21 +141,22 @@ static int build_train(knn_ctx* ctx, const double* dX, const int32_t* dlab, int6
   if ((rc = ctx->X32.ensure((size_t)n_pad * (DP + 4) * sizeof(float) + 1024))) return rc;
   if ((rc = ctx->xl2.ensure((size_t)n_pad * sizeof(float)))) return rc;
   if ((rc = ctx->xl1.ensure((size_t)n_pad * sizeof(float)))) return rc;
-  if ((rc = ctx->stats.ensure(2 * sizeof(unsigned long long)))) return rc;
+  if ((rc = ctx->stats.ensure(3 * sizeof(unsigned long long)))) return rc;
   if ((rc = ctx->mu.ensure((size_t)d * sizeof(double)))) return rc;
   if ((rc = ctx->mu_part.ensure((size_t)col_mean_blocks(n) * d * sizeof(double)))) return rc;
   launch_col_mean(dX, n, d, (double*)ctx->mu_part.p, (double*)ctx->mu.p, ctx->stream);
-  HIP_TRY(hipMemsetAsync(ctx->stats.p, 0, 2 * sizeof(unsigned long long), ctx->stream));
+  HIP_TRY(hipMemsetAsync(ctx->stats.p, 0, 3 * sizeof(unsigned long long), ctx->stream));
   launch_prep_train(dX, (const double*)ctx->mu.p, n, d, DP, n_pad, (float*)ctx->X32.p,
                     (float*)ctx->xl2.p, (float*)ctx->xl1.p, (unsigned long long*)ctx->stats.p,
                     ctx->stream);
   HIP_TRY(hipGetLastError());
-  unsigned long long st[2];
+  unsigned long long st[3];
   HIP_TRY(hipMemcpyAsync(st, ctx->stats.p, sizeof st, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   double x2, x1;
   memcpy(&x2, &st[0], 8);
   memcpy(&x1, &st[1], 8);
+  memcpy(&ctx->xamax, &st[2], 8);
   TrainDev& t = ctx->train;
   t.X64 = dX;
   t.mu = (const double*)ctx->mu.p;
@@ -170,7 +172,9 @@ static int build_train(knn_ctx* ctx, const double* dX, const int32_t* dlab, int6
   t.x1max = x1;
   ctx->class_cnt = class_cnt;
   ctx->idx_off = idx_off;
-  ctx->DPb = 0;  // bf16x3 copy is rebuilt lazily for the new train set
+  ctx->DPb = 0;  // bf16x3 / fp16 copies are rebuilt lazily for the new train set
+  ctx->DPh = 0;
+  ctx->fp16_off = false;
   ctx->trained = true;
   return KNN_OK;
 }
@@ -199,6 +203,36 @@ static int ensure_bf16x3(knn_ctx* ctx, hipStream_t s) {
   HIP_TRY(hipGetLastError());
   ctx->DPb = DPb;
   return KNN_OK;
+}
+
+// The fp16 copy of the train rows for kernel metric 4:
+// 2^jx (x - mu) in fp16 with jx from the largest |x_i - mu_i|, + the scaled
+// L2 seeds; same row count as X32, rows of DP/2 + 4 floats.
+static int ensure_fp16(knn_ctx* ctx, hipStream_t s) {
+  const TrainDev& t = ctx->train;
+  const int DPh = pad_dim_fp16(t.d);
+  if (DPh <= 0) return knn_fail(KNN_ERR_ARG, "fp16 path supports d <= 256");
+  if (ctx->DPh == DPh) return KNN_OK;
+  int e = 0;
+  if (ctx->xamax > 0.0) (void)std::frexp(ctx->xamax, &e);  // xamax < 2^e
+  ctx->jx = std::min(std::max(9 - e, -60), 60);
+  int rc;
+  if ((rc = ctx->XH.ensure((size_t)t.n_pad * (DPh / 2 + 4) * sizeof(float) + 1024))) return rc;
+  launch_prep_half_train(t.X64, t.mu, t.n, t.d, DPh, t.n_pad, ctx->jx,
+                         (unsigned short*)ctx->XH.p, t.xinit_l2, s);
+  HIP_TRY(hipGetLastError());
+  ctx->DPh = DPh;
+  return KNN_OK;
+}
+
+// fp16 candidate pass (kernel metric 4): PRECISION_FP16, or AUTO for batches
+// of >= 4096 queries (8-wave workgroups) until a batch certifies poorly.
+// Tuning key "fp16": -1 auto, 0 off, 1 on.
+static bool use_fp16(const knn_ctx* ctx, int metric, int64_t m) {
+  if (metric != KNN_METRIC_L2 || pad_dim_fp16(ctx->train.d) <= 0) return false;
+  if (ctx->tune_fp16 >= 0) return ctx->tune_fp16 > 0;
+  if (ctx->precision == KNN_PRECISION_FP16) return true;
+  return ctx->precision == KNN_PRECISION_AUTO && !ctx->fp16_off && m >= 4096;
 }
 
 static bool use_bf16x3(const knn_ctx* ctx, int metric) {
@@ -259,11 +293,11 @@ static void choose_geometry(knn_ctx* ctx, int metric, int DP, int nw, int n_qt, 
                             int W, int C, int& S_out, int& R_out) {
   const int S_hi = (int)std::max<int64_t>(1, std::min<int64_t>(64, n_tiles));
   int bestS = 1, bestR = 8;
-  const int lps = metric == 3 ? 4 : 2;  // lists per query per split
+  const int lps = metric >= 3 ? 4 : 2;  // lists per query per split
   for (int R : {4, 8, 16}) {
     // kernel metric 3 (16x16x32 layout) has R = 4 only; elsewhere R = 4 only on
     // request (resident kernel; tuning experiments)
-    if (metric == 3 ? R != 4 : (ctx->tune_R ? R != ctx->tune_R : R == 4)) continue;
+    if (metric >= 3 ? R != 4 : (ctx->tune_R ? R != ctx->tune_R : R == 4)) continue;
     if (R == 4 && (DP > 256 || metric == 1)) continue;
     const int64_t slots = (int64_t)cand_blocks_per_cu(metric, DP, R, nw) * ctx->cu_count;
     const int S_lo = std::min(S_hi, std::max(1, (C + lps * R - 1) / (lps * R)));
@@ -288,7 +322,7 @@ static void choose_geometry(knn_ctx* ctx, int metric, int DP, int nw, int n_qt, 
     // fast rescan absorbs it.  Without a fast rescan (d > kRescanFastMaxDP a
     // rescan is a full exact scan) R = 16 unless the share is at most 1/2.
     const bool fast_rescan = DP <= kRescanFastMaxDP;
-    if (ctx->tune_R || metric == 3 || (fast_rescan ? W <= 4 * bS : W <= bS)) break;
+    if (ctx->tune_R || metric >= 3 || (fast_rescan ? W <= 4 * bS : W <= bS)) break;
   }
   S_out = bestS;
   R_out = bestR;
@@ -302,8 +336,17 @@ static void choose_geometry(knn_ctx* ctx, int metric, int DP, int nw, int n_qt, 
 //   kmetric 2 (bf16x3): products exact, accumulation of 3DP+1 terms bounded
 //     with u' = 2^-23 (covers truncating adders), + 2^-15 for the hi/lo
 //     representation error (~3 * 2^-18 relative per product, x2 for -2q).
+//   kmetric 4 (fp16): both operands rounded to fp16 (u_h = 2^-11, x(1 +
+//     2^-12) for a double rounding via fp32) -> 2u_h + u_h^2 per product;
+//     products exact in fp32, DP+1 accumulated terms with u' = 2^-23.  The
+//     fp16 subnormal-range terms are absolute and added by the merge.
 static double err_factor(int kmetric, int DP) {
   const double u = std::ldexp(1.0, -24);
+  if (kmetric == 4) {
+    const double u2 = std::ldexp(1.0, -23), uh = std::ldexp(1.0, -11) * (1.0 + std::ldexp(1.0, -12));
+    const int n = DP + 1;
+    return (n * u2 / (1.0 - n * u2) + 2.0 * uh + uh * uh) * 1.02;
+  }
   if (kmetric == 2 || kmetric == 3) {  // bf16x3 on either MFMA shape
     const double u2 = std::ldexp(1.0, -23);
     const int n = 3 * DP + 1;
@@ -322,7 +365,12 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   // candidate-pass flavour: kmetric 2 = L2 via bf16x3 MFMA, else fp32
   int kmetric = metric, DP = t.DP;
   const float* Xk = t.X32;
-  if (use_bf16x3(ctx, metric)) {
+  if (use_fp16(ctx, metric, m)) {
+    if ((rc = ensure_fp16(ctx, s))) return rc;
+    kmetric = 4;
+    DP = ctx->DPh;
+    Xk = (const float*)ctx->XH.p;
+  } else if (use_bf16x3(ctx, metric)) {
     if ((rc = ensure_bf16x3(ctx, s))) return rc;
     kmetric = 2;
     DP = ctx->DPb;
@@ -339,7 +387,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   if (kmetric == 2 && !s3 && m16 && DP % 32 == 0) kmetric = 3;
   int nw = 4;
   if (DP <= 256 && kmetric != 1) nw = ctx->tune_nw ? ctx->tune_nw : (m >= 4096 ? 8 : 4);
-  if (kmetric == 3) nw = 8;
+  if (kmetric >= 3) nw = 8;
   if (s3) nw = 8;
   const int qpb = s3 ? kS3Rows : (DP <= 256 ? 32 * nw : kQPB);
   const int n_qt = (int)((m + qpb - 1) / qpb);
@@ -350,10 +398,11 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   C = std::min(C, kMaxUnion);
   int S = 1, R = 8;
   choose_geometry(ctx, kmetric, DP, nw, n_qt, n_tiles, W, C, S, R);
-  if (kmetric == 3) R = 4;
-  const int NL = (kmetric == 3 ? 4 : 2) * S;
+  if (kmetric >= 3) R = 4;
+  const int NL = (kmetric >= 3 ? 4 : 2) * S;
   C = std::min(C, NL * R);
   if ((rc = ctx->Q32.ensure((size_t)m_pad * DP * sizeof(float)))) return rc;
+  if (kmetric == 4 && (rc = ctx->qfac.ensure((size_t)m_pad * sizeof(float)))) return rc;
   if ((rc = ctx->cand_v.ensure((size_t)m_pad * NL * R * sizeof(float)))) return rc;
   if ((rc = ctx->cand_i.ensure((size_t)m_pad * NL * R * sizeof(int)))) return rc;
   // per-query global thresholds of the resident candidate kernel
@@ -375,6 +424,9 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   if (s3)
     launch_prep_split_tiled(dQ, t.mu, m, t.d, DP, m_pad, -2.0, (unsigned short*)ctx->Q32.p, nullptr,
                             nullptr, s);
+  else if (kmetric == 4)
+    launch_prep_half_queries(dQ, t.mu, m, t.d, DP, m_pad, ctx->jx, (unsigned short*)ctx->Q32.p,
+                             (float*)ctx->qfac.p, s);
   else if (kmetric == 2 || kmetric == 3)
     launch_prep_split(dQ, t.mu, m, t.d, DP, m_pad, -2.0, (unsigned short*)ctx->Q32.p, 2 * DP, nullptr,
                       nullptr, s);
@@ -397,6 +449,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   cl.ablate = ctx->tune_ablate;
   cl.nw = nw;
   cl.gthr = use_gthr ? (uint32_t*)ctx->gthr.p : nullptr;
+  cl.qfac = kmetric == 4 ? (const float*)ctx->qfac.p : nullptr;
   if (use_gthr) launch_fill_i32((int32_t*)ctx->gthr.p, m_pad * 4, (int32_t)kGthrInit, s);
   if (s3)
     launch_cand_s3((const unsigned short*)ctx->XB.p, (const float*)ctx->XS.p,
@@ -408,7 +461,8 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   if (tm) HIP_TRY(hipEventRecord(ctx->ev[2], s));
   HIP_TRY(hipMemsetAsync(ctx->rescan_cnt.p, 0, sizeof(int), s));
   launch_merge_rerank(metric, (const float*)ctx->cand_v.p, (const int*)ctx->cand_i.p, NL, R, t, dQ,
-                      m, W, C, err_factor(kmetric, DP), cl.gthr, sink, (int*)ctx->rescan_q.p,
+                      m, W, C, err_factor(kmetric, DP), ProxyScale{cl.qfac, std::ldexp(1.0, ctx->jx)},
+                      cl.gthr, sink, (int*)ctx->rescan_q.p,
                       (double*)ctx->rescan_tau.p, (int*)ctx->rescan_cnt.p, s);
   HIP_TRY(hipGetLastError());
   if (tm) HIP_TRY(hipEventRecord(ctx->ev[3], s));
@@ -416,6 +470,11 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   HIP_TRY(hipStreamSynchronize(s));
   const int nflag = ctx->h_count[0];
   ctx->last_rescan = nflag;
+  // AUTO retires the fp16 pass for this train set when a batch leaves more
+  // than 1/16 of its queries to the rescan (data whose neighbour gaps are
+  // too fine for fp16 operands): later batches take bf16x3
+  if (kmetric == 4 && ctx->precision == KNN_PRECISION_AUTO && (int64_t)nflag * 16 > m)
+    ctx->fp16_off = true;
   ctx->last_slow_rescan = 0;
   if (tm) {
     float ms;
@@ -688,7 +747,7 @@ int64_t knn_last_rescan_count(knn_ctx* ctx) { return ctx ? ctx->last_rescan : -1
 
 int knn_set_precision(knn_ctx* ctx, int mode) {
   if (!ctx) return knn_fail(KNN_ERR_ARG, "null context");
-  if (mode < KNN_PRECISION_AUTO || mode > KNN_PRECISION_BF16X3)
+  if (mode < KNN_PRECISION_AUTO || mode > KNN_PRECISION_FP16)
     return knn_fail(KNN_ERR_ARG, "unknown precision mode");
   ctx->precision = mode;
   return KNN_OK;
@@ -698,7 +757,10 @@ int knn_last_candidate_path(knn_ctx* ctx) { return ctx ? ctx->last_kmetric : -1;
 
 int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value) {
   if (!ctx || !key) return knn_fail(KNN_ERR_ARG, "null argument");
-  if (!strcmp(key, "mfma16")) {
+  if (!strcmp(key, "fp16")) {
+    if (value < -1 || value > 1) return knn_fail(KNN_ERR_ARG, "fp16 must be -1, 0 or 1");
+    ctx->tune_fp16 = (int)value;
+  } else if (!strcmp(key, "mfma16")) {
     if (value < -1 || value > 1) return knn_fail(KNN_ERR_ARG, "mfma16 must be -1, 0 or 1");
     ctx->tune_m16 = (int)value;
   } else if (!strcmp(key, "R")) {

@@ -348,6 +348,12 @@ int pad_dim_bf16x3(int d) {
 
 bool bf16x3_streamed(int DP) { return DP > 256; }
 
+// fp16 path: resident 16x16x32 kernel, DP % 32 == 0 and <= 256.
+int pad_dim_fp16(int d) {
+  const int DP = pad_dim((d + 31) / 32 * 32);
+  return (DP <= 256 && DP % 32 == 0) ? DP : -1;
+}
+
 int s3_blocks_per_cu(int R) {
   return R == 8 ? occupancy_of(cand_s3_kernel<8>, 512) : occupancy_of(cand_s3_kernel<16>, 512);
 }

@@ -65,22 +65,23 @@ constexpr int kPubEvery = 8;  // tiles between global-threshold exchanges
 // (not for R = 16 lists or DP > 160, whose registers do not fit: spills).
 template <int DP, int R, int METRIC, int NW>
 __global__ void __launch_bounds__(NW * 64)
-__attribute__((amdgpu_waves_per_eu(DP <= 160 && R <= 8 ? 4 : 1)))
+__attribute__((amdgpu_waves_per_eu((METRIC == 4 ? DP / 2 : DP) <= 160 && R <= 8 ? 4 : 1)))
 cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
             int n_qt, float* __restrict__ out_v, int* __restrict__ out_i, int abl,
-            uint32_t* gthr) {
+            uint32_t* gthr, const float* qfac) {
   // Q32 is deliberately not __restrict__: with it hipcc treats the query
   // fragments as invariant and re-loads them inside the tile loop instead of
   // keeping them in VGPRs (its waits would then also drain the LDS-DMA queue).
   // abl: timing-only ablations (results invalid): bit0 = no staging loads
   // after the first tiles, bit1 = no selection epilogue.  0 in production.
-  constexpr int RSF = DP + 4;               // row stride (floats), HBM and LDS
+  constexpr int DPF = METRIC == 4 ? DP / 2 : DP;  // payload floats per row
+  constexpr int RSF = DPF + 4;              // row stride (floats), HBM and LDS
   constexpr int TPB = KNN_RES_TPB;          // 32-row sub-tiles per staged tile
   constexpr int TBY = kTR * TPB * RSF * 4;  // tile bytes
   constexpr int NG = (TBY + 1023) / 1024;   // 1-KiB LDS-DMA pieces per tile
   constexpr int NB = KNN_RES_NB;            // LDS buffers (prefetch distance NB - 1)
   constexpr int BUFF = NG * 256;            // floats per buffer
-  constexpr int SEED = METRIC == 1 ? DP + 1 : DP;  // seed float within a row
+  constexpr int SEED = METRIC == 1 ? DP + 1 : DPF;  // seed float within a row
   __shared__ __attribute__((aligned(16))) float lds[NB * BUFF];
 
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -91,9 +92,10 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   const int j = lane & 31, h = lane >> 5;
   const int64_t qg = (int64_t)qt * (NW * 32) + wv * 32 + j;
   const float* qrow = Q32 + qg * DP;
-  // METRIC 3 (bf16x3 on 16x16x32): lane l holds queries wv*32 + qb*16 + (l&15),
-  // qb = 0, 1, against rows 4*(l>>4) + i of each 16-row block
-  constexpr bool M16 = METRIC == 3;
+  // METRIC 3 (bf16x3 on 16x16x32) and 4 (fp16 on 16x16x32): lane l holds
+  // queries wv*32 + qb*16 + (l&15), qb = 0, 1, against rows 4*(l>>4) + i of
+  // each 16-row block
+  constexpr bool M16 = METRIC == 3 || METRIC == 4;
   const int c16 = lane & 15, g16 = lane >> 4;
   const int64_t qb0 = (int64_t)qt * (NW * 32) + wv * 32 + c16;  // query of block 0 (+16: block 1)
 
@@ -101,7 +103,20 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   // float4 c holds dims 8c+4h..8c+4h+3 (four 32x32x2 k-steps).  METRIC 2:
   // the row is [qh | ql] in bf16 (-2q split hi/lo); float4 t (t < DP/16) is
   // qh dims 16t+8h..16t+8h+7, float4 DP/16+t the same dims of ql.
-  float4 qf[METRIC != 1 ? DP / 8 : 1];
+  // METRIC 4: fp16 -2q (per-query power-of-two scale), float4 qb*(DP/32)+ks
+  // = dims 32ks + 8*g16 .. +7 of query block qb.
+  constexpr int NQF = METRIC == 1 ? 1 : (METRIC == 4 ? DP / 16 : DP / 8);
+  float4 qf[NQF];
+  float fq[2] = {1.0f, 1.0f};  // METRIC 4: seed rescale to each query's units
+  if constexpr (METRIC == 4) {
+    asm volatile(
+        "global_load_dword %0, %2, off\n\t"
+        "global_load_dword %1, %3, off\n\t"
+        "s_waitcnt vmcnt(0)"
+        : "=&v"(fq[0]), "=&v"(fq[1])
+        : "v"(qfac + qb0), "v"(qfac + qb0 + 16)
+        : "memory");
+  }
   if constexpr (METRIC != 1) {
     // Loaded with inline asm (loads + their vmcnt(0) in one statement): with
     // ordinary loads hipcc places the vmcnt waits for these registers at
@@ -109,12 +124,15 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
     // tile and -- counting all vector-memory ops -- drains the in-flight
     // LDS-DMA pieces of the staging pipeline.
 #pragma unroll
-    for (int c0 = 0; c0 < DP / 8; c0 += 4) {
+    for (int c0 = 0; c0 < NQF; c0 += 4) {
       const float* p[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int c = c0 + u < DP / 8 ? c0 + u : c0;
-        if constexpr (M16) {
+        const int c = c0 + u < NQF ? c0 + u : c0;
+        if constexpr (METRIC == 4) {
+          const int ks = c % (DP / 32), qb = c / (DP / 32);
+          p[u] = Q32 + (qb0 + 16 * qb) * (DP / 2) + 16 * ks + 4 * g16;
+        } else if constexpr (M16) {
           // c = (qb*2 + part)*(DP/32) + ks: dims 32ks + 8*g16 .. +7 of part
           const int ks = c % (DP / 32), pp = (c / (DP / 32)) & 1, qb = c / (DP / 16);
           p[u] = Q32 + (qb0 + 16 * qb) * DP + pp * (DP / 2) + 16 * ks + 4 * g16;
@@ -134,9 +152,9 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
           : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3])
           : "memory");
       qf[c0] = v0;
-      if (c0 + 1 < DP / 8) qf[c0 + 1] = v1;
-      if (c0 + 2 < DP / 8) qf[c0 + 2] = v2;
-      if (c0 + 3 < DP / 8) qf[c0 + 3] = v3;
+      if (c0 + 1 < NQF) qf[c0 + 1] = v1;
+      if (c0 + 2 < NQF) qf[c0 + 2] = v2;
+      if (c0 + 3 < NQF) qf[c0 + 3] = v3;
     }
   }
 
@@ -278,10 +296,26 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float sd = base[(rb * 16 + 4 * g16 + i) * RSF + SEED];
-          acc[rb][0][i] = sd;
-          acc[rb][1][i] = sd;
+          acc[rb][0][i] = METRIC == 4 ? sd * fq[0] : sd;
+          acc[rb][1][i] = METRIC == 4 ? sd * fq[1] : sd;
         }
       }
+      if constexpr (METRIC == 4) {
+        // fp16 x fp16 products are exact in fp32: one MFMA per 32 dims
+#pragma unroll
+        for (int ks = 0; ks < DP / 32; ++ks) {
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb) {
+            const float* ar = base + (rb * 16 + c16) * RSF + 16 * ks + 4 * g16;
+            const f16x8 a = __builtin_bit_cast(f16x8, *(const float4*)ar);
+#pragma unroll
+            for (int qb = 0; qb < 2; ++qb) {
+              const f16x8 b = __builtin_bit_cast(f16x8, qf[qb * (DP / 32) + ks]);
+              acc[rb][qb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, acc[rb][qb], 0, 0, 0);
+            }
+          }
+        }
+      } else {
 #pragma unroll
       for (int ks = 0; ks < DP / 32; ++ks) {
 #pragma unroll
@@ -298,6 +332,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
             acc[rb][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc[rb][qb], 0, 0, 0);
           }
         }
+      }
       }
       const int row0 = (t * TPB + sub) * kTR + 4 * g16;
       if (!(abl & 2)) {
@@ -383,8 +418,9 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
 #undef KNN_ISSUE
 }
 
-// Compile-time dispatch over (R, METRIC): R in {4, 8, 16}; METRIC 0/1/2
-// (2 = bf16x3, resident kernel with DP % 16 == 0 only).
+// Compile-time dispatch over (R, METRIC): R in {4, 8, 16}; METRIC 0..4
+// (2 = bf16x3 with DP % 16 == 0; 3 = bf16x3 and 4 = fp16 on the 16x16x32
+// layout, DP % 32 == 0, R = 4, 8 waves).
 template <class F>
 static void with_R(int R, F f) {
   if (R == 4) f(std::integral_constant<int, 4>{});
@@ -396,7 +432,8 @@ static void with_M(int M, F f) {
   if (M == 0) f(std::integral_constant<int, 0>{});
   else if (M == 1) f(std::integral_constant<int, 1>{});
   else if (M == 2) f(std::integral_constant<int, 2>{});
-  else f(std::integral_constant<int, 3>{});
+  else if (M == 3) f(std::integral_constant<int, 3>{});
+  else f(std::integral_constant<int, 4>{});
 }
 
 template <int DP, int R, int METRIC, int NW>
@@ -404,7 +441,7 @@ static void launch_res(const CandLaunch& c, hipStream_t s) {
   hipLaunchKernelGGL((cand_kernel<DP, R, METRIC, NW>), dim3((unsigned)(c.n_qt * c.S)),
                      dim3(NW * 64), 0, s, c.X32, c.Q32, (int)(c.n_pad / (kTR * KNN_RES_TPB)), c.S,
                      c.n_qt,
-                     c.out_v, c.out_i, c.ablate, c.gthr);
+                     c.out_v, c.out_i, c.ablate, c.gthr, c.qfac);
 }
 
 // Instantiated variants: R in {4, 8, 16}; METRIC 0/2 with NW in {4, 8};
@@ -413,7 +450,7 @@ static void launch_res(const CandLaunch& c, hipStream_t s) {
 template <int DP, int R, int M, int NW>
 constexpr bool res_variant() {
   return (M != 2 || DP % 16 == 0) && (M != 1 || (NW == 4 && R != 4)) &&
-         (M != 3 || (DP % 32 == 0 && R == 4 && NW == 8));
+         (M < 3 || (DP % 32 == 0 && R == 4 && NW == 8));
 }
 
 template <int DP>

@@ -46,6 +46,7 @@ struct TrainDev {
 
 int pad_dim(int d);                 // padded dim the candidate kernels run at
 int pad_dim_bf16x3(int d);          // padded dim of the bf16x3 kernel, -1 if unsupported
+int pad_dim_fp16(int d);            // padded dim of the fp16 kernel (metric 4), -1 if unsupported
 bool bf16x3_streamed(int DP);       // bf16x3 at this DP runs the S3 stream kernel
 constexpr int kS3Rows = 256;        // S3 kernel: train rows per tile = queries per workgroup
 int s3_blocks_per_cu(int R);
@@ -64,7 +65,8 @@ bool cand_supported(int DP);
 int cand_tile_rows(int DP);         // train rows per tile of the kernel serving DP
 int cand_blocks_per_cu(int metric, int DP, int R, int nw);  // resident workgroups per CU
 
-// metric: 0 = L2 fp32 MFMA, 1 = L1 fp32 VALU, 2 = L2 bf16x3 MFMA
+// metric: 0 = L2 fp32 MFMA, 1 = L1 fp32 VALU, 2 = L2 bf16x3 MFMA (32x32x16),
+// 3 = L2 bf16x3 on 16x16x32, 4 = L2 fp16 on 16x16x32 (see knn_cand_res.hip)
 struct CandLaunch {
   int metric, DP, R, S, n_qt;
   int64_t n_pad;
@@ -76,6 +78,7 @@ struct CandLaunch {
   int ablate;   // timing-only ablation bits (0 in production)
   int nw;       // resident kernel: waves (x32 queries) per workgroup, 4 or 8
   uint32_t* gthr;  // resident kernel: per-query global thresholds [m_pad][4] (keys)
+  const float* qfac;  // metric 4: per-query seed rescale 2^(jq - jx) [m_pad]
 };
 constexpr uint32_t kGthrInit = 0xFF800000u;  // order-preserving key of +inf
 
@@ -93,10 +96,16 @@ void launch_cand(const CandLaunch& c, hipStream_t s);
 // or null when the kernel kept none
 // failed queries are appended to rescan_q with rescan_tau = the W-th exact
 // distance among their re-ranked rows (+inf if unknown)
+// Kernel metric 4 keeps proxies in per-query units 2^(jx + jq) (qfac[q] =
+// 2^(jq - jx), sx = 2^jx); qfac null = unscaled proxies.
+struct ProxyScale {
+  const float* qfac;
+  double sx;
+};
 void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int R,
                          const TrainDev& t, const double* Q64, int64_t m, int W, int C,
-                         double f_err, const uint32_t* gthr, const Sink& sink, int* rescan_q,
-                         double* rescan_tau, int* rescan_cnt, hipStream_t s);
+                         double f_err, ProxyScale ps, const uint32_t* gthr, const Sink& sink,
+                         int* rescan_q, double* rescan_tau, int* rescan_cnt, hipStream_t s);
 constexpr int kRescanCap = 1024;  // rows a fast rescan may append per query
 constexpr int kRescanFastMaxDP = 256;  // fast rescan: resident-kernel dimensions
 // Fast rescan of failed queries [f0, f0+nf): scratch qf[nf * t.DP], thr[nf],
@@ -119,6 +128,15 @@ void launch_fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t s);
 // fp64 rows -> [hi(DP) | lo(DP)] bf16 rows of scale*x (candidate metric 2 = L2 via bf16x3)
 // rows of `out` are row_shorts 16-bit words; xl2/xl1 (train only, else null)
 // fill the padded row's seed floats after the 2*DP bf16 payload
+// fp16 images of kernel metric 4 (knn_prep.hip): train rows of DP halves + 4
+// seed floats, scaled by 2^jx; query rows of DP halves of -2 * 2^jq (q - mu)
+// with fac[q] = 2^(jq - jx)
+void launch_prep_half_train(const double* X64, const double* mu, int64_t n, int d, int DP,
+                            int64_t n_pad, int jx, unsigned short* out, const float* xl2,
+                            hipStream_t s);
+void launch_prep_half_queries(const double* Q64, const double* mu, int64_t m, int d, int DP,
+                              int64_t m_pad, int jx, unsigned short* out, float* fac,
+                              hipStream_t s);
 void launch_prep_split(const double* X64, const double* mu, int64_t n, int d, int DP,
                        int64_t n_pad, double scale, unsigned short* out, int row_shorts,
                        const float* xl2, const float* xl1, hipStream_t s);

@@ -53,8 +53,8 @@ void launch_col_mean(const double* X64, int64_t n, int d, double* partial, doubl
 
 // One wave per train row: fp64 x - mu -> fp32 (zero padded to DP),
 // fl32(||x32||^2) seeds for the L2 accumulator, 0 seeds for L1, +inf on pad
-// rows; running max of ||x - mu||_2^2 and ||x - mu||_1 (fp64, non-negative
-// -> ordered as u64 bits).
+// rows; running max of ||x - mu||_2^2, ||x - mu||_1 and max |x_i - mu_i|
+// (fp64, non-negative -> ordered as u64 bits).
 __global__ void __launch_bounds__(256)
 prep_train_kernel(const double* __restrict__ X64, const double* __restrict__ mu, int64_t n, int d,
                   int DP, int64_t n_pad, float* __restrict__ X32, float* __restrict__ xl2,
@@ -62,7 +62,7 @@ prep_train_kernel(const double* __restrict__ X64, const double* __restrict__ mu,
   const int RSF = DP + 4;  // padded row: [x32 (DP) | ||x32||^2, l1 seed, 0, 0]
   const int lane = threadIdx.x & 63;
   const int64_t wstride = (int64_t)gridDim.x * 4;
-  double m2 = 0.0, m1 = 0.0;
+  double m2 = 0.0, m1 = 0.0, mabs = 0.0;
   for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n_pad; row += wstride) {
     double s32 = 0.0, s64 = 0.0, a64 = 0.0;
     for (int c = lane; c < DP; c += 64) {
@@ -72,6 +72,7 @@ prep_train_kernel(const double* __restrict__ X64, const double* __restrict__ mu,
         v = (float)x;
         s64 += x * x;
         a64 += __builtin_fabs(x);
+        mabs = fmax(mabs, __builtin_fabs(x));
       }
       X32[row * RSF + c] = v;
       s32 += (double)v * (double)v;
@@ -91,10 +92,12 @@ prep_train_kernel(const double* __restrict__ X64, const double* __restrict__ mu,
     m2 = fmax(m2, s64);
     m1 = fmax(m1, a64);
   }
+  mabs = wave_max_d(mabs);
   if (lane == 0) {
     // small relative slack covers the order of the fp64 sums above
     atomicMax(&stats[0], (unsigned long long)__double_as_longlong(m2 * (1.0 + 1e-12)));
     atomicMax(&stats[1], (unsigned long long)__double_as_longlong(m1 * (1.0 + 1e-12)));
+    atomicMax(&stats[2], (unsigned long long)__double_as_longlong(mabs));
   }
 }
 
@@ -157,6 +160,78 @@ void launch_prep_split(const double* X64, const double* mu, int64_t n, int d, in
   if (blocks > 16384) blocks = 16384;
   hipLaunchKernelGGL(prep_split_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X64, mu, n, d, DP,
                      n_pad, scale, out, row_shorts, xl2, xl1);
+}
+
+// ---------------------------------- fp16 images (kernel metric 4, d <= 256)
+// Train rows: [fp16(2^jx (x - mu)) (DP halves) | seeds (4 floats)], the seed
+// 2^(2 jx) fl32(||x32||^2) (exact power-of-two scaling; +inf on pad rows).
+// jx puts max |x - mu| * 2^jx in [2^8, 2^9): no fp16 overflow, and values
+// below the fp16 normal range are at most 2^-22 of the largest (their
+// absolute error is in the bound).
+__global__ void __launch_bounds__(256)
+prep_half_train_kernel(const double* __restrict__ X64, const double* __restrict__ mu, int64_t n,
+                       int d, int DP, int64_t n_pad, int jx, unsigned short* __restrict__ out,
+                       const float* __restrict__ xl2) {
+  const int row_shorts = DP + 8;
+  const int64_t total = n_pad * DP;
+  const float s2 = __builtin_ldexpf(1.0f, 2 * jx);
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * 256) {
+    const int64_t row = e / DP;
+    const int c = (int)(e - row * DP);
+    _Float16 h = (_Float16)0.0f;
+    if (row < n && c < d) h = (_Float16)__builtin_ldexp(X64[row * d + c] - mu[c], jx);
+    out[row * row_shorts + c] = __builtin_bit_cast(unsigned short, h);
+    if (c < 4) {
+      float* seed = (float*)(out + row * row_shorts + DP);
+      seed[c] = c == 0 ? xl2[row] * s2 : 0.0f;
+    }
+  }
+}
+
+void launch_prep_half_train(const double* X64, const double* mu, int64_t n, int d, int DP,
+                            int64_t n_pad, int jx, unsigned short* out, const float* xl2,
+                            hipStream_t s) {
+  int64_t blocks = (n_pad * DP + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(prep_half_train_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X64, mu, n, d,
+                     DP, n_pad, jx, out, xl2);
+}
+
+// Query rows: fp16(-2 * 2^jq (q - mu)) (DP halves), one power-of-two scale
+// per query: jq puts max |q - mu| * 2^jq in [2^8, 2^9).  fac[row] =
+// 2^(jq - jx) rescales the train seeds to the query's units inside the
+// kernel, so its proxies are 2^(jx + jq) (||x'||^2 - 2 q'.x').
+__global__ void __launch_bounds__(256)
+prep_half_queries_kernel(const double* __restrict__ Q64, const double* __restrict__ mu, int64_t m,
+                         int d, int DP, int64_t m_pad, int jx, unsigned short* __restrict__ out,
+                         float* __restrict__ fac) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wstride = (int64_t)gridDim.x * 4;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < m_pad; row += wstride) {
+    double amax = 0.0;
+    if (row < m)
+      for (int c = lane; c < d; c += 64) amax = fmax(amax, __builtin_fabs(Q64[row * d + c] - mu[c]));
+    amax = wave_max_d(amax);
+    int e = 0;
+    if (amax > 0.0) (void)__builtin_frexp(amax, &e);  // amax < 2^e
+    const int jq = min(max(9 - e, jx - 100), jx + 100);
+    for (int c = lane; c < DP; c += 64) {
+      _Float16 h = (_Float16)0.0f;
+      if (row < m && c < d) h = (_Float16)__builtin_ldexp(-2.0 * (Q64[row * d + c] - mu[c]), jq);
+      out[row * DP + c] = __builtin_bit_cast(unsigned short, h);
+    }
+    if (lane == 0) fac[row] = row < m ? __builtin_ldexpf(1.0f, jq - jx) : 1.0f;
+  }
+}
+
+void launch_prep_half_queries(const double* Q64, const double* mu, int64_t m, int d, int DP,
+                              int64_t m_pad, int jx, unsigned short* out, float* fac,
+                              hipStream_t s) {
+  int64_t blocks = (m_pad + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(prep_half_queries_kernel, dim3((unsigned)blocks), dim3(256), 0, s, Q64, mu, m,
+                     d, DP, m_pad, jx, out, fac);
 }
 
 __global__ void fill_i32_kernel(int32_t* p, int64_t n, int32_t v) {

@@ -132,13 +132,12 @@ template <int METRIC, int NT, int EPL>
 __global__ void __launch_bounds__(NT)
 merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, int U, int R,
                     TrainDev t, const double* __restrict__ Q64, int W, int Cmax, int C2,
-                    double f_err, const uint32_t* __restrict__ gthr, Sink sink,
+                    double f_err, ProxyScale ps, const uint32_t* __restrict__ gthr, Sink sink,
                     int* __restrict__ rescan_q, double* __restrict__ rescan_tau,
                     int* __restrict__ rescan_cnt) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int s_cn, s_cert;
-  __shared__ float s_lb;
-  __shared__ double s_qa, s_e;
+  __shared__ double s_lb, s_qa, s_e;
   const int d = t.d;
   // the query row is staged in LDS up to kMergeLdsDim dims, else read in place
   const bool q_in_lds = d <= kMergeLdsDim;
@@ -157,15 +156,26 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
 
   if (tid < 64) {
     // error bound of this query's proxies (the candidate operands are centred)
-    double qa = 0.0;
+    double qa = 0.0, q1 = 0.0;
     for (int c = lane; c < d; c += 64) {
       const double x = qv[c] - t.mu[c];
       qa += METRIC == 0 ? x * x : __builtin_fabs(x);
+      q1 += __builtin_fabs(x);
     }
     qa = wave_sum_d(qa) * (1.0 + 1e-12);
-    const double E =
+    double E =
         (METRIC == 0 ? f_err * (t.x2max + 2.1 * __builtin_sqrt(qa) * __builtin_sqrt(t.x2max))
                      : f_err * (qa + t.x1max)) + 1e-30;
+    // scaled proxies (kernel metric 4): proxy = sx * sq * (unscaled), both
+    // powers of two; operand values below the fp16 normal range may lose up
+    // to 2^-14 (scaled units) each: absolute terms of the bound
+    double pinv = 1.0;
+    if (ps.qfac) {
+      const double sq = ps.sx * (double)ps.qfac[q];
+      pinv = 1.0 / (ps.sx * sq);
+      q1 = wave_sum_d(q1) * (1.0 + 1e-12);
+      E += 0x1p-14 * 1.001 * (2.0 * q1 / ps.sx + t.x1max / sq) + t.DP * 0x1p-28 * pinv;
+    }
     // union in registers; min over full lists of their R-th (worst kept) entry
     const float* lv = cv + q * U;
     const int* li = ci + q * U;
@@ -196,7 +206,7 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
         for (int e = 0; e < EPL; ++e) cnt += __popcll(__ballot(f2key(v[e]) <= T));
         if (cnt < W) pre |= 1u << b;
       }
-      const double vw = (double)key2f(pre);
+      const double vw = (double)key2f(pre) * pinv;
       tsel = vw + 2.0 * E + 1e-9 * (__builtin_fabs(vw) + qa + E) + 1e-300;
     }
     float lbx = KNN_INF_F;
@@ -204,7 +214,7 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
 #pragma unroll
     for (int e = 0; e < EPL; ++e) {
       const bool valid = v[e] < KNN_INF_F;
-      const bool sel = valid && (double)v[e] <= tsel;
+      const bool sel = valid && (double)v[e] * pinv <= tsel;
       if (valid && !sel) lbx = fminf(lbx, v[e]);
       const unsigned long long mk = __ballot(sel);
       if (sel) {
@@ -214,6 +224,37 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
       cn += __popcll(mk);
     }
     lbx = wave_min(lbx);
+    if (cn > Cmax) {
+      // more rows inside the selection window than this launch re-ranks:
+      // re-rank the Cmax smallest proxies instead (ties at the cut filled in
+      // lane order).  Rows left out have proxy >= the cut, so the bound
+      // below may still certify; if not, the W-th exact distance of these
+      // rows still bounds the fast rescan.
+      uint32_t pre = 0;  // key of the Cmax-th smallest proxy
+      for (int b = 31; b >= 0; --b) {
+        const uint32_t T = pre | ((1u << b) - 1u);
+        int cnt = 0;
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) cnt += __popcll(__ballot(v[e] < KNN_INF_F && f2key(v[e]) <= T));
+        if (cnt < Cmax) pre |= 1u << b;
+      }
+      cn = 0;
+      for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) {
+          const uint32_t ky = f2key(v[e]);
+          const bool sel = v[e] < KNN_INF_F && (pass == 0 ? ky < pre : ky == pre);
+          const unsigned long long mk = __ballot(sel);
+          if (sel) {
+            const int pos = cn + lanes_below(mk);
+            if (pos < Cmax) di[pos] = id[e];
+          }
+          cn += __popcll(mk);
+        }
+      }
+      cn = min(cn, Cmax);
+      lbx = key2f(pre);
+    }
     // the candidate kernel also filtered with the query's global threshold
     // (cand_kernel): rows it dropped have proxy >= its final value
     float tq = KNN_INF_F;
@@ -223,7 +264,7 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
     }
     if (lane == 0) {
       s_cn = cn;
-      s_lb = fminf(fminf(lbx, mlr), tq);
+      s_lb = (double)fminf(fminf(lbx, mlr), tq) * pinv;
       s_qa = qa;
       s_e = E;
     }
@@ -244,19 +285,19 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
   // certification: every row not re-ranked has proxy >= LB, hence exact
   // distance >= the bound below (rigorous error bound E)
   if (tid == 0) {
-    const float LB = s_lb;
+    const double LB = s_lb;
     bool cert;
-    if (!(LB < KNN_INF_F)) {
+    if (!(LB < KNN_INF_D)) {
       cert = true;  // nothing was left out: every row was re-ranked exactly
     } else if (cn < W) {
       cert = false;
     } else {
       const double dw = dk[W - 1], qa = s_qa, E = s_e;
       if (METRIC == 0) {
-        const double bound = ((double)LB + qa * (1.0 - 2e-12) - E) * (1.0 - 1e-12);
+        const double bound = (LB + qa * (1.0 - 2e-12) - E) * (1.0 - 1e-12);
         cert = bound > dw * dw * (1.0 + 1e-12);
       } else {
-        const double bound = ((double)LB - E) * (1.0 - 1e-12);
+        const double bound = (LB - E) * (1.0 - 1e-12);
         cert = bound > dw * (1.0 + 1e-12);
       }
     }
@@ -286,26 +327,26 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
 template <int METRIC, int NT, int EPL>
 static void launch_mr(const float* cv, const int* ci, int U, int R, const TrainDev& t,
                       const double* Q64, int64_t m, int W, int Cmax, int C2, double f_err,
-                      const uint32_t* gthr, const Sink& sink, int* rescan_q,
+                      ProxyScale ps, const uint32_t* gthr, const Sink& sink, int* rescan_q,
                       double* rescan_tau, int* rescan_cnt, hipStream_t s) {
   const size_t lds = (size_t)(t.d <= kMergeLdsDim ? t.d : 0) * 8 + (size_t)C2 * 8 +
                      (size_t)NT * 17 * 8 + (size_t)C2 * 8;
   hipLaunchKernelGGL((merge_rerank_kernel<METRIC, NT, EPL>), dim3((unsigned)m), dim3(NT), lds, s,
-                     cv, ci, U, R, t, Q64, W, Cmax, C2, f_err, gthr, sink, rescan_q, rescan_tau,
+                     cv, ci, U, R, t, Q64, W, Cmax, C2, f_err, ps, gthr, sink, rescan_q, rescan_tau,
                      rescan_cnt);
 }
 
 void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int R,
                          const TrainDev& t, const double* Q64, int64_t m, int W, int C,
-                         double f_err, const uint32_t* gthr, const Sink& sink, int* rescan_q,
-                         double* rescan_tau, int* rescan_cnt, hipStream_t s) {
+                         double f_err, ProxyScale ps, const uint32_t* gthr, const Sink& sink,
+                         int* rescan_q, double* rescan_tau, int* rescan_cnt, hipStream_t s) {
   if (m <= 0) return;
   const int U = NL * R;  // <= 2 * 64 * 16 (choose_geometry bounds S and R)
   int C2 = 1;
   while (C2 < C) C2 <<= 1;
   const bool big = C2 > 64, wide = U > 1024;
 #define KNN_MR(M_, NT_, EPL_) \
-  launch_mr<M_, NT_, EPL_>(cv, ci, U, R, t, Q64, m, W, C, C2, f_err, gthr, sink, rescan_q, \
+  launch_mr<M_, NT_, EPL_>(cv, ci, U, R, t, Q64, m, W, C, C2, f_err, ps, gthr, sink, rescan_q, \
                            rescan_tau, rescan_cnt, s)
   if (metric == 0) {
     if (big) { if (wide) KNN_MR(0, 256, 32); else KNN_MR(0, 256, 16); }

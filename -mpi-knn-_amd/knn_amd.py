@@ -35,7 +35,7 @@ EXPORTED = (
     "knn_last_geometry", "knn_set_precision", "knn_last_candidate_path", "knn_set_tuning",
     "knn_minmax_device", "knn_normalize_device", "knn_normalize", "knn_group_normalize",
 )
-PRECISION_AUTO, PRECISION_FP32, PRECISION_BF16X3 = 0, 1, 2
+PRECISION_AUTO, PRECISION_FP32, PRECISION_BF16X3, PRECISION_FP16 = 0, 1, 2, 3
 PHASE_PREP, PHASE_CANDIDATE, PHASE_RERANK, PHASE_RESCAN = 0, 1, 2, 3
 
 

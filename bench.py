@@ -318,9 +318,18 @@ def main():
                     % (n, m, d, k, C))
         parallelism = "train-sharded tp%d" % world
 
-    bf16 = main_r["path"] in (2, 3)
-    peak = PEAK_BF16_TFLOPS if bf16 else PEAK_FP32_TFLOPS
-    mfma_mult = 3.0 if bf16 else 1.0  # MFMA flops issued per algorithmic flop
+    path = main_r["path"]
+    bf16 = path in (2, 3)
+    # fp16 / bf16 MFMA share the dense peak; bf16x3 issues 3 MFMA flops per
+    # algorithmic flop, fp16 and fp32 one
+    peak = PEAK_BF16_TFLOPS if path in (2, 3, 4) else PEAK_FP32_TFLOPS
+    mfma_mult = 3.0 if bf16 else 1.0
+    cand_desc = {
+        0: "fp32 MFMA 32x32x2",
+        2: "bf16x3 split (qh.xh+ql.xh+qh.xl) on MFMA 32x32x16 bf16",
+        3: "bf16x3 split (qh.xh+ql.xh+qh.xl) on MFMA 16x16x32 bf16",
+        4: "fp16 operands (power-of-two scaled, centred) on MFMA 16x16x32 f16",
+    }.get(path, "kernel metric %d" % path)
     achieved = flops / main_r["t_cand"] / 1e12
     geom = main_r["geom"]
     n_qt = max(1, geom["workgroups"] // max(1, geom["splits"]))
@@ -339,15 +348,12 @@ def main():
         "higher_is_better": True,
         "scaling": "weak" if args.mode == "query" else "strong",
         "vs_baseline": None,
-        "dtype": "bf16x3" if bf16 else "fp32",
+        "dtype": {2: "bf16x3", 3: "bf16x3", 4: "fp16"}.get(path, "fp32"),
         "data": "synthetic (seeded Gaussian mixture scaled to [0,1) on the 8-bit grid k/256, "
                 "SIFT-like; fp64 inputs)",
         "config": {"workload": workload, "n_train": n, "queries": m, "dim": d, "k": k,
                    "parallelism": parallelism,
-                   "candidate_pass": ("bf16x3 split (qh.xh+ql.xh+qh.xl) on MFMA %s bf16"
-                                      % ("16x16x32" if main_r["path"] == 3 else "32x32x16")
-                                      if bf16 else "fp32 MFMA 32x32x2")
-                                     + " + fused top-R per lane, certified bound",
+                   "candidate_pass": cand_desc + " + fused top-R per lane, certified bound",
                    "rerank": "fp64 exact (reference arithmetic), certified; labels exact",
                    "geometry": geom, "rescanned_queries": main_r["resc"]},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",

@@ -160,23 +160,31 @@ int knn_last_geometry(knn_ctx* ctx, int64_t out[4]);
 
 /* Candidate-pass precision for L2 (the result is the exact fp64 top-k in
  * every mode; this only selects how candidates are found):
- *   AUTO (default): bf16x3 where supported (d <= 256), else fp32;
+ *   AUTO (default): fp16 for batches of >= 4096 queries at d <= 256 (until
+ *         a batch of this train set leaves > 1/16 of its queries to the
+ *         rescan), else bf16x3 (d > 256 on the streamed kernel);
  *   FP32: v_mfma_f32_32x32x2_f32 on fp32 copies;
- *   BF16X3: q.x as qh.xh + ql.xh + qh.xl on v_mfma_f32_32x32x16_bf16
- *           (hi/lo bf16 split of the fp64 values, ~2^-16 relative error).
- * Environment override at knn_create: KNN_PRECISION=fp32|bf16x3. */
+ *   BF16X3: q.x as qh.xh + ql.xh + qh.xl on bf16 MFMA
+ *           (hi/lo bf16 split of the fp64 values, ~2^-16 relative error);
+ *   FP16: q.x on v_mfma_f32_16x16x32_f16 with both operands in fp16 under
+ *         power-of-two scales (~2^-10 relative error), d <= 256.
+ * Environment override at knn_create: KNN_PRECISION=fp32|bf16x3|fp16. */
 #define KNN_PRECISION_AUTO 0
 #define KNN_PRECISION_FP32 1
 #define KNN_PRECISION_BF16X3 2
+#define KNN_PRECISION_FP16 3
 int knn_set_precision(knn_ctx* ctx, int mode);
-/* Candidate kernel flavour of the last search: 0 fp32 L2, 1 fp32 L1, 2 bf16x3 L2. */
+/* Candidate kernel flavour of the last search: 0 fp32 L2, 1 fp32 L1, 2 bf16x3
+ * L2 (32x32x16 MFMA), 3 bf16x3 L2 (16x16x32), 4 fp16 L2 (16x16x32). */
 int knn_last_candidate_path(knn_ctx* ctx);
 
 /* Tuning overrides for experiments (0 = automatic): "R" list entries per
  * lane (4, 8, 16), "S" train splits per query tile (1..64), "nw" waves per
  * candidate workgroup (4 or 8; 32 queries per wave), "ablate" (bits 0/1:
  * timing-only kernel ablations, results invalid; bit 2: no per-query global
- * threshold exchange in the resident kernel, results stay exact). */
+ * threshold exchange in the resident kernel, results stay exact); -1 = auto
+ * for "fp16" (fp16 candidate pass: 0 off, 1 on) and "mfma16" (bf16x3 on the
+ * 16x16x32 layout: 0 off, 1 on). */
 int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value);
 
 /* Synchronise the context's stream. */

@@ -132,18 +132,23 @@ def test_cfg2_full(knn):
     clf = knn.Classifier(0)
     clf.set_train_device(X.data_ptr(), lab.data_ptr(), n, d, C, keep=(X, lab))
     got, idx, dist, flags = classify(knn, clf, Q, k)
+    assert clf.last_candidate_path() == 4, "cfg2 should run the fp16 candidate pass"
     lab_all = lab.cpu().numpy()
     check_properties(X, lab_all, Q, k, got, idx, dist, np.arange(m))
     check_oracle(X, lab_all, Q, k, got, idx, dist, np.arange(0, m, m // 32))
     check_optimal(X, Q, k, dist, np.arange(0, m, m // 512))
     # the other candidate paths give the same exact answer
-    clf.set_tuning("mfma16", 0)  # bf16x3 on 32x32x16
-    got16, idx16, dist16, _ = classify(knn, clf, Q, k)
-    np.testing.assert_array_equal(got16, got)
-    assert (dist16.view(np.int64) == dist.view(np.int64)).all()
+    clf.set_precision(knn.PRECISION_BF16X3)
+    for m16, path in ((1, 3), (0, 2)):  # bf16x3 on 16x16x32, then on 32x32x16
+        clf.set_tuning("mfma16", m16)
+        gotb, idxb, distb, _ = classify(knn, clf, Q, k)
+        assert clf.last_candidate_path() == path
+        np.testing.assert_array_equal(gotb, got)
+        assert (distb.view(np.int64) == dist.view(np.int64)).all()
     clf.set_tuning("mfma16", -1)
     clf.set_precision(knn.PRECISION_FP32)
     got32, idx32, dist32, _ = classify(knn, clf, Q, k)
+    assert clf.last_candidate_path() == 0
     np.testing.assert_array_equal(got32, got)
     assert (dist32.view(np.int64) == dist.view(np.int64)).all()
     clf.close()

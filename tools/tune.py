@@ -3,7 +3,7 @@
 (interleaved rounds, medians; cdna_hip_programming.md §5.4 rule 24).
 Usage: python tools/tune.py [--rounds 5] [--n 1000000 --m 10000 --d 128 --k 10]
 Variants: "prec:R:S[:ablate[:nw]]" e.g. auto:0:0 fp32:8:0 auto:8:0:1:8
-(prec: auto | fp32 | bf16x3 | m16 = bf16x3 on the 16x16x32 MFMA layout)
+(prec: auto | fp32 | bf16x3 | m16 = bf16x3 on the 16x16x32 MFMA layout | fp16)
 (ablate bits: 1 = no staging loads, 2 = no selection epilogue; timing only;
 nw = waves per candidate workgroup, 0 auto / 4 / 8)"""
 import argparse
@@ -38,7 +38,8 @@ def main():
     res = {v: [] for v in a.variants}
     tot = {}
     info = {}
-    prec = {"auto": knn.PRECISION_AUTO, "fp32": knn.PRECISION_FP32, "bf16x3": knn.PRECISION_BF16X3}
+    prec = {"auto": knn.PRECISION_AUTO, "fp32": knn.PRECISION_FP32, "bf16x3": knn.PRECISION_BF16X3,
+            "m16": knn.PRECISION_BF16X3, "fp16": knn.PRECISION_FP16}
     for r in range(a.rounds + 1):
         for v in a.variants:
             parts = v.split(":")
@@ -46,8 +47,8 @@ def main():
             abl = int(parts[3]) if len(parts) > 3 else 0
             nw = int(parts[4]) if len(parts) > 4 else 0
             clf.set_tuning("nw", nw)
-            clf.set_precision(prec["auto" if p == "m16" else p])
-            clf.set_tuning("mfma16", 1 if p == "m16" else (-1 if p == "auto" else 0))
+            clf.set_precision(prec[p])
+            clf.set_tuning("mfma16", 1 if p == "m16" else (0 if p == "bf16x3" else -1))
             clf.set_tuning("R", int(R))
             clf.set_tuning("S", int(S))
             clf.set_tuning("ablate", abl)
