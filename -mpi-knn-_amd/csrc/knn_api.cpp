@@ -205,6 +205,14 @@ static int ensure_bf16x3(knn_ctx* ctx, hipStream_t s) {
   return KNN_OK;
 }
 
+// Exponent jx with max|x_i - mu_i| * 2^jx in [2^8, 2^9); the fp16 path is
+// used only while |jx| <= 60 (its seeds 2^(2 jx) ||x||^2 stay in fp32 range).
+static int fp16_scale_exp(double xamax) {
+  int e = 0;
+  if (xamax > 0.0) (void)std::frexp(xamax, &e);  // xamax < 2^e
+  return 9 - e;
+}
+
 // The fp16 copy of the train rows for kernel metric 4:
 // 2^jx (x - mu) in fp16 with jx from the largest |x_i - mu_i|, + the scaled
 // L2 seeds; same row count as X32, rows of DP/2 + 4 floats.
@@ -213,9 +221,7 @@ static int ensure_fp16(knn_ctx* ctx, hipStream_t s) {
   const int DPh = pad_dim_fp16(t.d);
   if (DPh <= 0) return knn_fail(KNN_ERR_ARG, "fp16 path supports d <= 256");
   if (ctx->DPh == DPh) return KNN_OK;
-  int e = 0;
-  if (ctx->xamax > 0.0) (void)std::frexp(ctx->xamax, &e);  // xamax < 2^e
-  ctx->jx = std::min(std::max(9 - e, -60), 60);
+  ctx->jx = fp16_scale_exp(ctx->xamax);
   int rc;
   if ((rc = ctx->XH.ensure((size_t)t.n_pad * (DPh / 2 + 4) * sizeof(float) + 1024))) return rc;
   launch_prep_half_train(t.X64, t.mu, t.n, t.d, DPh, t.n_pad, ctx->jx,
@@ -230,6 +236,7 @@ static int ensure_fp16(knn_ctx* ctx, hipStream_t s) {
 // Tuning key "fp16": -1 auto, 0 off, 1 on.
 static bool use_fp16(const knn_ctx* ctx, int metric, int64_t m) {
   if (metric != KNN_METRIC_L2 || pad_dim_fp16(ctx->train.d) <= 0) return false;
+  if (std::abs(fp16_scale_exp(ctx->xamax)) > 60) return false;
   if (ctx->tune_fp16 >= 0) return ctx->tune_fp16 > 0;
   if (ctx->precision == KNN_PRECISION_FP16) return true;
   return ctx->precision == KNN_PRECISION_AUTO && !ctx->fp16_off && m >= 4096;

@@ -14,6 +14,17 @@
 #endif
 static_assert(KNN_RES_TPB * knnk::kTR == knnk::kResTileRows || KNN_RES_TPB != 2,
               "default tile rows must match kResTileRows");
+// fp16 kernel (METRIC 4) experiments: sub-tiles per staged tile, per-tile
+// cached quad thresholds, seeds read as one float4 per 4 rows
+#ifndef KNN_M4_TPB
+#define KNN_M4_TPB 4
+#endif
+#ifndef KNN_M4_TE_CACHE
+#define KNN_M4_TE_CACHE 1
+#endif
+#ifndef KNN_M4_SEED4
+#define KNN_M4_SEED4 1
+#endif
 
 namespace knnk {
 
@@ -31,6 +42,9 @@ __device__ __forceinline__ void wait_barrier_x(int extra) {
 }
 
 constexpr int kPubEvery = 8;  // tiles between global-threshold exchanges
+
+template <int METRIC>
+constexpr int res_tpb() { return METRIC == 4 ? KNN_M4_TPB : KNN_RES_TPB; }
 
 // Train rows in HBM (X32 for fp32/L1, XB for bf16x3) share one padded row
 // format of RSF = DP + 4 floats: [payload (DP floats) | ||x32||^2, l1 seed,
@@ -68,7 +82,7 @@ __global__ void __launch_bounds__(NW * 64)
 __attribute__((amdgpu_waves_per_eu((METRIC == 4 ? DP / 2 : DP) <= 160 && R <= 8 ? 4 : 1)))
 cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
             int n_qt, float* __restrict__ out_v, int* __restrict__ out_i, int abl,
-            uint32_t* gthr, const float* qfac) {
+            uint32_t* gthr) {
   // Q32 is deliberately not __restrict__: with it hipcc treats the query
   // fragments as invariant and re-loads them inside the tile loop instead of
   // keeping them in VGPRs (its waits would then also drain the LDS-DMA queue).
@@ -76,7 +90,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   // after the first tiles, bit1 = no selection epilogue.  0 in production.
   constexpr int DPF = METRIC == 4 ? DP / 2 : DP;  // payload floats per row
   constexpr int RSF = DPF + 4;              // row stride (floats), HBM and LDS
-  constexpr int TPB = KNN_RES_TPB;          // 32-row sub-tiles per staged tile
+  constexpr int TPB = res_tpb<METRIC>();    // 32-row sub-tiles per staged tile
   constexpr int TBY = kTR * TPB * RSF * 4;  // tile bytes
   constexpr int NG = (TBY + 1023) / 1024;   // 1-KiB LDS-DMA pieces per tile
   constexpr int NB = KNN_RES_NB;            // LDS buffers (prefetch distance NB - 1)
@@ -103,20 +117,10 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   // float4 c holds dims 8c+4h..8c+4h+3 (four 32x32x2 k-steps).  METRIC 2:
   // the row is [qh | ql] in bf16 (-2q split hi/lo); float4 t (t < DP/16) is
   // qh dims 16t+8h..16t+8h+7, float4 DP/16+t the same dims of ql.
-  // METRIC 4: fp16 -2q (per-query power-of-two scale), float4 qb*(DP/32)+ks
+  // METRIC 4: fp16 -2q (the train set's power-of-two scale), float4 qb*(DP/32)+ks
   // = dims 32ks + 8*g16 .. +7 of query block qb.
   constexpr int NQF = METRIC == 1 ? 1 : (METRIC == 4 ? DP / 16 : DP / 8);
   float4 qf[NQF];
-  float fq[2] = {1.0f, 1.0f};  // METRIC 4: seed rescale to each query's units
-  if constexpr (METRIC == 4) {
-    asm volatile(
-        "global_load_dword %0, %2, off\n\t"
-        "global_load_dword %1, %3, off\n\t"
-        "s_waitcnt vmcnt(0)"
-        : "=&v"(fq[0]), "=&v"(fq[1])
-        : "v"(qfac + qb0), "v"(qfac + qb0 + 16)
-        : "memory");
-  }
   if constexpr (METRIC != 1) {
     // Loaded with inline asm (loads + their vmcnt(0) in one statement): with
     // ordinary loads hipcc places the vmcnt waits for these registers at
@@ -193,9 +197,9 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   // (l & 31) of the wave (lanes 0-15 block 0, 16-31 block 1; 32-63 repeat)
   const uint32_t goff =
       M16 ? (uint32_t)(((int64_t)qt * (NW * 32) + wv * 32 + (lane & 31)) * 16) : (uint32_t)(qg * 16);
-  float tq[NQL];
+  float tq[NQL], te[NQL];
 #pragma unroll
-  for (int b = 0; b < NQL; ++b) tq[b] = KNN_INF_F;
+  for (int b = 0; b < NQL; ++b) tq[b] = te[b] = KNN_INF_F;
   uint32_t last_pub = kKeyInf;
   int x_ops = 0, x_age = -1;  // ops of the pending exchange, tiles since it
 
@@ -224,6 +228,10 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   int cur = 0, nxt = PD;  // buffer of tile it, buffer that tile it+PD goes to
   for (int it = 0; it < my_nt; ++it) {
     const int t = split + it * S;
+    if constexpr (METRIC == 4 && KNN_M4_TE_CACHE) {
+#pragma unroll
+      for (int b = 0; b < NQL; ++b) thr[b] = L[b][R - 1];  // for the exchange below
+    }
     {
       // this wave's pieces of tile `it` have landed once at most the pieces
       // of the (up to PD-1) later tiles already issued remain outstanding;
@@ -282,6 +290,12 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
         }
       }
     }
+    if constexpr (METRIC == 4 && KNN_M4_TE_CACHE) {
+      // the quad's shared filter, refreshed once per staged tile (a stale,
+      // larger value only admits more insertions)
+#pragma unroll
+      for (int b = 0; b < NQL; ++b) te[b] = __builtin_fminf(quad_min(thr[b]), tq[b]);
+    }
 #pragma unroll
     for (int sub = 0; sub < TPB; ++sub) {
     const float* base = lds + cur * BUFF + sub * kTR * RSF;
@@ -293,11 +307,18 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       f32x4 acc[2][2];
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb) {
+        if constexpr (METRIC == 4 && KNN_M4_SEED4) {
+          // the pad of row 4g carries the seeds of rows 4g .. 4g+3
+          const float4 sd = *(const float4*)(base + (rb * 16 + 4 * g16) * RSF + SEED);
+          acc[rb][0] = f32x4{sd.x, sd.y, sd.z, sd.w};
+          acc[rb][1] = acc[rb][0];
+        } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float sd = base[(rb * 16 + 4 * g16 + i) * RSF + SEED];
-          acc[rb][0][i] = METRIC == 4 ? sd * fq[0] : sd;
-          acc[rb][1][i] = METRIC == 4 ? sd * fq[1] : sd;
+          acc[rb][0][i] = sd;
+          acc[rb][1][i] = sd;
+        }
         }
       }
       if constexpr (METRIC == 4) {
@@ -336,9 +357,15 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       }
       const int row0 = (t * TPB + sub) * kTR + 4 * g16;
       if (!(abl & 2)) {
+        if constexpr (METRIC == 4 && KNN_M4_TE_CACHE) {
 #pragma unroll
-        for (int qb = 0; qb < 2; ++qb)
-          select_quad<R>(acc[0][qb], acc[1][qb], row0, L[qb], I[qb], thr[qb], tq[qb]);
+          for (int qb = 0; qb < 2; ++qb)
+            select_quad_te<R>(acc[0][qb], acc[1][qb], row0, L[qb], I[qb], te[qb]);
+        } else {
+#pragma unroll
+          for (int qb = 0; qb < 2; ++qb)
+            select_quad<R>(acc[0][qb], acc[1][qb], row0, L[qb], I[qb], thr[qb], tq[qb]);
+        }
       } else if (acc[0][0][0] == 1234.5f && acc[1][1][3] == 1234.5f) {
         thr[0] = acc[0][1][2];  // keep the accumulators live
       }
@@ -439,9 +466,9 @@ static void with_M(int M, F f) {
 template <int DP, int R, int METRIC, int NW>
 static void launch_res(const CandLaunch& c, hipStream_t s) {
   hipLaunchKernelGGL((cand_kernel<DP, R, METRIC, NW>), dim3((unsigned)(c.n_qt * c.S)),
-                     dim3(NW * 64), 0, s, c.X32, c.Q32, (int)(c.n_pad / (kTR * KNN_RES_TPB)), c.S,
+                     dim3(NW * 64), 0, s, c.X32, c.Q32, (int)(c.n_pad / (kTR * res_tpb<METRIC>())), c.S,
                      c.n_qt,
-                     c.out_v, c.out_i, c.ablate, c.gthr, c.qfac);
+                     c.out_v, c.out_i, c.ablate, c.gthr);
 }
 
 // Instantiated variants: R in {4, 8, 16}; METRIC 0/2 with NW in {4, 8};

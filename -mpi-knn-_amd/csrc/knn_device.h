@@ -249,6 +249,28 @@ __device__ __forceinline__ void select_quad(const f32x4& a, const f32x4& b, int 
   }
 }
 
+// select_quad with the quad's filter te kept by the caller (refreshed from
+// the 4 lanes' thresholds once per staged tile); an insertion lowers it to
+// this lane's new R-th entry.  thr is then L[R-1] and needs no copy.
+template <int R>
+__device__ __forceinline__ void select_quad_te(const f32x4& a, const f32x4& b, int row0,
+                                               float (&L)[R], int (&I)[R], float& te) {
+  const float mn = __builtin_fminf(__builtin_fminf(__builtin_fminf(a[0], a[1]),
+                                                   __builtin_fminf(a[2], a[3])),
+                                   __builtin_fminf(__builtin_fminf(b[0], b[1]),
+                                                   __builtin_fminf(b[2], b[3])));
+  if (mn < te) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float v = i < 4 ? a[i] : b[i - 4];
+      if (v < te) {
+        list_insert<R>(L, I, v, row0 + (i < 4 ? i : 16 + i - 4));
+        te = __builtin_fminf(te, L[R - 1]);
+      }
+    }
+  }
+}
+
 // Lists are stored [query][split][half][R] so a query's 2S lists are contiguous.
 template <int R>
 __device__ __forceinline__ void write_lists(float* __restrict__ out_v, int* __restrict__ out_i,

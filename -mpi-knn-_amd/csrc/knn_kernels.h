@@ -78,7 +78,7 @@ struct CandLaunch {
   int ablate;   // timing-only ablation bits (0 in production)
   int nw;       // resident kernel: waves (x32 queries) per workgroup, 4 or 8
   uint32_t* gthr;  // resident kernel: per-query global thresholds [m_pad][4] (keys)
-  const float* qfac;  // metric 4: per-query seed rescale 2^(jq - jx) [m_pad]
+  const float* qfac;  // metric 4: per-query validity (1, or 0 = out of fp16 range) [m_pad]
 };
 constexpr uint32_t kGthrInit = 0xFF800000u;  // order-preserving key of +inf
 
@@ -96,8 +96,9 @@ void launch_cand(const CandLaunch& c, hipStream_t s);
 // or null when the kernel kept none
 // failed queries are appended to rescan_q with rescan_tau = the W-th exact
 // distance among their re-ranked rows (+inf if unknown)
-// Kernel metric 4 keeps proxies in per-query units 2^(jx + jq) (qfac[q] =
-// 2^(jq - jx), sx = 2^jx); qfac null = unscaled proxies.
+// Kernel metric 4 keeps proxies in units sx^2 = 2^(2 jx); qfac[q] = 1, or 0
+// when the query's proxies are void (out of the fp16 range: sent to the
+// rescan); qfac null = unscaled proxies.
 struct ProxyScale {
   const float* qfac;
   double sx;
@@ -129,8 +130,8 @@ void launch_fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t s);
 // rows of `out` are row_shorts 16-bit words; xl2/xl1 (train only, else null)
 // fill the padded row's seed floats after the 2*DP bf16 payload
 // fp16 images of kernel metric 4 (knn_prep.hip): train rows of DP halves + 4
-// seed floats, scaled by 2^jx; query rows of DP halves of -2 * 2^jq (q - mu)
-// with fac[q] = 2^(jq - jx)
+// seed floats, scaled by 2^jx; query rows of DP halves of -2 * 2^jx (q - mu)
+// with fac[q] = 1 (0: out of the fp16 range, zero operands)
 void launch_prep_half_train(const double* X64, const double* mu, int64_t n, int d, int DP,
                             int64_t n_pad, int jx, unsigned short* out, const float* xl2,
                             hipStream_t s);

@@ -183,8 +183,10 @@ prep_half_train_kernel(const double* __restrict__ X64, const double* __restrict_
     if (row < n && c < d) h = (_Float16)__builtin_ldexp(X64[row * d + c] - mu[c], jx);
     out[row * row_shorts + c] = __builtin_bit_cast(unsigned short, h);
     if (c < 4) {
+      // slot 0: the row's own seed; the pad of row 4g also carries the seeds
+      // of rows 4g+1 .. 4g+3 (one float4 read per 4 rows; n_pad % 4 == 0)
       float* seed = (float*)(out + row * row_shorts + DP);
-      seed[c] = c == 0 ? xl2[row] * s2 : 0.0f;
+      seed[c] = (c == 0 || (row & 3) == 0) ? xl2[row + c] * s2 : 0.0f;
     }
   }
 }
@@ -198,10 +200,11 @@ void launch_prep_half_train(const double* X64, const double* mu, int64_t n, int 
                      DP, n_pad, jx, out, xl2);
 }
 
-// Query rows: fp16(-2 * 2^jq (q - mu)) (DP halves), one power-of-two scale
-// per query: jq puts max |q - mu| * 2^jq in [2^8, 2^9).  fac[row] =
-// 2^(jq - jx) rescales the train seeds to the query's units inside the
-// kernel, so its proxies are 2^(jx + jq) (||x'||^2 - 2 q'.x').
+// Query rows: fp16(-2 * 2^jx (q - mu)) (DP halves): the train set's scale,
+// so the kernel's proxies are 2^(2 jx) (||x'||^2 - 2 q'.x') with no per-query
+// rescaling.  fac[row] = 1, or 0 when 2 |q_i - mu_i| 2^jx would leave the
+// fp16 range (a query ~64x farther out than any train row): its proxies are
+// not used and the merge sends it to the exact rescan.
 __global__ void __launch_bounds__(256)
 prep_half_queries_kernel(const double* __restrict__ Q64, const double* __restrict__ mu, int64_t m,
                          int d, int DP, int64_t m_pad, int jx, unsigned short* __restrict__ out,
@@ -212,16 +215,14 @@ prep_half_queries_kernel(const double* __restrict__ Q64, const double* __restric
     double amax = 0.0;
     if (row < m)
       for (int c = lane; c < d; c += 64) amax = fmax(amax, __builtin_fabs(Q64[row * d + c] - mu[c]));
-    amax = wave_max_d(amax);
-    int e = 0;
-    if (amax > 0.0) (void)__builtin_frexp(amax, &e);  // amax < 2^e
-    const int jq = min(max(9 - e, jx - 100), jx + 100);
+    // out of range (or NaN): zero operands (finite proxies) and fac = 0
+    const bool ok = __builtin_ldexp(2.0 * wave_max_d(amax), jx) < 65000.0;
     for (int c = lane; c < DP; c += 64) {
       _Float16 h = (_Float16)0.0f;
-      if (row < m && c < d) h = (_Float16)__builtin_ldexp(-2.0 * (Q64[row * d + c] - mu[c]), jq);
+      if (ok && row < m && c < d) h = (_Float16)__builtin_ldexp(-2.0 * (Q64[row * d + c] - mu[c]), jx);
       out[row * DP + c] = __builtin_bit_cast(unsigned short, h);
     }
-    if (lane == 0) fac[row] = row < m ? __builtin_ldexpf(1.0f, jq - jx) : 1.0f;
+    if (lane == 0) fac[row] = ok ? 1.0f : 0.0f;
   }
 }
 

@@ -171,10 +171,13 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
     // to 2^-14 (scaled units) each: absolute terms of the bound
     double pinv = 1.0;
     if (ps.qfac) {
-      const double sq = ps.sx * (double)ps.qfac[q];
+      // qfac[q] = 0: the query left the fp16 range, its proxies are void
+      const double f = ps.qfac[q] > 0.0f ? (double)ps.qfac[q] : 1.0;
+      const double sq = ps.sx * f;
       pinv = 1.0 / (ps.sx * sq);
       q1 = wave_sum_d(q1) * (1.0 + 1e-12);
       E += 0x1p-14 * 1.001 * (2.0 * q1 / ps.sx + t.x1max / sq) + t.DP * 0x1p-28 * pinv;
+      if (!(ps.qfac[q] > 0.0f)) E = KNN_INF_D;
     }
     // union in registers; min over full lists of their R-th (worst kept) entry
     const float* lv = cv + q * U;

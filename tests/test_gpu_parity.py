@@ -156,6 +156,20 @@ def test_duplicates_force_rescan(clf, knn):
     assert (flags[:32] & knn.FLAG_EXACT_RESCAN).all()
 
 
+def test_scale_extremes(clf, knn):
+    """Operand scaling edge cases of the reduced-precision candidate passes:
+    queries far outside the train range (fp16 overflow -> rescan), a train
+    set of tiny magnitude, and one of huge magnitude; exact results in every
+    mode."""
+    rng = np.random.default_rng(19)
+    tr, lab, te = _mix(rng, 3000, 96, 64, 4)
+    te[:8] *= 1e4                    # ~1e4 x the train spread
+    te[8:12] = 1e12
+    run_case(clf, knn, tr, lab, te, 7, 0, 4)
+    run_case(clf, knn, tr * 1e-12, lab, te * 1e-12, 7, 0, 4)
+    run_case(clf, knn, tr * 1e12, lab, te * 1e12, 7, 0, 4)
+
+
 def test_integer_ties(clf, knn):
     """SIFT-like integer data: many exact distance ties."""
     rng = np.random.default_rng(11)
