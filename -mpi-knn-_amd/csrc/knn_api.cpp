@@ -146,17 +146,29 @@ static int build_train(knn_ctx* ctx, const double* dX, const int32_t* dlab, int6
   if ((rc = ctx->mu_part.ensure((size_t)col_mean_blocks(n) * d * sizeof(double)))) return rc;
   launch_col_mean(dX, n, d, (double*)ctx->mu_part.p, (double*)ctx->mu.p, ctx->stream);
   HIP_TRY(hipMemsetAsync(ctx->stats.p, 0, 3 * sizeof(unsigned long long), ctx->stream));
-  launch_prep_train(dX, (const double*)ctx->mu.p, n, d, DP, n_pad, (float*)ctx->X32.p,
-                    (float*)ctx->xl2.p, (float*)ctx->xl1.p, (unsigned long long*)ctx->stats.p,
-                    ctx->stream);
+  unsigned long long* st_d = (unsigned long long*)ctx->stats.p;
+  // operand scale 2^jx: max |x_i - mu_i| * 2^jx in [2^8, 2^9) (knn_prep.hip)
+  launch_absmax(dX, (const double*)ctx->mu.p, n, d, st_d + 2, ctx->stream);
   HIP_TRY(hipGetLastError());
-  unsigned long long st[3];
-  HIP_TRY(hipMemcpyAsync(st, ctx->stats.p, sizeof st, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipMemcpyAsync(ctx->h_stats + 2, st_d + 2, 8, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  memcpy(&ctx->xamax, &ctx->h_stats[2], 8);
+  int e = 0;
+  if (ctx->xamax > 0.0) (void)std::frexp(ctx->xamax, &e);  // xamax < 2^e
+  // |x - mu| up to 2^400 (beyond, fp32 operands could overflow); tiny data
+  // is scaled up at most 2^450 (smaller values are covered by the bound's
+  // absolute terms)
+  if (!(ctx->xamax < std::ldexp(1.0, 400)))
+    return knn_fail(KNN_ERR_ARG, "train values out of range (|x - mean| must be < 2^400 and finite)");
+  const int jx = std::min(9 - e, 450);
+  launch_prep_train(dX, (const double*)ctx->mu.p, n, d, DP, n_pad, jx, (float*)ctx->X32.p,
+                    (float*)ctx->xl2.p, (float*)ctx->xl1.p, st_d, ctx->stream);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(ctx->h_stats, st_d, 2 * 8, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   double x2, x1;
-  memcpy(&x2, &st[0], 8);
-  memcpy(&x1, &st[1], 8);
-  memcpy(&ctx->xamax, &st[2], 8);
+  memcpy(&x2, &ctx->h_stats[0], 8);
+  memcpy(&x1, &ctx->h_stats[1], 8);
   TrainDev& t = ctx->train;
   t.X64 = dX;
   t.mu = (const double*)ctx->mu.p;
@@ -170,6 +182,7 @@ static int build_train(knn_ctx* ctx, const double* dX, const int32_t* dlab, int6
   t.DP = DP;
   t.x2max = x2;
   t.x1max = x1;
+  t.jx = jx;
   ctx->class_cnt = class_cnt;
   ctx->idx_off = idx_off;
   ctx->DPb = 0;  // bf16x3 / fp16 copies are rebuilt lazily for the new train set
@@ -193,11 +206,11 @@ static int ensure_bf16x3(knn_ctx* ctx, hipStream_t s) {
     const int64_t n3 = (t.n + kS3Rows - 1) / kS3Rows * kS3Rows;
     if ((rc = ctx->XB.ensure((size_t)n3 * DPb * 4))) return rc;
     if ((rc = ctx->XS.ensure((size_t)n3 * sizeof(float)))) return rc;
-    launch_prep_split_tiled(t.X64, t.mu, t.n, t.d, DPb, n3, 1.0, (unsigned short*)ctx->XB.p, t.xinit_l2,
+    launch_prep_split_tiled(t.X64, t.mu, t.n, t.d, DPb, n3, std::ldexp(1.0, t.jx), (unsigned short*)ctx->XB.p, t.xinit_l2,
                             (float*)ctx->XS.p, s);
   } else {
     if ((rc = ctx->XB.ensure((size_t)t.n_pad * (DPb + 4) * sizeof(float) + 1024))) return rc;
-    launch_prep_split(t.X64, t.mu, t.n, t.d, DPb, t.n_pad, 1.0, (unsigned short*)ctx->XB.p,
+    launch_prep_split(t.X64, t.mu, t.n, t.d, DPb, t.n_pad, std::ldexp(1.0, t.jx), (unsigned short*)ctx->XB.p,
                       2 * (DPb + 4), t.xinit_l2, t.xinit_l1, s);
   }
   HIP_TRY(hipGetLastError());
@@ -205,26 +218,17 @@ static int ensure_bf16x3(knn_ctx* ctx, hipStream_t s) {
   return KNN_OK;
 }
 
-// Exponent jx with max|x_i - mu_i| * 2^jx in [2^8, 2^9); the fp16 path is
-// used only while |jx| <= 60 (its seeds 2^(2 jx) ||x||^2 stay in fp32 range).
-static int fp16_scale_exp(double xamax) {
-  int e = 0;
-  if (xamax > 0.0) (void)std::frexp(xamax, &e);  // xamax < 2^e
-  return 9 - e;
-}
-
 // The fp16 copy of the train rows for kernel metric 4:
-// 2^jx (x - mu) in fp16 with jx from the largest |x_i - mu_i|, + the scaled
-// L2 seeds; same row count as X32, rows of DP/2 + 4 floats.
+// 2^jx (x - mu) in fp16 (the operand scale of every path) + the L2 seeds;
+// same row count as X32, rows of DP/2 + 4 floats.
 static int ensure_fp16(knn_ctx* ctx, hipStream_t s) {
   const TrainDev& t = ctx->train;
   const int DPh = pad_dim_fp16(t.d);
   if (DPh <= 0) return knn_fail(KNN_ERR_ARG, "fp16 path supports d <= 256");
   if (ctx->DPh == DPh) return KNN_OK;
-  ctx->jx = fp16_scale_exp(ctx->xamax);
   int rc;
   if ((rc = ctx->XH.ensure((size_t)t.n_pad * (DPh / 2 + 4) * sizeof(float) + 1024))) return rc;
-  launch_prep_half_train(t.X64, t.mu, t.n, t.d, DPh, t.n_pad, ctx->jx,
+  launch_prep_half_train(t.X64, t.mu, t.n, t.d, DPh, t.n_pad, t.jx,
                          (unsigned short*)ctx->XH.p, t.xinit_l2, s);
   HIP_TRY(hipGetLastError());
   ctx->DPh = DPh;
@@ -236,7 +240,6 @@ static int ensure_fp16(knn_ctx* ctx, hipStream_t s) {
 // Tuning key "fp16": -1 auto, 0 off, 1 on.
 static bool use_fp16(const knn_ctx* ctx, int metric, int64_t m) {
   if (metric != KNN_METRIC_L2 || pad_dim_fp16(ctx->train.d) <= 0) return false;
-  if (std::abs(fp16_scale_exp(ctx->xamax)) > 60) return false;
   if (ctx->tune_fp16 >= 0) return ctx->tune_fp16 > 0;
   if (ctx->precision == KNN_PRECISION_FP16) return true;
   return ctx->precision == KNN_PRECISION_AUTO && !ctx->fp16_off && m >= 4096;
@@ -409,7 +412,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   const int NL = (kmetric >= 3 ? 4 : 2) * S;
   C = std::min(C, NL * R);
   if ((rc = ctx->Q32.ensure((size_t)m_pad * DP * sizeof(float)))) return rc;
-  if (kmetric == 4 && (rc = ctx->qfac.ensure((size_t)m_pad * sizeof(float)))) return rc;
+  if ((rc = ctx->qvalid.ensure((size_t)m_pad * sizeof(float)))) return rc;
   if ((rc = ctx->cand_v.ensure((size_t)m_pad * NL * R * sizeof(float)))) return rc;
   if ((rc = ctx->cand_i.ensure((size_t)m_pad * NL * R * sizeof(int)))) return rc;
   // per-query global thresholds of the resident candidate kernel
@@ -428,18 +431,24 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   ctx->geom[3] = C;
   const bool tm = ctx->timing;
   if (tm) HIP_TRY(hipEventRecord(ctx->ev[0], s));
+  // query operands: scale * 2^jx (q - mu), scale -2 for L2; a query whose
+  // operands would leave the format's range (fp16: 65000, else 2^100) is
+  // marked void and goes to the exact rescan
+  const double qscale = metric == KNN_METRIC_L2 ? -2.0 : 1.0;
+  float* qvalid = (float*)ctx->qvalid.p;
+  launch_query_check(dQ, t.mu, m, t.d, m_pad, qscale, t.jx,
+                     kmetric == 4 ? 65000.0 : std::ldexp(1.0, 100), qvalid, s);
   if (s3)
-    launch_prep_split_tiled(dQ, t.mu, m, t.d, DP, m_pad, -2.0, (unsigned short*)ctx->Q32.p, nullptr,
-                            nullptr, s);
+    launch_prep_split_tiled(dQ, t.mu, m, t.d, DP, m_pad, std::ldexp(qscale, t.jx),
+                            (unsigned short*)ctx->Q32.p, nullptr, nullptr, s);
   else if (kmetric == 4)
-    launch_prep_half_queries(dQ, t.mu, m, t.d, DP, m_pad, ctx->jx, (unsigned short*)ctx->Q32.p,
-                             (float*)ctx->qfac.p, s);
+    launch_prep_half_queries(dQ, t.mu, m, t.d, DP, m_pad, t.jx, (unsigned short*)ctx->Q32.p,
+                             qvalid, s);
   else if (kmetric == 2 || kmetric == 3)
-    launch_prep_split(dQ, t.mu, m, t.d, DP, m_pad, -2.0, (unsigned short*)ctx->Q32.p, 2 * DP, nullptr,
-                      nullptr, s);
+    launch_prep_split(dQ, t.mu, m, t.d, DP, m_pad, std::ldexp(qscale, t.jx),
+                      (unsigned short*)ctx->Q32.p, 2 * DP, nullptr, nullptr, s);
   else
-    launch_prep_queries(dQ, t.mu, m, t.d, DP, m_pad, metric == 0 ? -2.0f : 1.0f,
-                        (float*)ctx->Q32.p, s);
+    launch_prep_queries(dQ, t.mu, m, t.d, DP, m_pad, qscale, t.jx, (float*)ctx->Q32.p, s);
   if (tm) HIP_TRY(hipEventRecord(ctx->ev[1], s));
   CandLaunch cl{};
   cl.metric = kmetric;
@@ -456,7 +465,6 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   cl.ablate = ctx->tune_ablate;
   cl.nw = nw;
   cl.gthr = use_gthr ? (uint32_t*)ctx->gthr.p : nullptr;
-  cl.qfac = kmetric == 4 ? (const float*)ctx->qfac.p : nullptr;
   if (use_gthr) launch_fill_i32((int32_t*)ctx->gthr.p, m_pad * 4, (int32_t)kGthrInit, s);
   if (s3)
     launch_cand_s3((const unsigned short*)ctx->XB.p, (const float*)ctx->XS.p,
@@ -468,7 +476,9 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   if (tm) HIP_TRY(hipEventRecord(ctx->ev[2], s));
   HIP_TRY(hipMemsetAsync(ctx->rescan_cnt.p, 0, sizeof(int), s));
   launch_merge_rerank(metric, (const float*)ctx->cand_v.p, (const int*)ctx->cand_i.p, NL, R, t, dQ,
-                      m, W, C, err_factor(kmetric, DP), ProxyScale{cl.qfac, std::ldexp(1.0, ctx->jx)},
+                      m, W, C, err_factor(kmetric, DP),
+                      kmetric == 4 ? ProxyScale{qvalid, 0x1p-14, 0x1p-28}
+                                   : ProxyScale{qvalid, 0x1p-125, 0x1p-124},
                       cl.gthr, sink, (int*)ctx->rescan_q.p,
                       (double*)ctx->rescan_tau.p, (int*)ctx->rescan_cnt.p, s);
   HIP_TRY(hipGetLastError());

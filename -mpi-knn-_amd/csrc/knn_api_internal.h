@@ -18,6 +18,7 @@ struct knn_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   int* h_count = nullptr;  // pinned
+  unsigned long long h_stats[3] = {0, 0, 0};  // train statistics read back at build
   bool trained = false;
   int class_cnt = 0;
   int64_t idx_off = 0;
@@ -27,7 +28,6 @@ struct knn_ctx {
   int precision = 0;     // KNN_PRECISION_*
   int DPb = 0;           // padded dim of the bf16x3 copy (0 = not built)
   int DPh = 0;           // padded dim of the fp16 copy (0 = not built)
-  int jx = 0;            // fp16 copy: train operands scaled by 2^jx
   double xamax = 0.0;    // max |x_i - mu_i| over the train set
   bool fp16_off = false; // AUTO: fp16 candidate pass retired for this train set
                          // (a batch certified too few queries, see knn_run_search)
@@ -46,14 +46,14 @@ struct knn_ctx {
   // train-side HBM
   DevBuf X64_own, lab_own, X32, xl2, xl1, stats, XB, XS, XH, mu, mu_part;
   // per-classify workspace
-  DevBuf Q64, Q32, qfac, cand_v, cand_i, gthr, rescan_q, rescan_tau, rescan_cnt, ra_k, ra_i, rb_k,
+  DevBuf Q64, Q32, qvalid, cand_v, cand_i, gthr, rescan_q, rescan_tau, rescan_cnt, ra_k, ra_i, rb_k,
       rb_i, fr_cnt, fr_buf, fr_q, slow_q;
   // host-API outputs
   DevBuf o_lab, o_idx, o_dist, o_flags;
   // normalisation: per-thread partial max/min, bounds, host-API staging
   DevBuf nrm_part, nrm_mm, nrm_X;
   std::vector<DevBuf*> all_bufs() {
-    return {&X64_own, &lab_own, &X32, &xl2, &xl1, &stats, &XB, &XS, &XH, &mu, &mu_part, &Q64, &Q32, &qfac, &cand_v, &cand_i, &gthr, &rescan_tau, &fr_cnt, &fr_buf, &fr_q, &slow_q,
+    return {&X64_own, &lab_own, &X32, &xl2, &xl1, &stats, &XB, &XS, &XH, &mu, &mu_part, &Q64, &Q32, &qvalid, &cand_v, &cand_i, &gthr, &rescan_tau, &fr_cnt, &fr_buf, &fr_q, &slow_q,
             &rescan_q, &rescan_cnt, &ra_k, &ra_i, &rb_k, &rb_i, &o_lab, &o_idx, &o_dist,
             &o_flags, &nrm_part, &nrm_mm, &nrm_X};
   }

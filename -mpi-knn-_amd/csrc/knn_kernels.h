@@ -42,6 +42,7 @@ struct TrainDev {
   int64_t n, n_pad;
   int d, DP;
   double x2max, x1max;   // max ||x - mu||_2^2, max ||x - mu||_1 over the train rows
+  int jx;                // candidate operands are 2^jx (x - mu) (knn_prep.hip)
 };
 
 int pad_dim(int d);                 // padded dim the candidate kernels run at
@@ -78,7 +79,6 @@ struct CandLaunch {
   int ablate;   // timing-only ablation bits (0 in production)
   int nw;       // resident kernel: waves (x32 queries) per workgroup, 4 or 8
   uint32_t* gthr;  // resident kernel: per-query global thresholds [m_pad][4] (keys)
-  const float* qfac;  // metric 4: per-query validity (1, or 0 = out of fp16 range) [m_pad]
 };
 constexpr uint32_t kGthrInit = 0xFF800000u;  // order-preserving key of +inf
 
@@ -86,22 +86,27 @@ constexpr uint32_t kGthrInit = 0xFF800000u;  // order-preserving key of +inf
 int col_mean_blocks(int64_t n);  // rows of the `partial` scratch (x d doubles)
 void launch_col_mean(const double* X64, int64_t n, int d, double* partial, double* mu,
                      hipStream_t s);
+void launch_absmax(const double* X64, const double* mu, int64_t n, int d, unsigned long long* out,
+                   hipStream_t s);
 void launch_prep_train(const double* X64, const double* mu, int64_t n, int d, int DP,
-                       int64_t n_pad, float* X32, float* xl2, float* xl1,
+                       int64_t n_pad, int jx, float* X32, float* xl2, float* xl1,
                        unsigned long long* stats, hipStream_t s);
+void launch_query_check(const double* Q64, const double* mu, int64_t m, int d, int64_t m_pad,
+                        double scale, int jx, double limit, float* valid, hipStream_t s);
 void launch_prep_queries(const double* Q64, const double* mu, int64_t m, int d, int DP,
-                         int64_t m_pad, float scale, float* Q32, hipStream_t s);
+                         int64_t m_pad, double scale, int jx, float* Q32, hipStream_t s);
 void launch_cand(const CandLaunch& c, hipStream_t s);
 // gthr: the candidate kernel's per-query global thresholds ([m_pad][4] keys)
 // or null when the kernel kept none
 // failed queries are appended to rescan_q with rescan_tau = the W-th exact
 // distance among their re-ranked rows (+inf if unknown)
-// Kernel metric 4 keeps proxies in units sx^2 = 2^(2 jx); qfac[q] = 1, or 0
-// when the query's proxies are void (out of the fp16 range: sent to the
-// rescan); qfac null = unscaled proxies.
+// Proxies are in units 2^(2 t.jx) (L2) / 2^t.jx (L1).  valid[q] = 0: the
+// query's operands left the format's range, its proxies are void (exact
+// rescan).  ue / up: absolute error per operand element / per product in
+// scaled units, for values outside the format's normal range.
 struct ProxyScale {
-  const float* qfac;
-  double sx;
+  const float* valid;
+  double ue, up;
 };
 void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int R,
                          const TrainDev& t, const double* Q64, int64_t m, int W, int C,
@@ -131,12 +136,12 @@ void launch_fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t s);
 // fill the padded row's seed floats after the 2*DP bf16 payload
 // fp16 images of kernel metric 4 (knn_prep.hip): train rows of DP halves + 4
 // seed floats, scaled by 2^jx; query rows of DP halves of -2 * 2^jx (q - mu)
-// with fac[q] = 1 (0: out of the fp16 range, zero operands)
+// (zero for queries launch_query_check marked invalid)
 void launch_prep_half_train(const double* X64, const double* mu, int64_t n, int d, int DP,
                             int64_t n_pad, int jx, unsigned short* out, const float* xl2,
                             hipStream_t s);
 void launch_prep_half_queries(const double* Q64, const double* mu, int64_t m, int d, int DP,
-                              int64_t m_pad, int jx, unsigned short* out, float* fac,
+                              int64_t m_pad, int jx, unsigned short* out, const float* valid,
                               hipStream_t s);
 void launch_prep_split(const double* X64, const double* mu, int64_t n, int d, int DP,
                        int64_t n_pad, double scale, unsigned short* out, int row_shorts,

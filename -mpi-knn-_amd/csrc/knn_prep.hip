@@ -51,28 +51,56 @@ void launch_col_mean(const double* X64, int64_t n, int d, double* partial, doubl
                      mu);
 }
 
-// One wave per train row: fp64 x - mu -> fp32 (zero padded to DP),
+// max |x_i - mu_i| over the train set (fp64, non-negative -> ordered as
+// u64 bits): fixes the operand scale 2^jx before any rounding to fp32.
+__global__ void __launch_bounds__(256)
+absmax_kernel(const double* __restrict__ X64, const double* __restrict__ mu, int64_t n, int d,
+              unsigned long long* __restrict__ out) {
+  double m = 0.0;
+  const int64_t total = n * d;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * 256)
+    m = fmax(m, __builtin_fabs(X64[e] - mu[e % d]));
+  m = wave_max_d(m);
+  if ((threadIdx.x & 63) == 0) atomicMax(out, (unsigned long long)__double_as_longlong(m));
+}
+
+void launch_absmax(const double* X64, const double* mu, int64_t n, int d, unsigned long long* out,
+                   hipStream_t s) {
+  int64_t blocks = (n * d + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(absmax_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X64, mu, n, d, out);
+}
+
+// Operand scale.  Every candidate-pass operand is 2^jx (x - mu), jx putting
+// max |x_i - mu_i| * 2^jx in [2^8, 2^9) (exact power-of-two scaling): the
+// reduced-precision arithmetic then runs in the same range whatever the
+// data's magnitude, and proxies are 2^(2 jx) (L2) / 2^jx (L1) times the
+// unscaled ones (the merge unscales).  Values far below the largest may
+// still leave the normal range of fp32 / fp16: the merge's absolute error
+// terms cover that.
+
+// One wave per train row: fp64 2^jx (x - mu) -> fp32 (zero padded to DP),
 // fl32(||x32||^2) seeds for the L2 accumulator, 0 seeds for L1, +inf on pad
-// rows; running max of ||x - mu||_2^2, ||x - mu||_1 and max |x_i - mu_i|
-// (fp64, non-negative -> ordered as u64 bits).
+// rows; running max of the unscaled ||x - mu||_2^2 and ||x - mu||_1 (fp64,
+// non-negative -> ordered as u64 bits).
 __global__ void __launch_bounds__(256)
 prep_train_kernel(const double* __restrict__ X64, const double* __restrict__ mu, int64_t n, int d,
-                  int DP, int64_t n_pad, float* __restrict__ X32, float* __restrict__ xl2,
+                  int DP, int64_t n_pad, int jx, float* __restrict__ X32, float* __restrict__ xl2,
                   float* __restrict__ xl1, unsigned long long* __restrict__ stats) {
   const int RSF = DP + 4;  // padded row: [x32 (DP) | ||x32||^2, l1 seed, 0, 0]
   const int lane = threadIdx.x & 63;
   const int64_t wstride = (int64_t)gridDim.x * 4;
-  double m2 = 0.0, m1 = 0.0, mabs = 0.0;
+  double m2 = 0.0, m1 = 0.0;
   for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n_pad; row += wstride) {
     double s32 = 0.0, s64 = 0.0, a64 = 0.0;
     for (int c = lane; c < DP; c += 64) {
       float v = 0.0f;
       if (row < n && c < d) {
         const double x = X64[row * d + c] - mu[c];
-        v = (float)x;
+        v = (float)__builtin_ldexp(x, jx);
         s64 += x * x;
         a64 += __builtin_fabs(x);
-        mabs = fmax(mabs, __builtin_fabs(x));
       }
       X32[row * RSF + c] = v;
       s32 += (double)v * (double)v;
@@ -92,44 +120,69 @@ prep_train_kernel(const double* __restrict__ X64, const double* __restrict__ mu,
     m2 = fmax(m2, s64);
     m1 = fmax(m1, a64);
   }
-  mabs = wave_max_d(mabs);
   if (lane == 0) {
     // small relative slack covers the order of the fp64 sums above
     atomicMax(&stats[0], (unsigned long long)__double_as_longlong(m2 * (1.0 + 1e-12)));
     atomicMax(&stats[1], (unsigned long long)__double_as_longlong(m1 * (1.0 + 1e-12)));
-    atomicMax(&stats[2], (unsigned long long)__double_as_longlong(mabs));
   }
 }
 
 void launch_prep_train(const double* X64, const double* mu, int64_t n, int d, int DP,
-                       int64_t n_pad, float* X32, float* xl2, float* xl1,
+                       int64_t n_pad, int jx, float* X32, float* xl2, float* xl1,
                        unsigned long long* stats, hipStream_t s) {
   int64_t blocks = (n_pad + 3) / 4;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(prep_train_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X64, mu, n, d,
-                     DP, n_pad, X32, xl2, xl1, stats);
+                     DP, n_pad, jx, X32, xl2, xl1, stats);
 }
 
+// Per query: valid[row] = 1 when every |scale * 2^jx (q_i - mu_i)| stays below
+// `limit` (the operand format's safe range), else 0: the query's proxies are
+// then void and the merge sends it to the exact rescan (pad rows: 1).
+__global__ void __launch_bounds__(256)
+query_check_kernel(const double* __restrict__ Q64, const double* __restrict__ mu, int64_t m, int d,
+                   int64_t m_pad, double scale, int jx, double limit, float* __restrict__ valid) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wstride = (int64_t)gridDim.x * 4;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < m_pad; row += wstride) {
+    bool ok = true;
+    if (row < m)
+      for (int c = lane; c < d; c += 64)
+        ok = ok && __builtin_fabs(__builtin_ldexp(scale * (Q64[row * d + c] - mu[c]), jx)) < limit;
+    ok = __ballot(!ok) == 0;
+    if (lane == 0) valid[row] = ok ? 1.0f : 0.0f;
+  }
+}
+
+void launch_query_check(const double* Q64, const double* mu, int64_t m, int d, int64_t m_pad,
+                        double scale, int jx, double limit, float* valid, hipStream_t s) {
+  int64_t blocks = (m_pad + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(query_check_kernel, dim3((unsigned)blocks), dim3(256), 0, s, Q64, mu, m, d,
+                     m_pad, scale, jx, limit, valid);
+}
+
+// scale * 2^jx (q - mu) -> fp32 rows of DP (zero padded)
 __global__ void __launch_bounds__(256)
 prep_queries_kernel(const double* __restrict__ Q64, const double* __restrict__ mu, int64_t m,
-                    int d, int DP, int64_t m_pad, float scale, float* __restrict__ Q32) {
+                    int d, int DP, int64_t m_pad, double scale, int jx, float* __restrict__ Q32) {
   const int64_t total = m_pad * DP;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * 256) {
     const int64_t row = e / DP;
     const int c = (int)(e - row * DP);
     float v = 0.0f;
-    if (row < m && c < d) v = scale * (float)(Q64[row * d + c] - mu[c]);  // x(-2) is exact
+    if (row < m && c < d) v = (float)__builtin_ldexp(scale * (Q64[row * d + c] - mu[c]), jx);
     Q32[e] = v;
   }
 }
 
 void launch_prep_queries(const double* Q64, const double* mu, int64_t m, int d, int DP,
-                         int64_t m_pad, float scale, float* Q32, hipStream_t s) {
+                         int64_t m_pad, double scale, int jx, float* Q32, hipStream_t s) {
   int64_t blocks = (m_pad * DP + 255) / 256;
   if (blocks > 16384) blocks = 16384;
   hipLaunchKernelGGL(prep_queries_kernel, dim3((unsigned)blocks), dim3(256), 0, s, Q64, mu, m, d,
-                     DP, m_pad, scale, Q32);
+                     DP, m_pad, scale, jx, Q32);
 }
 
 __global__ void __launch_bounds__(256)
@@ -164,17 +217,15 @@ void launch_prep_split(const double* X64, const double* mu, int64_t n, int d, in
 
 // ---------------------------------- fp16 images (kernel metric 4, d <= 256)
 // Train rows: [fp16(2^jx (x - mu)) (DP halves) | seeds (4 floats)], the seed
-// 2^(2 jx) fl32(||x32||^2) (exact power-of-two scaling; +inf on pad rows).
-// jx puts max |x - mu| * 2^jx in [2^8, 2^9): no fp16 overflow, and values
-// below the fp16 normal range are at most 2^-22 of the largest (their
-// absolute error is in the bound).
+// fl32(||x32||^2) of the (equally scaled) fp32 copy; +inf on pad rows.  With
+// max |x - mu| * 2^jx < 2^9 nothing overflows fp16; values below its normal
+// range carry an absolute error the merge's bound includes.
 __global__ void __launch_bounds__(256)
 prep_half_train_kernel(const double* __restrict__ X64, const double* __restrict__ mu, int64_t n,
                        int d, int DP, int64_t n_pad, int jx, unsigned short* __restrict__ out,
                        const float* __restrict__ xl2) {
   const int row_shorts = DP + 8;
   const int64_t total = n_pad * DP;
-  const float s2 = __builtin_ldexpf(1.0f, 2 * jx);
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * 256) {
     const int64_t row = e / DP;
@@ -186,7 +237,7 @@ prep_half_train_kernel(const double* __restrict__ X64, const double* __restrict_
       // slot 0: the row's own seed; the pad of row 4g also carries the seeds
       // of rows 4g+1 .. 4g+3 (one float4 read per 4 rows; n_pad % 4 == 0)
       float* seed = (float*)(out + row * row_shorts + DP);
-      seed[c] = (c == 0 || (row & 3) == 0) ? xl2[row + c] * s2 : 0.0f;
+      seed[c] = (c == 0 || (row & 3) == 0) ? xl2[row + c] : 0.0f;
     }
   }
 }
@@ -200,39 +251,32 @@ void launch_prep_half_train(const double* X64, const double* mu, int64_t n, int 
                      DP, n_pad, jx, out, xl2);
 }
 
-// Query rows: fp16(-2 * 2^jx (q - mu)) (DP halves): the train set's scale,
-// so the kernel's proxies are 2^(2 jx) (||x'||^2 - 2 q'.x') with no per-query
-// rescaling.  fac[row] = 1, or 0 when 2 |q_i - mu_i| 2^jx would leave the
-// fp16 range (a query ~64x farther out than any train row): its proxies are
-// not used and the merge sends it to the exact rescan.
+// Query rows: fp16(-2 * 2^jx (q - mu)) (DP halves), the train set's scale;
+// a query launch_query_check marked invalid (valid[row] = 0: beyond the
+// fp16 range) gets zero operands, i.e. finite proxies the merge ignores.
 __global__ void __launch_bounds__(256)
 prep_half_queries_kernel(const double* __restrict__ Q64, const double* __restrict__ mu, int64_t m,
                          int d, int DP, int64_t m_pad, int jx, unsigned short* __restrict__ out,
-                         float* __restrict__ fac) {
-  const int lane = threadIdx.x & 63;
-  const int64_t wstride = (int64_t)gridDim.x * 4;
-  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < m_pad; row += wstride) {
-    double amax = 0.0;
-    if (row < m)
-      for (int c = lane; c < d; c += 64) amax = fmax(amax, __builtin_fabs(Q64[row * d + c] - mu[c]));
-    // out of range (or NaN): zero operands (finite proxies) and fac = 0
-    const bool ok = __builtin_ldexp(2.0 * wave_max_d(amax), jx) < 65000.0;
-    for (int c = lane; c < DP; c += 64) {
-      _Float16 h = (_Float16)0.0f;
-      if (ok && row < m && c < d) h = (_Float16)__builtin_ldexp(-2.0 * (Q64[row * d + c] - mu[c]), jx);
-      out[row * DP + c] = __builtin_bit_cast(unsigned short, h);
-    }
-    if (lane == 0) fac[row] = ok ? 1.0f : 0.0f;
+                         const float* __restrict__ valid) {
+  const int64_t total = m_pad * DP;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * 256) {
+    const int64_t row = e / DP;
+    const int c = (int)(e - row * DP);
+    _Float16 h = (_Float16)0.0f;
+    if (row < m && c < d && valid[row] > 0.0f)
+      h = (_Float16)__builtin_ldexp(-2.0 * (Q64[row * d + c] - mu[c]), jx);
+    out[e] = __builtin_bit_cast(unsigned short, h);
   }
 }
 
 void launch_prep_half_queries(const double* Q64, const double* mu, int64_t m, int d, int DP,
-                              int64_t m_pad, int jx, unsigned short* out, float* fac,
+                              int64_t m_pad, int jx, unsigned short* out, const float* valid,
                               hipStream_t s) {
-  int64_t blocks = (m_pad + 3) / 4;
-  if (blocks > 8192) blocks = 8192;
+  int64_t blocks = (m_pad * DP + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
   hipLaunchKernelGGL(prep_half_queries_kernel, dim3((unsigned)blocks), dim3(256), 0, s, Q64, mu, m,
-                     d, DP, m_pad, jx, out, fac);
+                     d, DP, m_pad, jx, out, valid);
 }
 
 __global__ void fill_i32_kernel(int32_t* p, int64_t n, int32_t v) {

@@ -165,20 +165,16 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
     qa = wave_sum_d(qa) * (1.0 + 1e-12);
     double E =
         (METRIC == 0 ? f_err * (t.x2max + 2.1 * __builtin_sqrt(qa) * __builtin_sqrt(t.x2max))
-                     : f_err * (qa + t.x1max)) + 1e-30;
-    // scaled proxies (kernel metric 4): proxy = sx * sq * (unscaled), both
-    // powers of two; operand values below the fp16 normal range may lose up
-    // to 2^-14 (scaled units) each: absolute terms of the bound
-    double pinv = 1.0;
-    if (ps.qfac) {
-      // qfac[q] = 0: the query left the fp16 range, its proxies are void
-      const double f = ps.qfac[q] > 0.0f ? (double)ps.qfac[q] : 1.0;
-      const double sq = ps.sx * f;
-      pinv = 1.0 / (ps.sx * sq);
-      q1 = wave_sum_d(q1) * (1.0 + 1e-12);
-      E += 0x1p-14 * 1.001 * (2.0 * q1 / ps.sx + t.x1max / sq) + t.DP * 0x1p-28 * pinv;
-      if (!(ps.qfac[q] > 0.0f)) E = KNN_INF_D;
-    }
+                     : f_err * (qa + t.x1max)) + 1e-300;
+    // proxies are in scaled units (operands 2^jx (x - mu), knn_prep.hip):
+    // unscale exactly; operand values outside the format's normal range add
+    // absolute error terms (ue per element, up per product, scaled units)
+    const double pinv = __builtin_ldexp(1.0, METRIC == 0 ? -2 * t.jx : -t.jx);
+    const double sinv = __builtin_ldexp(1.0, -t.jx);
+    q1 = wave_sum_d(q1) * (1.0 + 1e-12);
+    if (METRIC == 0) E += ps.ue * 1.001 * (2.0 * q1 + t.x1max) * sinv + t.DP * ps.up * pinv;
+    else E += 2.0 * ps.ue * 1.001 * t.DP * sinv;
+    const bool void_q = ps.valid && !(ps.valid[q] > 0.0f);
     // union in registers; min over full lists of their R-th (worst kept) entry
     const float* lv = cv + q * U;
     const int* li = ci + q * U;
@@ -266,7 +262,7 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
       tq = key2f(max(max(g[0], g[1]), max(g[2], g[3])));
     }
     if (lane == 0) {
-      s_cn = cn;
+      s_cn = void_q ? Cmax + 1 : cn;  // void proxies: exact rescan below
       s_lb = (double)fminf(fminf(lbx, mlr), tq) * pinv;
       s_qa = qa;
       s_e = E;
@@ -274,7 +270,7 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
   }
   __syncthreads();
   const int cn = s_cn;
-  if (cn > Cmax) {  // re-rank set beyond this launch's capacity: exact rescan
+  if (cn > Cmax) {  // void proxies (the window overflow is handled above): exact rescan
     if (tid == 0) {
       const int f = atomicAdd(rescan_cnt, 1);
       rescan_q[f] = (int)q;
@@ -388,27 +384,33 @@ rescan_prep_kernel(TrainDev t, const double* __restrict__ Q64, const int* __rest
                    float* __restrict__ thr) {
   const int s = blockIdx.x, lane = threadIdx.x, d = t.d, DP = t.DP;
   const double* qr = Q64 + (int64_t)rescan_q[f0 + s] * d;
-  double qa = 0.0;
+  double qa = 0.0, q1 = 0.0;
   for (int i = lane; i < DP; i += 64) {
     float v = 0.0f;
     if (i < d) {
       const double x = qr[i] - t.mu[i];
       qa += METRIC == 0 ? x * x : __builtin_fabs(x);
-      v = (float)x * (METRIC == 0 ? -2.0f : 1.0f);
+      q1 += __builtin_fabs(x);
+      v = (float)__builtin_ldexp(x * (METRIC == 0 ? -2.0 : 1.0), t.jx);  // X32's scale
     }
     qf[(int64_t)s * DP + i] = v;
   }
   qa = wave_sum_d(qa) * (1.0 + 1e-12);
+  q1 = wave_sum_d(q1) * (1.0 + 1e-12);
   if (lane == 0) {
     const double tq = tau[f0 + s];
+    const double sinv = __builtin_ldexp(1.0, -t.jx);
     double T;
+    // unscaled threshold (+ the fp32 absolute terms of the merge), then
+    // scaled to the proxies' units
     if (METRIC == 0) {
-      const double E =
-          f_err * (t.x2max + 2.1 * __builtin_sqrt(qa) * __builtin_sqrt(t.x2max)) + 1e-30;
-      T = tq * tq * (1.0 + 1e-12) - qa * (1.0 - 2e-12) + E;
+      const double E = f_err * (t.x2max + 2.1 * __builtin_sqrt(qa) * __builtin_sqrt(t.x2max)) +
+                       0x1p-125 * 1.001 * (2.0 * q1 + t.x1max) * sinv +
+                       DP * 0x1p-124 * sinv * sinv + 1e-300;
+      T = __builtin_ldexp(tq * tq * (1.0 + 1e-12) - qa * (1.0 - 2e-12) + E, 2 * t.jx);
     } else {
-      const double E = f_err * (qa + t.x1max) + 1e-30;
-      T = tq * (1.0 + 1e-12) + E;
+      const double E = f_err * (qa + t.x1max) + 2.0 * 0x1p-125 * 1.001 * DP * sinv + 1e-300;
+      T = __builtin_ldexp(tq * (1.0 + 1e-12) + E, t.jx);
     }
     // round T up to a float (the order-preserving key's successor is the next float up)
     float tf = (float)T;

@@ -166,8 +166,10 @@ def test_scale_extremes(clf, knn):
     te[:8] *= 1e4                    # ~1e4 x the train spread
     te[8:12] = 1e12
     run_case(clf, knn, tr, lab, te, 7, 0, 4)
-    run_case(clf, knn, tr * 1e-12, lab, te * 1e-12, 7, 0, 4)
-    run_case(clf, knn, tr * 1e12, lab, te * 1e12, 7, 0, 4)
+    run_case(clf, knn, tr * 1e-30, lab, te * 1e-30, 7, 0, 4)
+    run_case(clf, knn, tr * 1e25, lab, te * 1e25, 7, 0, 4)
+    run_case(clf, knn, tr * 1e-30, lab, te * 1e-30, 7, 1, 4)
+    run_case(clf, knn, tr * 1e25, lab, te * 1e25, 7, 1, 4)
 
 
 def test_integer_ties(clf, knn):
