@@ -37,6 +37,7 @@ def main():
     ref = None
     res = {v: [] for v in a.variants}
     tot = {}
+    ph = {}
     info = {}
     prec = {"auto": knn.PRECISION_AUTO, "fp32": knn.PRECISION_FP32, "bf16x3": knn.PRECISION_BF16X3,
             "m16": knn.PRECISION_BF16X3, "fp16": knn.PRECISION_FP16}
@@ -61,12 +62,15 @@ def main():
                 continue
             res[v].append(clf.last_phase_ms(knn.PHASE_CANDIDATE))
             tot.setdefault(v, []).append(sum(clf.last_phase_ms(p) for p in range(4)))
+            ph.setdefault(v, []).append([clf.last_phase_ms(p) for p in range(4)])
     flops = 2.0 * a.n * a.d * a.m
     for v in a.variants:
         ms = np.median(res[v])
         print("%-14s cand %8.3f ms (min %8.3f)  %7.1f TF/s  all phases %8.3f ms  %s rescans=%d "
               "same_labels=%s" % (v, ms, np.min(res[v]), flops / ms / 1e9, np.median(tot[v]),
                                   info[v][0], info[v][1], info[v][2]))
+        print("%-14s phases ms: prep %.3f cand %.3f rerank %.3f rescan %.3f" %
+              ((v,) + tuple(np.median(np.array(ph[v]), axis=0))))
 
 
 if __name__ == "__main__":
