@@ -141,7 +141,7 @@ static int build_train(knn_ctx* ctx, const double* dX, const int32_t* dlab, int6
   if ((rc = ctx->X32.ensure((size_t)n_pad * (DP + 4) * sizeof(float) + 1024))) return rc;
   if ((rc = ctx->xl2.ensure((size_t)n_pad * sizeof(float)))) return rc;
   if ((rc = ctx->xl1.ensure((size_t)n_pad * sizeof(float)))) return rc;
-  if ((rc = ctx->stats.ensure(3 * sizeof(unsigned long long)))) return rc;
+  if ((rc = ctx->stats.ensure(4 * sizeof(unsigned long long)))) return rc;
   if ((rc = ctx->mu.ensure((size_t)d * sizeof(double)))) return rc;
   if ((rc = ctx->mu_part.ensure((size_t)col_mean_blocks(n) * d * sizeof(double)))) return rc;
   launch_col_mean(dX, n, d, (double*)ctx->mu_part.p, (double*)ctx->mu.p, ctx->stream);
@@ -161,6 +161,11 @@ static int build_train(knn_ctx* ctx, const double* dX, const int32_t* dlab, int6
   if (!(ctx->xamax < std::ldexp(1.0, 400)))
     return knn_fail(KNN_ERR_ARG, "train values out of range (|x - mean| must be < 2^400 and finite)");
   const int jx = std::min(9 - e, 450);
+  // centre on the 2^-(jx+2) grid: data on any coarser grid (bytes scaled by a
+  // power of two, integers, ...) is then exact in the fp16 operands, whose
+  // measured representation error vanishes from the bound;
+  // the shift is <= 2^-11 of max |x - mu|, immaterial for the centring
+  launch_round_mu((double*)ctx->mu.p, d, jx + 2, ctx->stream);
   launch_prep_train(dX, (const double*)ctx->mu.p, n, d, DP, n_pad, jx, (float*)ctx->X32.p,
                     (float*)ctx->xl2.p, (float*)ctx->xl1.p, st_d, ctx->stream);
   HIP_TRY(hipGetLastError());
@@ -228,9 +233,17 @@ static int ensure_fp16(knn_ctx* ctx, hipStream_t s) {
   if (ctx->DPh == DPh) return KNN_OK;
   int rc;
   if ((rc = ctx->XH.ensure((size_t)t.n_pad * (DPh / 2 + 4) * sizeof(float) + 1024))) return rc;
+  unsigned long long* st_d = (unsigned long long*)ctx->stats.p + 3;
+  HIP_TRY(hipMemsetAsync(st_d, 0, 8, s));
   launch_prep_half_train(t.X64, t.mu, t.n, t.d, DPh, t.n_pad, t.jx,
-                         (unsigned short*)ctx->XH.p, t.xinit_l2, s);
+                         (unsigned short*)ctx->XH.p, t.xinit_l2, st_d, s);
   HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(ctx->h_stats + 3, st_d, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  double dx2;
+  memcpy(&dx2, &ctx->h_stats[3], 8);
+  // + the fp64 rounding of x - mu itself (<= 2^-53 relative per element)
+  ctx->train.dxmax = std::sqrt(dx2) * (1.0 + 1e-12) + 0x1p-50 * std::sqrt(t.x2max);
   ctx->DPh = DPh;
   return KNN_OK;
 }
@@ -346,16 +359,17 @@ static void choose_geometry(knn_ctx* ctx, int metric, int DP, int nw, int n_qt, 
 //   kmetric 2 (bf16x3): products exact, accumulation of 3DP+1 terms bounded
 //     with u' = 2^-23 (covers truncating adders), + 2^-15 for the hi/lo
 //     representation error (~3 * 2^-18 relative per product, x2 for -2q).
-//   kmetric 4 (fp16): both operands rounded to fp16 (u_h = 2^-11, x(1 +
-//     2^-12) for a double rounding via fp32) -> 2u_h + u_h^2 per product;
-//     products exact in fp32, DP+1 accumulated terms with u' = 2^-23.  The
-//     fp16 subnormal-range terms are absolute and added by the merge.
+//   kmetric 4 (fp16): products of the fp16 operands exact in fp32, DP+1
+//     accumulated terms with u' = 2^-23.  The operands' representation
+//     error is measured (train: TrainDev::dxmax, queries: by the merge from
+//     the operands themselves) and added by the merge with the seed's own
+//     rounding and the fp16 subnormal-range terms.
 static double err_factor(int kmetric, int DP) {
   const double u = std::ldexp(1.0, -24);
   if (kmetric == 4) {
-    const double u2 = std::ldexp(1.0, -23), uh = std::ldexp(1.0, -11) * (1.0 + std::ldexp(1.0, -12));
+    const double u2 = std::ldexp(1.0, -23);
     const int n = DP + 1;
-    return (n * u2 / (1.0 - n * u2) + 2.0 * uh + uh * uh) * 1.02;
+    return n * u2 / (1.0 - n * u2) * 1.02;
   }
   if (kmetric == 2 || kmetric == 3) {  // bf16x3 on either MFMA shape
     const double u2 = std::ldexp(1.0, -23);
@@ -477,7 +491,8 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   HIP_TRY(hipMemsetAsync(ctx->rescan_cnt.p, 0, sizeof(int), s));
   launch_merge_rerank(metric, (const float*)ctx->cand_v.p, (const int*)ctx->cand_i.p, NL, R, t, dQ,
                       m, W, C, err_factor(kmetric, DP),
-                      kmetric == 4 ? ProxyScale{qvalid, 0x1p-14, 0x1p-28}
+                      kmetric == 4 ? ProxyScale{qvalid, 0x1p-14, 0x1p-28,
+                                                (const unsigned short*)ctx->Q32.p, DP}
                                    : ProxyScale{qvalid, 0x1p-125, 0x1p-124},
                       cl.gthr, sink, (int*)ctx->rescan_q.p,
                       (double*)ctx->rescan_tau.p, (int*)ctx->rescan_cnt.p, s);

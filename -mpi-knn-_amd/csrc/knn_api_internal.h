@@ -18,7 +18,7 @@ struct knn_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   int* h_count = nullptr;  // pinned
-  unsigned long long h_stats[3] = {0, 0, 0};  // train statistics read back at build
+  unsigned long long h_stats[4] = {0, 0, 0, 0};  // train statistics read back at build
   bool trained = false;
   int class_cnt = 0;
   int64_t idx_off = 0;

@@ -42,6 +42,7 @@ struct TrainDev {
   int64_t n, n_pad;
   int d, DP;
   double x2max, x1max;   // max ||x - mu||_2^2, max ||x - mu||_1 over the train rows
+  double dxmax;          // max ||fp16 row / 2^jx - (x - mu)||_2 of the fp16 copy (when built)
   int jx;                // candidate operands are 2^jx (x - mu) (knn_prep.hip)
 };
 
@@ -104,9 +105,14 @@ void launch_cand(const CandLaunch& c, hipStream_t s);
 // query's operands left the format's range, its proxies are void (exact
 // rescan).  ue / up: absolute error per operand element / per product in
 // scaled units, for values outside the format's normal range.
+// qh (fp16 pass, else null): the query operands actually used, rows of
+// qh_stride halves of -2 * 2^jx (q - mu); the merge measures their
+// representation error instead of assuming the format's worst case.
 struct ProxyScale {
   const float* valid;
   double ue, up;
+  const unsigned short* qh = nullptr;
+  int qh_stride = 0;
 };
 void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int R,
                          const TrainDev& t, const double* Q64, int64_t m, int W, int C,
@@ -137,9 +143,14 @@ void launch_fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t s);
 // fp16 images of kernel metric 4 (knn_prep.hip): train rows of DP halves + 4
 // seed floats, scaled by 2^jx; query rows of DP halves of -2 * 2^jx (q - mu)
 // (zero for queries launch_query_check marked invalid)
+// dx2max: running max (u64 bits of a non-negative double) of the rows'
+// ||fp16 / 2^jx - (x - mu)||_2^2 (measured representation error)
 void launch_prep_half_train(const double* X64, const double* mu, int64_t n, int d, int DP,
                             int64_t n_pad, int jx, unsigned short* out, const float* xl2,
-                            hipStream_t s);
+                            unsigned long long* dx2max, hipStream_t s);
+// mu <- mu rounded to a multiple of 2^-g (the centre then sits on any data
+// grid at least as coarse, so such data is exact in the fp16 operands)
+void launch_round_mu(double* mu, int d, int g, hipStream_t s);
 void launch_prep_half_queries(const double* Q64, const double* mu, int64_t m, int d, int DP,
                               int64_t m_pad, int jx, unsigned short* out, const float* valid,
                               hipStream_t s);

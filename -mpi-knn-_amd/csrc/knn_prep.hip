@@ -223,32 +223,55 @@ void launch_prep_split(const double* X64, const double* mu, int64_t n, int d, in
 __global__ void __launch_bounds__(256)
 prep_half_train_kernel(const double* __restrict__ X64, const double* __restrict__ mu, int64_t n,
                        int d, int DP, int64_t n_pad, int jx, unsigned short* __restrict__ out,
-                       const float* __restrict__ xl2) {
+                       const float* __restrict__ xl2, unsigned long long* __restrict__ dx2max) {
+  // one wave per row; the row's representation error ||h / 2^jx - (x - mu)||^2
+  // is measured in fp64 (h / 2^jx - x is exact: Sterbenz, or h = 0)
   const int row_shorts = DP + 8;
-  const int64_t total = n_pad * DP;
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * 256) {
-    const int64_t row = e / DP;
-    const int c = (int)(e - row * DP);
-    _Float16 h = (_Float16)0.0f;
-    if (row < n && c < d) h = (_Float16)__builtin_ldexp(X64[row * d + c] - mu[c], jx);
-    out[row * row_shorts + c] = __builtin_bit_cast(unsigned short, h);
-    if (c < 4) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wstride = (int64_t)gridDim.x * 4;
+  const double sinv = __builtin_ldexp(1.0, -jx);
+  double m = 0.0;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n_pad; row += wstride) {
+    double e2 = 0.0;
+    for (int c = lane; c < DP; c += 64) {
+      _Float16 h = (_Float16)0.0f;
+      if (row < n && c < d) {
+        const double x = X64[row * d + c] - mu[c];
+        h = (_Float16)__builtin_ldexp(x, jx);
+        const double e = (double)h * sinv - x;
+        e2 += e * e;
+      }
+      out[row * row_shorts + c] = __builtin_bit_cast(unsigned short, h);
+    }
+    if (lane < 4) {
       // slot 0: the row's own seed; the pad of row 4g also carries the seeds
       // of rows 4g+1 .. 4g+3 (one float4 read per 4 rows; n_pad % 4 == 0)
       float* seed = (float*)(out + row * row_shorts + DP);
-      seed[c] = (c == 0 || (row & 3) == 0) ? xl2[row + c] : 0.0f;
+      seed[lane] = (lane == 0 || (row & 3) == 0) ? xl2[row + lane] : 0.0f;
     }
+    m = fmax(m, wave_sum_d(e2));
   }
+  if (lane == 0) atomicMax(dx2max, (unsigned long long)__double_as_longlong(m * (1.0 + 1e-12)));
 }
 
 void launch_prep_half_train(const double* X64, const double* mu, int64_t n, int d, int DP,
                             int64_t n_pad, int jx, unsigned short* out, const float* xl2,
-                            hipStream_t s) {
-  int64_t blocks = (n_pad * DP + 255) / 256;
-  if (blocks > 16384) blocks = 16384;
+                            unsigned long long* dx2max, hipStream_t s) {
+  int64_t blocks = (n_pad + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(prep_half_train_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X64, mu, n, d,
-                     DP, n_pad, jx, out, xl2);
+                     DP, n_pad, jx, out, xl2, dx2max);
+}
+
+__global__ void round_mu_kernel(double* mu, int d, int g) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= d) return;
+  // |mu| 2^g >= 2^52: already a multiple of 2^-g (and no overflow)
+  const double y = __builtin_ldexp(mu[c], g);
+  if (__builtin_fabs(y) < 0x1p52) mu[c] = __builtin_ldexp(__builtin_rint(y), -g);
+}
+void launch_round_mu(double* mu, int d, int g, hipStream_t s) {
+  hipLaunchKernelGGL(round_mu_kernel, dim3((d + 255) / 256), dim3(256), 0, s, mu, d, g);
 }
 
 // Query rows: fp16(-2 * 2^jx (q - mu)) (DP halves), the train set's scale;

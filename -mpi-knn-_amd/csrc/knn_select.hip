@@ -166,6 +166,25 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
     double E =
         (METRIC == 0 ? f_err * (t.x2max + 2.1 * __builtin_sqrt(qa) * __builtin_sqrt(t.x2max))
                      : f_err * (qa + t.x1max)) + 1e-300;
+    if (METRIC == 0 && ps.qh) {
+      // fp16 operands: f_err covers the accumulation only; add the measured
+      // representation error (q' = q - mu, x' = x - mu, dq / dx the operand
+      // errors in unscaled units):  2 |q'.dx + dq.x' + dq.dx| <=
+      // 2 (|q'| dxmax + |dq| (xmax + dxmax)), plus the fl32 seed's own
+      // rounding (3u ||x'||^2, u = 2^-24)
+      const unsigned short* qh = ps.qh + q * (int64_t)ps.qh_stride;
+      const double qs = -__builtin_ldexp(0.5, -t.jx);  // operand = -2 * 2^jx q'
+      double dq2 = 0.0;
+      for (int c = lane; c < d; c += 64) {
+        const double e = (double)__builtin_bit_cast(_Float16, qh[c]) * qs - (qv[c] - t.mu[c]);
+        dq2 += e * e;
+      }
+      const double qn = __builtin_sqrt(qa), xm = __builtin_sqrt(t.x2max);
+      const double dq = __builtin_sqrt(wave_sum_d(dq2) * (1.0 + 1e-12)) * (1.0 + 1e-12) +
+                        0x1p-50 * qn;
+      E = f_err * (t.x2max + 2.0 * (qn + dq) * (xm + t.dxmax) * 1.001) + 3.01 * 0x1p-24 * t.x2max +
+          2.0 * (qn * t.dxmax + dq * (xm + t.dxmax)) * 1.001 + 1e-300;
+    }
     // proxies are in scaled units (operands 2^jx (x - mu), knn_prep.hip):
     // unscale exactly; operand values outside the format's normal range add
     // absolute error terms (ue per element, up per product, scaled units)
