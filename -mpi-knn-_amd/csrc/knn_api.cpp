@@ -316,11 +316,13 @@ static void choose_geometry(knn_ctx* ctx, int metric, int DP, int nw, int n_qt, 
                             int W, int C, int& S_out, int& R_out) {
   const int S_hi = (int)std::max<int64_t>(1, std::min<int64_t>(64, n_tiles));
   int bestS = 1, bestR = 8;
-  const int lps = metric >= 3 ? 4 : 2;  // lists per query per split
+  const bool quad = metric >= 3 && metric <= 5;  // 16x16 layouts
+  const int lps = quad ? 4 : 2;  // lists per query per split
   for (int R : {4, 8, 16}) {
-    // kernel metric 3 (16x16x32 layout) has R = 4 only; elsewhere R = 4 only on
-    // request (resident kernel; tuning experiments)
-    if (metric >= 3 ? R != 4 : (ctx->tune_R ? R != ctx->tune_R : R == 4)) continue;
+    // kernel metrics 3-5 (16x16x32 layout) have R = 4 only; elsewhere R = 4
+    // only on request (resident kernel; tuning experiments); 6 has no R = 16
+    if (quad ? R != 4 : (ctx->tune_R ? R != ctx->tune_R : R == 4)) continue;
+    if (metric == 6 && R == 16) continue;
     if (R == 4 && (DP > 256 || metric == 1)) continue;
     const int64_t slots = (int64_t)cand_blocks_per_cu(metric, DP, R, nw) * ctx->cu_count;
     const int S_lo = std::min(S_hi, std::max(1, (C + lps * R - 1) / (lps * R)));
@@ -345,7 +347,7 @@ static void choose_geometry(knn_ctx* ctx, int metric, int DP, int nw, int n_qt, 
     // fast rescan absorbs it.  Without a fast rescan (d > kRescanFastMaxDP a
     // rescan is a full exact scan) R = 16 unless the share is at most 1/2.
     const bool fast_rescan = DP <= kRescanFastMaxDP;
-    if (ctx->tune_R || metric >= 3 || (fast_rescan ? W <= 4 * bS : W <= bS)) break;
+    if (ctx->tune_R || quad || (fast_rescan ? W <= 4 * bS : W <= bS)) break;
   }
   S_out = bestS;
   R_out = bestR;
@@ -413,7 +415,18 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   if (DP <= 256 && kmetric != 1) nw = ctx->tune_nw ? ctx->tune_nw : (m >= 4096 ? 8 : 4);
   if (kmetric >= 3) nw = 8;
   if (s3) nw = 8;
-  const int qpb = s3 ? kS3Rows : (DP <= 256 ? 32 * nw : kQPB);
+  // fp16 MFMA shape (tuning key "f16layout": 0 = 16x16x32, 32 queries per
+  // wave (kernel flavour 4); 1 = the same with 64 queries per wave (5); 2 =
+  // 32x32x16 (6); -1 auto): one arithmetic, error bound and proxy scale, so
+  // kmetric stays 4 outside the launch
+  int lmetric = kmetric;
+  if (kmetric == 4) {
+    const int lay = ctx->tune_f16l < 0 ? 0 : ctx->tune_f16l;
+    lmetric = 4 + lay;
+    if (lay > 0 && ctx->tune_nw) nw = ctx->tune_nw;
+  }
+  const bool wide = lmetric == 5;
+  const int qpb = s3 ? kS3Rows : (DP <= 256 ? 32 * nw * (wide ? 2 : 1) : kQPB);
   const int n_qt = (int)((m + qpb - 1) / qpb);
   const int64_t m_pad = (int64_t)n_qt * qpb;
   const int64_t n_pad3 = (t.n + kS3Rows - 1) / kS3Rows * kS3Rows;
@@ -421,9 +434,10 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   int C = (int)std::min<int64_t>(t.n, std::max(2 * W, W + 16));
   C = std::min(C, kMaxUnion);
   int S = 1, R = 8;
-  choose_geometry(ctx, kmetric, DP, nw, n_qt, n_tiles, W, C, S, R);
-  if (kmetric >= 3) R = 4;
-  const int NL = (kmetric >= 3 ? 4 : 2) * S;
+  choose_geometry(ctx, lmetric, DP, nw, n_qt, n_tiles, W, C, S, R);
+  const bool quad_lists = lmetric >= 3 && lmetric <= 5;  // 16x16 layouts: 4 lists per split
+  if (quad_lists) R = 4;
+  const int NL = (quad_lists ? 4 : 2) * S;
   C = std::min(C, NL * R);
   if ((rc = ctx->Q32.ensure((size_t)m_pad * DP * sizeof(float)))) return rc;
   if ((rc = ctx->qvalid.ensure((size_t)m_pad * sizeof(float)))) return rc;
@@ -465,7 +479,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
     launch_prep_queries(dQ, t.mu, m, t.d, DP, m_pad, qscale, t.jx, (float*)ctx->Q32.p, s);
   if (tm) HIP_TRY(hipEventRecord(ctx->ev[1], s));
   CandLaunch cl{};
-  cl.metric = kmetric;
+  cl.metric = lmetric;
   cl.DP = DP;
   cl.R = R;
   cl.S = S;
@@ -792,6 +806,9 @@ int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value) {
   if (!strcmp(key, "fp16")) {
     if (value < -1 || value > 1) return knn_fail(KNN_ERR_ARG, "fp16 must be -1, 0 or 1");
     ctx->tune_fp16 = (int)value;
+  } else if (!strcmp(key, "f16layout")) {
+    if (value < -1 || value > 2) return knn_fail(KNN_ERR_ARG, "f16layout must be -1 .. 2");
+    ctx->tune_f16l = (int)value;
   } else if (!strcmp(key, "mfma16")) {
     if (value < -1 || value > 1) return knn_fail(KNN_ERR_ARG, "mfma16 must be -1, 0 or 1");
     ctx->tune_m16 = (int)value;

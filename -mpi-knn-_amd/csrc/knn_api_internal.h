@@ -35,6 +35,7 @@ struct knn_ctx {
   int tune_ablate = 0;         // timing-only kernel ablations
   int tune_nw = 0;             // resident kernel waves per workgroup (0 = auto)
   int tune_fp16 = -1;          // fp16 candidate pass: -1 auto, 0 off, 1 on
+  int tune_f16l = -1;          // fp16 MFMA layout: -1 auto, 0 16x16, 1 16x16 wide, 2 32x32
   int tune_m16 = -1;           // bf16x3 on the 16x16x32 MFMA layout: -1 auto, 0 off, 1 on
   int last_nw = 0;
   int last_kmetric = -1; // candidate kernel metric of the last search (knn_kernels.h)

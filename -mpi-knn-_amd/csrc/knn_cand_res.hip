@@ -25,6 +25,16 @@ static_assert(KNN_RES_TPB * knnk::kTR == knnk::kResTileRows || KNN_RES_TPB != 2,
 #ifndef KNN_M4_SEED4
 #define KNN_M4_SEED4 1
 #endif
+// METRIC 5 = the fp16 kernel with 64 queries per wave (4 query blocks of 16):
+// each A fragment read from LDS feeds 4 MFMAs instead of 2, halving the LDS
+// read traffic per MFMA (the 32-query kernel moves 128 B/clk/CU of A
+// fragments at full MFMA rate -- the whole LDS bandwidth)
+#ifndef KNN_M5_TPB
+#define KNN_M5_TPB 4
+#endif
+#ifndef KNN_M5_WPE
+#define KNN_M5_WPE 2
+#endif
 
 namespace knnk {
 
@@ -44,7 +54,9 @@ __device__ __forceinline__ void wait_barrier_x(int extra) {
 constexpr int kPubEvery = 8;  // tiles between global-threshold exchanges
 
 template <int METRIC>
-constexpr int res_tpb() { return METRIC == 4 ? KNN_M4_TPB : KNN_RES_TPB; }
+constexpr int res_tpb() {
+  return METRIC == 5 ? KNN_M5_TPB : (METRIC == 4 || METRIC == 6 ? KNN_M4_TPB : KNN_RES_TPB);
+}
 
 // Train rows in HBM (X32 for fp32/L1, XB for bf16x3) share one padded row
 // format of RSF = DP + 4 floats: [payload (DP floats) | ||x32||^2, l1 seed,
@@ -79,7 +91,8 @@ constexpr int res_tpb() { return METRIC == 4 ? KNN_M4_TPB : KNN_RES_TPB; }
 // (not for R = 16 lists or DP > 160, whose registers do not fit: spills).
 template <int DP, int R, int METRIC, int NW>
 __global__ void __launch_bounds__(NW * 64)
-__attribute__((amdgpu_waves_per_eu((METRIC == 4 ? DP / 2 : DP) <= 160 && R <= 8 ? 4 : 1)))
+__attribute__((amdgpu_waves_per_eu(METRIC == 5 ? KNN_M5_WPE
+                                   : ((METRIC >= 4 ? DP / 2 : DP) <= 160 && R <= 8 ? 4 : 1))))
 cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
             int n_qt, float* __restrict__ out_v, int* __restrict__ out_i, int abl,
             uint32_t* gthr) {
@@ -88,7 +101,10 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   // keeping them in VGPRs (its waits would then also drain the LDS-DMA queue).
   // abl: timing-only ablations (results invalid): bit0 = no staging loads
   // after the first tiles, bit1 = no selection epilogue.  0 in production.
-  constexpr int DPF = METRIC == 4 ? DP / 2 : DP;  // payload floats per row
+  // fp16 operands: METRIC 4/5 on the 16x16x32 layout, 6 on 32x32x16
+  constexpr bool F16 = METRIC >= 4;
+  constexpr bool TEC = (METRIC == 4 || METRIC == 5) && KNN_M4_TE_CACHE;
+  constexpr int DPF = F16 ? DP / 2 : DP;    // payload floats per row
   constexpr int RSF = DPF + 4;              // row stride (floats), HBM and LDS
   constexpr int TPB = res_tpb<METRIC>();    // 32-row sub-tiles per staged tile
   constexpr int TBY = kTR * TPB * RSF * 4;  // tile bytes
@@ -109,9 +125,12 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   // METRIC 3 (bf16x3 on 16x16x32) and 4 (fp16 on 16x16x32): lane l holds
   // queries wv*32 + qb*16 + (l&15), qb = 0, 1, against rows 4*(l>>4) + i of
   // each 16-row block
-  constexpr bool M16 = METRIC == 3 || METRIC == 4;
+  // (METRIC 5: qb = 0..3, 64 queries per wave)
+  constexpr bool M16 = METRIC >= 3 && METRIC <= 5;
+  constexpr int QB = METRIC == 5 ? 4 : 2;  // 16-query blocks per wave (M16)
+  constexpr int QW = M16 ? 16 * QB : 32;   // queries per wave
   const int c16 = lane & 15, g16 = lane >> 4;
-  const int64_t qb0 = (int64_t)qt * (NW * 32) + wv * 32 + c16;  // query of block 0 (+16: block 1)
+  const int64_t qb0 = (int64_t)qt * (NW * QW) + wv * QW + c16;  // query of block 0 (+16 qb: block qb)
 
   // B operand resident in VGPRs for the whole kernel.  METRIC 0: fp32 -2q,
   // float4 c holds dims 8c+4h..8c+4h+3 (four 32x32x2 k-steps).  METRIC 2:
@@ -119,7 +138,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   // qh dims 16t+8h..16t+8h+7, float4 DP/16+t the same dims of ql.
   // METRIC 4: fp16 -2q (the train set's power-of-two scale), float4 qb*(DP/32)+ks
   // = dims 32ks + 8*g16 .. +7 of query block qb.
-  constexpr int NQF = METRIC == 1 ? 1 : (METRIC == 4 ? DP / 16 : DP / 8);
+  constexpr int NQF = METRIC == 1 ? 1 : (METRIC == 6 ? DP / 16 : (F16 ? QB * DP / 32 : DP / 8));
   float4 qf[NQF];
   if constexpr (METRIC != 1) {
     // Loaded with inline asm (loads + their vmcnt(0) in one statement): with
@@ -133,7 +152,10 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int c = c0 + u < NQF ? c0 + u : c0;
-        if constexpr (METRIC == 4) {
+        if constexpr (METRIC == 6) {
+          // 32x32x16 B fragment: query j, dims 16c + 8h .. +7
+          p[u] = Q32 + qg * (DP / 2) + 8 * c + 4 * h;
+        } else if constexpr (F16) {
           const int ks = c % (DP / 32), qb = c / (DP / 32);
           p[u] = Q32 + (qb0 + 16 * qb) * (DP / 2) + 16 * ks + 4 * g16;
         } else if constexpr (M16) {
@@ -162,7 +184,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
     }
   }
 
-  constexpr int NQL = M16 ? 2 : 1;  // queries (lists) per lane
+  constexpr int NQL = M16 ? QB : 1;  // queries (lists) per lane
   float L[NQL][R];
   int I[NQL][R];
   float thr[NQL];
@@ -195,8 +217,10 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   // barrier ever waits on a (contended) atomic.
   // byte offset of gthr[query][0]: the lane's query, or for METRIC 3 query
   // (l & 31) of the wave (lanes 0-15 block 0, 16-31 block 1; 32-63 repeat)
+  // (METRIC 5: lane l <-> query l of the wave)
   const uint32_t goff =
-      M16 ? (uint32_t)(((int64_t)qt * (NW * 32) + wv * 32 + (lane & 31)) * 16) : (uint32_t)(qg * 16);
+      M16 ? (uint32_t)(((int64_t)qt * (NW * QW) + wv * QW + (lane & (QW - 1))) * 16)
+          : (uint32_t)(qg * 16);
   float tq[NQL], te[NQL];
 #pragma unroll
   for (int b = 0; b < NQL; ++b) tq[b] = te[b] = KNN_INF_F;
@@ -228,7 +252,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   int cur = 0, nxt = PD;  // buffer of tile it, buffer that tile it+PD goes to
   for (int it = 0; it < my_nt; ++it) {
     const int t = split + it * S;
-    if constexpr (METRIC == 4 && KNN_M4_TE_CACHE) {
+    if constexpr (TEC) {
 #pragma unroll
       for (int b = 0; b < NQL; ++b) thr[b] = L[b][R - 1];  // for the exchange below
     }
@@ -266,7 +290,12 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
           // (one lane per query, only when it improved), fetch its 4 slots
           uint32_t pk;
           bool pub;
-          if constexpr (M16) {
+          if constexpr (QB == 4) {
+            const float m0 = quad_min(thr[0]), m1 = quad_min(thr[1]);
+            const float m2 = quad_min(thr[2]), m3 = quad_min(thr[3]);
+            pk = f2key(g16 == 0 ? m0 : g16 == 1 ? m1 : g16 == 2 ? m2 : m3);
+            pub = pk < last_pub;
+          } else if constexpr (M16) {
             const float m0 = quad_min(thr[0]), m1 = quad_min(thr[1]);
             pk = f2key(g16 == 0 ? m0 : m1);
             pub = g16 < 2 && pk < last_pub;
@@ -290,7 +319,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
         }
       }
     }
-    if constexpr (METRIC == 4 && KNN_M4_TE_CACHE) {
+    if constexpr (TEC) {
       // the quad's shared filter, refreshed once per staged tile (a stale,
       // larger value only admits more insertions)
 #pragma unroll
@@ -304,24 +333,24 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       // bf16x3 on v_mfma_f32_16x16x32_bf16: 2 row blocks x 2 query blocks of
       // 16; lane l: A = row rb*16 + (l&15), B = query qb*16 + (l&15), k-group
       // l>>4; D = rows rb*16 + 4(l>>4) + i, column l&15
-      f32x4 acc[2][2];
+      f32x4 acc[2][QB];
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb) {
-        if constexpr (METRIC == 4 && KNN_M4_SEED4) {
+        if constexpr (F16 && KNN_M4_SEED4) {
           // the pad of row 4g carries the seeds of rows 4g .. 4g+3
           const float4 sd = *(const float4*)(base + (rb * 16 + 4 * g16) * RSF + SEED);
-          acc[rb][0] = f32x4{sd.x, sd.y, sd.z, sd.w};
-          acc[rb][1] = acc[rb][0];
+#pragma unroll
+          for (int qb = 0; qb < QB; ++qb) acc[rb][qb] = f32x4{sd.x, sd.y, sd.z, sd.w};
         } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float sd = base[(rb * 16 + 4 * g16 + i) * RSF + SEED];
-          acc[rb][0][i] = sd;
-          acc[rb][1][i] = sd;
+#pragma unroll
+          for (int qb = 0; qb < QB; ++qb) acc[rb][qb][i] = sd;
         }
         }
       }
-      if constexpr (METRIC == 4) {
+      if constexpr (F16) {
         // fp16 x fp16 products are exact in fp32: one MFMA per 32 dims
 #pragma unroll
         for (int ks = 0; ks < DP / 32; ++ks) {
@@ -330,7 +359,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
             const float* ar = base + (rb * 16 + c16) * RSF + 16 * ks + 4 * g16;
             const f16x8 a = __builtin_bit_cast(f16x8, *(const float4*)ar);
 #pragma unroll
-            for (int qb = 0; qb < 2; ++qb) {
+            for (int qb = 0; qb < QB; ++qb) {
               const f16x8 b = __builtin_bit_cast(f16x8, qf[qb * (DP / 32) + ks]);
               acc[rb][qb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, acc[rb][qb], 0, 0, 0);
             }
@@ -345,7 +374,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
           const bf16x8 ah = __builtin_bit_cast(bf16x8, *(const float4*)ar);
           const bf16x8 al = __builtin_bit_cast(bf16x8, *(const float4*)(ar + DP / 2));
 #pragma unroll
-          for (int qb = 0; qb < 2; ++qb) {
+          for (int qb = 0; qb < QB; ++qb) {
             const bf16x8 bh = __builtin_bit_cast(bf16x8, qf[(qb * 2 + 0) * (DP / 32) + ks]);
             const bf16x8 bl = __builtin_bit_cast(bf16x8, qf[(qb * 2 + 1) * (DP / 32) + ks]);
             acc[rb][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc[rb][qb], 0, 0, 0);
@@ -357,13 +386,13 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       }
       const int row0 = (t * TPB + sub) * kTR + 4 * g16;
       if (!(abl & 2)) {
-        if constexpr (METRIC == 4 && KNN_M4_TE_CACHE) {
+        if constexpr (TEC) {
 #pragma unroll
-          for (int qb = 0; qb < 2; ++qb)
+          for (int qb = 0; qb < QB; ++qb)
             select_quad_te<R>(acc[0][qb], acc[1][qb], row0, L[qb], I[qb], te[qb]);
         } else {
 #pragma unroll
-          for (int qb = 0; qb < 2; ++qb)
+          for (int qb = 0; qb < QB; ++qb)
             select_quad<R>(acc[0][qb], acc[1][qb], row0, L[qb], I[qb], thr[qb], tq[qb]);
         }
       } else if (acc[0][0][0] == 1234.5f && acc[1][1][3] == 1234.5f) {
@@ -371,9 +400,32 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       }
     } else {
     f32x16 acc;
+    if constexpr (METRIC == 6) {
+      // rows 8q + 4h .. +3: their seeds sit in the pad of row 8q + 4h
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = base[((i & 3) + 8 * (i >> 2) + 4 * h) * RSF + SEED];
-    if constexpr (METRIC == 0) {
+      for (int q = 0; q < 4; ++q) {
+        const float4 sd = *(const float4*)(base + (8 * q + 4 * h) * RSF + SEED);
+        acc[4 * q] = sd.x;
+        acc[4 * q + 1] = sd.y;
+        acc[4 * q + 2] = sd.z;
+        acc[4 * q + 3] = sd.w;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] = base[((i & 3) + 8 * (i >> 2) + 4 * h) * RSF + SEED];
+    }
+    if constexpr (METRIC == 6) {
+      // fp16 on v_mfma_f32_32x32x16_f16: one MFMA per 16 dims (products
+      // exact in fp32); 24 of its 32 issue cycles are free for the epilogue's
+      // VALU work, against 8 of 16 on the 16x16x32 shape
+      const float* arow = base + j * RSF + 4 * h;
+#pragma unroll
+      for (int tt = 0; tt < DP / 16; ++tt) {
+        const f16x8 a = __builtin_bit_cast(f16x8, *(const float4*)(arow + 8 * tt));
+        const f16x8 b = __builtin_bit_cast(f16x8, qf[tt]);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc, 0, 0, 0);
+      }
+    } else if constexpr (METRIC == 0) {
       const float* arow = base + j * RSF + 4 * h;
 #pragma unroll
       for (int c = 0; c < DP / 8; ++c) {
@@ -431,7 +483,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   if constexpr (M16) {
     // 4 lists per query per split (lane groups l>>4): [query][4S][R]
 #pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
+    for (int qb = 0; qb < QB; ++qb) {
       const int64_t o = ((qb0 + 16 * qb) * (4 * S) + split * 4 + g16) * R;
 #pragma unroll
       for (int t = 0; t < R; t += 4) {
@@ -460,7 +512,9 @@ static void with_M(int M, F f) {
   else if (M == 1) f(std::integral_constant<int, 1>{});
   else if (M == 2) f(std::integral_constant<int, 2>{});
   else if (M == 3) f(std::integral_constant<int, 3>{});
-  else f(std::integral_constant<int, 4>{});
+  else if (M == 4) f(std::integral_constant<int, 4>{});
+  else if (M == 5) f(std::integral_constant<int, 5>{});
+  else f(std::integral_constant<int, 6>{});
 }
 
 template <int DP, int R, int METRIC, int NW>
@@ -477,7 +531,8 @@ static void launch_res(const CandLaunch& c, hipStream_t s) {
 template <int DP, int R, int M, int NW>
 constexpr bool res_variant() {
   return (M != 2 || DP % 16 == 0) && (M != 1 || (NW == 4 && R != 4)) &&
-         (M < 3 || (DP % 32 == 0 && R == 4 && NW == 8));
+         (M < 3 || M == 6 || (DP % 32 == 0 && R == 4 && (NW == 8 || M == 5))) &&
+         (M != 6 || (DP % 16 == 0 && R != 16));
 }
 
 template <int DP>

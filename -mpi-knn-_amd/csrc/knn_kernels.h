@@ -68,7 +68,8 @@ int cand_tile_rows(int DP);         // train rows per tile of the kernel serving
 int cand_blocks_per_cu(int metric, int DP, int R, int nw);  // resident workgroups per CU
 
 // metric: 0 = L2 fp32 MFMA, 1 = L1 fp32 VALU, 2 = L2 bf16x3 MFMA (32x32x16),
-// 3 = L2 bf16x3 on 16x16x32, 4 = L2 fp16 on 16x16x32 (see knn_cand_res.hip)
+// 3 = L2 bf16x3 on 16x16x32, 4 = L2 fp16 on 16x16x32, 5 = 4 with 64 queries
+// per wave, 6 = L2 fp16 on 32x32x16 (see knn_cand_res.hip)
 struct CandLaunch {
   int metric, DP, R, S, n_qt;
   int64_t n_pad;

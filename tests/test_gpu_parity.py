@@ -34,16 +34,19 @@ def knn():
     return mod
 
 
-@pytest.fixture(scope="module", params=["auto", "fp32", "m16", "fp16"])
+@pytest.fixture(scope="module", params=["auto", "fp32", "m16", "fp16", "f16w", "f16l"])
 def clf(knn, request):
     """Every parity test runs with the default candidate path (AUTO: fp16 for
     batches of >= 4096 queries at d <= 256, else bf16x3 on 32x32x16 for L2),
     with the fp32 path forced, with bf16x3 on the 16x16x32 MFMA layout forced,
-    and with the fp16 path forced (every batch size)."""
+    and with the fp16 path forced (every batch size) on each of its MFMA
+    layouts (16x16x32 with 32 or 64 queries per wave, 32x32x16)."""
     c = knn.Classifier(0)
     c.set_precision({"auto": knn.PRECISION_AUTO, "fp32": knn.PRECISION_FP32,
-                     "m16": knn.PRECISION_BF16X3, "fp16": knn.PRECISION_FP16}[request.param])
+                     "m16": knn.PRECISION_BF16X3, "fp16": knn.PRECISION_FP16,
+                     "f16w": knn.PRECISION_FP16, "f16l": knn.PRECISION_FP16}[request.param])
     c.set_tuning("mfma16", 1 if request.param == "m16" else -1)
+    c.set_tuning("f16layout", {"fp16": 0, "f16w": 1, "f16l": 2}.get(request.param, -1))
     yield c
     c.close()
 
