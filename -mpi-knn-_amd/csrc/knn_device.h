@@ -252,6 +252,22 @@ __device__ __forceinline__ void select_quad(const f32x4& a, const f32x4& b, int 
 // select_quad with the quad's filter te kept by the caller (refreshed from
 // the 4 lanes' thresholds once per staged tile); an insertion lowers it to
 // this lane's new R-th entry.  thr is then L[R-1] and needs no copy.
+// row + c computed where it is used: a plain add is hoisted out of the
+// insertion branch by the compiler and then costs one VALU op per value on
+// every tile, inserting or not
+#ifndef KNN_ROW_AT
+#define KNN_ROW_AT 1
+#endif
+__device__ __forceinline__ int row_at(int row0, int c) {
+#if KNN_ROW_AT
+  int r;
+  asm volatile("v_add_u32 %0, %1, %2" : "=v"(r) : "v"(row0), "i"(c));
+  return r;
+#else
+  return row0 + c;
+#endif
+}
+
 template <int R>
 __device__ __forceinline__ void select_quad_te(const f32x4& a, const f32x4& b, int row0,
                                                float (&L)[R], int (&I)[R], float& te) {
@@ -264,7 +280,7 @@ __device__ __forceinline__ void select_quad_te(const f32x4& a, const f32x4& b, i
     for (int i = 0; i < 8; ++i) {
       const float v = i < 4 ? a[i] : b[i - 4];
       if (v < te) {
-        list_insert<R>(L, I, v, row0 + (i < 4 ? i : 16 + i - 4));
+        list_insert<R>(L, I, v, row_at(row0, i < 4 ? i : 16 + i - 4));
         te = __builtin_fminf(te, L[R - 1]);
       }
     }
