@@ -52,6 +52,18 @@ __device__ __forceinline__ void wait_barrier_x(int extra) {
 }
 
 constexpr int kPubEvery = 8;  // tiles between global-threshold exchanges
+// Early exchanges (KNN_EARLY_X): also at tiles 0, 1, 2 and 4.  The fetch at
+// tile 0 hands a workgroup of a later grid round the thresholds the earlier
+// rounds already published, and the early publishes shorten every list's
+// cold start -- the insertion-heavy tiles before a filter threshold exists,
+// where some lane of the wave inserts on nearly every value.
+#ifndef KNN_EARLY_X
+#define KNN_EARLY_X 1
+#endif
+__device__ __forceinline__ bool exchange_tile(int it) {
+  if (KNN_EARLY_X && it < kPubEvery) return it == 0 || it == 1 || it == 2 || it == 4;
+  return (it & (kPubEvery - 1)) == kPubEvery - 1;
+}
 
 template <int METRIC>
 constexpr int res_tpb() {
@@ -285,7 +297,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
           }
           x_age = -1;
         }
-        if ((it & (kPubEvery - 1)) == kPubEvery - 1 && it + PD < my_nt) {
+        if (x_age < 0 && exchange_tile(it) && it + PD < my_nt) {
           // publish the best list threshold of the query's lanes in this wave
           // (one lane per query, only when it improved), fetch its 4 slots
           uint32_t pk;
