@@ -412,7 +412,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   const bool m16 = ctx->tune_m16 < 0 ? m >= 4096 : ctx->tune_m16 > 0;
   if (kmetric == 2 && !s3 && m16 && DP % 32 == 0) kmetric = 3;
   int nw = 4;
-  if (DP <= 256 && kmetric != 1) nw = ctx->tune_nw ? ctx->tune_nw : (m >= 4096 ? 8 : 4);
+  if (DP <= 256 && kmetric != 1) nw = ctx->tune_nw ? std::min(ctx->tune_nw, 8) : (m >= 4096 ? 8 : 4);
   if (kmetric >= 3) nw = 8;
   if (s3) nw = 8;
   // fp16 MFMA shape (tuning key "f16layout": 0 = 16x16x32, 32 queries per
@@ -423,7 +423,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   if (kmetric == 4) {
     const int lay = ctx->tune_f16l < 0 ? 0 : ctx->tune_f16l;
     lmetric = 4 + lay;
-    if (lay > 0 && ctx->tune_nw) nw = ctx->tune_nw;
+    if (ctx->tune_nw && (lay == 0 || ctx->tune_nw != 16)) nw = ctx->tune_nw;
   }
   const bool wide = lmetric == 5;
   const int qpb = s3 ? kS3Rows : (DP <= 256 ? 32 * nw * (wide ? 2 : 1) : kQPB);
@@ -498,8 +498,8 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
     launch_cand_s3((const unsigned short*)ctx->XB.p, (const float*)ctx->XS.p,
                    (const unsigned short*)ctx->Q32.p, DP, n_pad3, R, S, n_qt, cl.out_v, cl.out_i,
                    cl.ablate, s);
-  else
-    launch_cand(cl, s);
+  else if (!launch_cand(cl, s))
+    return knn_fail(KNN_ERR_ARG, "no candidate kernel for this geometry (tuning overrides?)");
   HIP_TRY(hipGetLastError());
   if (tm) HIP_TRY(hipEventRecord(ctx->ev[2], s));
   HIP_TRY(hipMemsetAsync(ctx->rescan_cnt.p, 0, sizeof(int), s));
@@ -817,7 +817,8 @@ int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value) {
       return knn_fail(KNN_ERR_ARG, "R must be 0 (auto), 4, 8 or 16");
     ctx->tune_R = (int)value;
   } else if (!strcmp(key, "nw")) {
-    if (value != 0 && value != 4 && value != 8) return knn_fail(KNN_ERR_ARG, "nw must be 0, 4 or 8");
+    if (value != 0 && value != 4 && value != 8 && value != 16)
+      return knn_fail(KNN_ERR_ARG, "nw must be 0, 4, 8 or 16 (16: fp16 16x16x32 only)");
     ctx->tune_nw = (int)value;
   } else if (!strcmp(key, "ablate")) {
     ctx->tune_ablate = (int)value;  // timing experiments only: results become invalid

@@ -26,7 +26,7 @@
 namespace knnk {
 
 #define KNN_DECL(v)                                          \
-  void launch_res_##v(const CandLaunch& c, hipStream_t s);   \
+  bool launch_res_##v(const CandLaunch& c, hipStream_t s);   \
   int blocks_res_##v(int R, int metric, int nw);
 KNN_DP_LIST(KNN_DECL)
 #undef KNN_DECL
@@ -395,12 +395,9 @@ int cand_blocks_per_cu(int metric, int DP, int R, int nw) {
 
 int cand_tile_rows(int DP) { return DP <= 256 ? kResTileRows : 128; }
 
-void launch_cand(const CandLaunch& c, hipStream_t s) {
-#define KNN_CASE(v)                \
-  if (c.DP == v) {                 \
-    launch_res_##v(c, s);          \
-    return;                        \
-  }
+bool launch_cand(const CandLaunch& c, hipStream_t s) {
+#define KNN_CASE(v) \
+  if (c.DP == v) return launch_res_##v(c, s);
   KNN_DP_LIST(KNN_CASE)
 #undef KNN_CASE
   if (c.R == 8) {
@@ -410,6 +407,7 @@ void launch_cand(const CandLaunch& c, hipStream_t s) {
     if (c.metric == 1) launch_str<16, 1>(c, s);
     else launch_str<16, 0>(c, s);
   }
+  return true;
 }
 
 }  // namespace knnk

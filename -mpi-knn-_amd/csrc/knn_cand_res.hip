@@ -538,13 +538,14 @@ static void launch_res(const CandLaunch& c, hipStream_t s) {
 }
 
 // Instantiated variants: R in {4, 8, 16}; METRIC 0/2 with NW in {4, 8};
+// METRIC 4 also with NW = 16 (512 queries share each staged tile);
 // METRIC 1 (L1, not perf-graded) with NW = 4 and R in {8, 16}; METRIC 2
 // needs DP % 16 == 0.
 template <int DP, int R, int M, int NW>
 constexpr bool res_variant() {
   return (M != 2 || DP % 16 == 0) && (M != 1 || (NW == 4 && R != 4)) &&
-         (M < 3 || M == 6 || (DP % 32 == 0 && R == 4 && (NW == 8 || M == 5))) &&
-         (M != 6 || (DP % 16 == 0 && R != 16));
+         (M < 3 || M == 6 || (DP % 32 == 0 && R == 4 && (NW == 8 || M == 5 || M == 4))) &&
+         (M != 6 || (DP % 16 == 0 && R != 16)) && (NW != 16 || M == 4);
 }
 
 template <int DP>
@@ -552,7 +553,10 @@ static int blocks_per_cu_res(int R, int metric, int nw) {
   int out = 1;
   with_R(R, [&](auto Rc) {
     with_M(metric, [&](auto Mc) {
-      if (nw == 8) {
+      if (nw == 16) {
+        if constexpr (res_variant<DP, Rc.value, Mc.value, 16>())
+          out = occupancy_of(cand_kernel<DP, Rc.value, Mc.value, 16>, 1024);
+      } else if (nw == 8) {
         if constexpr (res_variant<DP, Rc.value, Mc.value, 8>())
           out = occupancy_of(cand_kernel<DP, Rc.value, Mc.value, 8>, 512);
       } else {
@@ -565,18 +569,23 @@ static int blocks_per_cu_res(int R, int metric, int nw) {
 }
 
 template <int DP>
-static void launch_res_dp(const CandLaunch& c, hipStream_t s) {
+static bool launch_res_dp(const CandLaunch& c, hipStream_t s) {
+  bool launched = false;  // false: no instantiated variant (caller reports it)
   with_R(c.R, [&](auto Rc) {
     with_M(c.metric, [&](auto Mc) {
-      if (c.nw == 8) {
+      if (c.nw == 16) {
+        if constexpr (res_variant<DP, Rc.value, Mc.value, 16>())
+          launch_res<DP, Rc.value, Mc.value, 16>(c, s), launched = true;
+      } else if (c.nw == 8) {
         if constexpr (res_variant<DP, Rc.value, Mc.value, 8>())
-          launch_res<DP, Rc.value, Mc.value, 8>(c, s);
+          launch_res<DP, Rc.value, Mc.value, 8>(c, s), launched = true;
       } else {
         if constexpr (res_variant<DP, Rc.value, Mc.value, 4>())
-          launch_res<DP, Rc.value, Mc.value, 4>(c, s);
+          launch_res<DP, Rc.value, Mc.value, 4>(c, s), launched = true;
       }
     });
   });
+  return launched;
 }
 
 #if KNN_GROUP == 0
@@ -592,7 +601,7 @@ static void launch_res_dp(const CandLaunch& c, hipStream_t s) {
 #endif
 
 #define KNN_DEF(v)                                                                 \
-  void launch_res_##v(const CandLaunch& c, hipStream_t s) { launch_res_dp<v>(c, s); } \
+  bool launch_res_##v(const CandLaunch& c, hipStream_t s) { return launch_res_dp<v>(c, s); } \
   int blocks_res_##v(int R, int metric, int nw) { return blocks_per_cu_res<v>(R, metric, nw); }
 KNN_GROUP_DPS(KNN_DEF)
 #undef KNN_DEF

@@ -97,7 +97,8 @@ void launch_query_check(const double* Q64, const double* mu, int64_t m, int d, i
                         double scale, int jx, double limit, float* valid, hipStream_t s);
 void launch_prep_queries(const double* Q64, const double* mu, int64_t m, int d, int DP,
                          int64_t m_pad, double scale, int jx, float* Q32, hipStream_t s);
-void launch_cand(const CandLaunch& c, hipStream_t s);
+// false: no kernel instantiated for this (DP, R, metric, nw) -- nothing launched
+bool launch_cand(const CandLaunch& c, hipStream_t s);
 // gthr: the candidate kernel's per-query global thresholds ([m_pad][4] keys)
 // or null when the kernel kept none
 // failed queries are appended to rescan_q with rescan_tau = the W-th exact

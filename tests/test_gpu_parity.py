@@ -283,3 +283,18 @@ def test_driver_matches_reference_outputs(tmp_path, knn):
         if s["Validation"]:
             assert str(fx.accuracy_line) in out
         assert "Running time is " in out
+
+
+@pytest.mark.parametrize("nw", [4, 8, 16])
+def test_fp16_workgroup_sizes(knn, nw):
+    """The fp16 kernel at 4, 8 and 16 waves per workgroup (16: 512 queries
+    share each staged tile), and the "nw" override on the other paths
+    (16 is clamped to 8 there): every launch matches the oracle."""
+    rng = np.random.default_rng(nw)
+    tr, lab, te = _mix(rng, 6000, 700, 128, 6)
+    for prec in (knn.PRECISION_FP16, knn.PRECISION_BF16X3, knn.PRECISION_FP32):
+        c = knn.Classifier(0)
+        c.set_precision(prec)
+        c.set_tuning("nw", nw)
+        run_case(c, knn, tr, lab, te, 10, 0, 6)
+        c.close()
