@@ -262,8 +262,10 @@ def main():
             fp32_r = run(knn.PRECISION_FP32, max(3, args.steps // 2), 1)
         same = bool(torch.equal(labels_auto, out_lab))
         total_q = m * world * args.steps
-        workload = ("cfg2: %d train x %d queries per GPU, d=%d, k=%d, L2, %d classes"
-                    % (n, m, d, k, C))
+        tag = {(1_000_000, 128, 10): "cfg2", (1_000_000, 960, 100): "cfg5"}.get(
+            (n, d, k), "custom")
+        workload = ("%s: %d train x %d queries per GPU, d=%d, k=%d, L2, %d classes"
+                    % (tag, n, m, d, k, C))
         parallelism = "query-sharded dp%d" % world
     else:
         # train-sharded: this rank's rows only; the same queries on every rank
