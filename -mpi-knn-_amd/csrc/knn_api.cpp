@@ -94,11 +94,16 @@ int knn_create(knn_ctx** out, int device) {
     delete c;
     return knn_fail(KNN_ERR_DEVICE, "hipStreamCreate failed");
   }
-  if (hipHostMalloc((void**)&c->h_count, sizeof(int) * 4, hipHostMallocDefault) != hipSuccess) {
-    (void)hipStreamDestroy(c->stream);
-    delete c;
-    return knn_fail(KNN_ERR_DEVICE, "hipHostMalloc failed");
+  // per-call rescan counts, written by the device (host-mapped pinned memory)
+  if (hipHostMalloc((void**)&c->h_counts, sizeof(int) * 4, hipHostMallocMapped) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&c->d_counts, c->h_counts, 0) != hipSuccess ||
+      hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming) != hipSuccess ||
+      c->totals.ensure(2 * sizeof(unsigned long long)) != KNN_OK ||
+      hipMemset(c->totals.p, 0, 2 * sizeof(unsigned long long)) != hipSuccess) {
+    knn_destroy(c);
+    return knn_fail(KNN_ERR_DEVICE, "context setup (pinned counters / events) failed");
   }
+  c->h_counts[0] = c->h_counts[1] = 0;
   if (hipDeviceGetAttribute(&c->cu_count, hipDeviceAttributeMultiprocessorCount, device) !=
           hipSuccess ||
       c->cu_count <= 0)
@@ -115,12 +120,14 @@ int knn_create(knn_ctx** out, int device) {
 int knn_destroy(knn_ctx* ctx) {
   if (!ctx) return KNN_OK;
   (void)hipSetDevice(ctx->device);
-  (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   for (DevBuf* b : ctx->all_bufs()) b->release();
-  for (auto& e : ctx->ev)
-    if (e) (void)hipEventDestroy(e);
-  if (ctx->h_count) (void)hipHostFree(ctx->h_count);
-  (void)hipStreamDestroy(ctx->stream);
+  for (auto& tc : ctx->ring)
+    for (auto& e : tc.ev)
+      if (e) (void)hipEventDestroy(e);
+  if (ctx->done_ev) (void)hipEventDestroy(ctx->done_ev);
+  if (ctx->h_counts) (void)hipHostFree(ctx->h_counts);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return KNN_OK;
 }
@@ -141,17 +148,26 @@ static int build_train(knn_ctx* ctx, const double* dX, const int32_t* dlab, int6
   if ((rc = ctx->X32.ensure((size_t)n_pad * (DP + 4) * sizeof(float) + 1024))) return rc;
   if ((rc = ctx->xl2.ensure((size_t)n_pad * sizeof(float)))) return rc;
   if ((rc = ctx->xl1.ensure((size_t)n_pad * sizeof(float)))) return rc;
-  if ((rc = ctx->stats.ensure(4 * sizeof(unsigned long long)))) return rc;
+  if ((rc = ctx->stats.ensure(6 * sizeof(unsigned long long)))) return rc;
   if ((rc = ctx->mu.ensure((size_t)d * sizeof(double)))) return rc;
   if ((rc = ctx->mu_part.ensure((size_t)col_mean_blocks(n) * d * sizeof(double)))) return rc;
   launch_col_mean(dX, n, d, (double*)ctx->mu_part.p, (double*)ctx->mu.p, ctx->stream);
-  HIP_TRY(hipMemsetAsync(ctx->stats.p, 0, 3 * sizeof(unsigned long long), ctx->stream));
+  HIP_TRY(hipMemsetAsync(ctx->stats.p, 0, 6 * sizeof(unsigned long long), ctx->stream));
   unsigned long long* st_d = (unsigned long long*)ctx->stats.p;
-  // operand scale 2^jx: max |x_i - mu_i| * 2^jx in [2^8, 2^9) (knn_prep.hip)
-  launch_absmax(dX, (const double*)ctx->mu.p, n, d, st_d + 2, ctx->stream);
+  // operand scale 2^jx: max |x_i - mu_i| * 2^jx in [2^8, 2^9) (knn_prep.hip);
+  // with it, the count of non-finite values and of labels out of range
+  launch_absmax(dX, (const double*)ctx->mu.p, n, d, st_d + 2, st_d + 4, ctx->stream);
+  launch_label_check(dlab, n, class_cnt, st_d + 5, ctx->stream);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(ctx->h_stats + 2, st_d + 2, 8, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipMemcpyAsync(ctx->h_stats + 2, st_d + 2, 4 * 8, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
+  ctx->trained = false;
+  if (ctx->h_stats[4])
+    return knn_fail(KNN_ERR_ARG, "train set holds " + std::to_string(ctx->h_stats[4]) +
+                                     " non-finite values (NaN / inf): distances undefined");
+  if (ctx->h_stats[5])
+    return knn_fail(KNN_ERR_ARG, std::to_string(ctx->h_stats[5]) +
+                                     " train labels outside [0, class_cnt)");
   memcpy(&ctx->xamax, &ctx->h_stats[2], 8);
   int e = 0;
   if (ctx->xamax > 0.0) (void)std::frexp(ctx->xamax, &e);  // xamax < 2^e
@@ -192,7 +208,9 @@ static int build_train(knn_ctx* ctx, const double* dX, const int32_t* dlab, int6
   ctx->idx_off = idx_off;
   ctx->DPb = 0;  // bf16x3 / fp16 copies are rebuilt lazily for the new train set
   ctx->DPh = 0;
+  ctx->DPs = 0;
   ctx->fp16_off = false;
+  ctx->auto_pending = false;
   ctx->trained = true;
   return KNN_OK;
 }
@@ -251,11 +269,14 @@ static int ensure_fp16(knn_ctx* ctx, hipStream_t s) {
 // fp16 candidate pass (kernel metric 4): PRECISION_FP16, or AUTO for batches
 // of >= 4096 queries (8-wave workgroups) until a batch certifies poorly.
 // Tuning key "fp16": -1 auto, 0 off, 1 on.
-static bool use_fp16(const knn_ctx* ctx, int metric, int64_t m) {
+// (W > kQuadMaxW: the R = 4 lists of the 16x16 layouts would overflow too
+// often -- AUTO keeps those for the 32x32 bf16x3 kernel with R = 8/16 lists)
+constexpr int kQuadMaxW = 64;
+static bool use_fp16(const knn_ctx* ctx, int metric, int64_t m, int W) {
   if (metric != KNN_METRIC_L2 || pad_dim_fp16(ctx->train.d) <= 0) return false;
   if (ctx->tune_fp16 >= 0) return ctx->tune_fp16 > 0;
   if (ctx->precision == KNN_PRECISION_FP16) return true;
-  return ctx->precision == KNN_PRECISION_AUTO && !ctx->fp16_off && m >= 4096;
+  return ctx->precision == KNN_PRECISION_AUTO && !ctx->fp16_off && m >= 4096 && W <= kQuadMaxW;
 }
 
 static bool use_bf16x3(const knn_ctx* ctx, int metric) {
@@ -316,16 +337,21 @@ static void choose_geometry(knn_ctx* ctx, int metric, int DP, int nw, int n_qt, 
                             int W, int C, int& S_out, int& R_out) {
   const int S_hi = (int)std::max<int64_t>(1, std::min<int64_t>(64, n_tiles));
   int bestS = 1, bestR = 8;
-  const bool quad = metric >= 3 && metric <= 5;  // 16x16 layouts
+  const bool quad = metric == 3 || metric == 4;  // 16x16 layouts
   const int lps = quad ? 4 : 2;  // lists per query per split
   for (int R : {4, 8, 16}) {
-    // kernel metrics 3-5 (16x16x32 layout) have R = 4 only; elsewhere R = 4
-    // only on request (resident kernel; tuning experiments); 6 has no R = 16
+    // kernel metrics 3, 4 (16x16x32 layout) have R = 4 only; elsewhere R = 4
+    // only on request (resident kernel; tuning experiments)
     if (quad ? R != 4 : (ctx->tune_R ? R != ctx->tune_R : R == 4)) continue;
-    if (metric == 6 && R == 16) continue;
     if (R == 4 && (DP > 256 || metric == 1)) continue;
     const int64_t slots = (int64_t)cand_blocks_per_cu(metric, DP, R, nw) * ctx->cu_count;
-    const int S_lo = std::min(S_hi, std::max(1, (C + lps * R - 1) / (lps * R)));
+    // the union of the lists must hold the C re-rank candidates; with R = 4
+    // lists (16x16 layouts) also S >= W, i.e. at most W/4S of the query's
+    // top W expected per list: a list holding 5 of them (an overflow ->
+    // the query fails certification) then has probability ~C(W,5)/(4S)^5
+    int S_lo = std::max(1, (C + lps * R - 1) / (lps * R));
+    if (quad) S_lo = std::max(S_lo, W);
+    S_lo = std::min(S_hi, S_lo);
     auto eff_of = [&](int S) {
       const int64_t wg = (int64_t)n_qt * S;
       const int64_t rounds = (wg + slots - 1) / slots;
@@ -344,10 +370,8 @@ static void choose_geometry(knn_ctx* ctx, int metric, int DP, int nw, int n_qt, 
     bestR = R;
     // R = 8 when the expected share of the top W per list (2S lists) is at
     // most 2: a list overflow (-> certification fails) is then rare and the
-    // fast rescan absorbs it.  Without a fast rescan (d > kRescanFastMaxDP a
-    // rescan is a full exact scan) R = 16 unless the share is at most 1/2.
-    const bool fast_rescan = DP <= kRescanFastMaxDP;
-    if (ctx->tune_R || quad || (fast_rescan ? W <= 4 * bS : W <= bS)) break;
+    // fast rescan absorbs it; else R = 16.
+    if (ctx->tune_R || quad || W <= 4 * bS) break;
   }
   S_out = bestS;
   R_out = bestR;
@@ -383,15 +407,51 @@ static double err_factor(int kmetric, int DP) {
   return (gam + (kmetric == 0 ? 5.0 : 3.0) * u) * 1.01;
 }
 
-// Core search: candidate pass + merge/re-rank/certify + rescan.
+// ---- timing ring (knn_set_timing): events of a call are read back lazily
+static void fold_timing(knn_ctx* ctx, TimedCall& tc) {
+  if (!tc.pending) return;
+  (void)hipEventSynchronize(tc.ev[4]);
+  for (int p = 0; p < 4; p++) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, tc.ev[p], tc.ev[p + 1]) == hipSuccess) ctx->tsum[p] += ms;
+  }
+  ctx->tcalls++;
+  tc.pending = false;
+}
+
+static TimedCall* timing_slot(knn_ctx* ctx) {
+  if (!ctx->timing) return nullptr;
+  TimedCall& tc = ctx->ring[ctx->ring_next];
+  fold_timing(ctx, tc);  // waits only when kTimingRing calls are still in flight
+  ctx->ring_last = ctx->ring_next;
+  ctx->ring_next = (ctx->ring_next + 1) % kTimingRing;
+  tc.pending = true;
+  return &tc;
+}
+
+// The deferred AUTO decision: once the last fp16 call has completed, its
+// rescan count (written by the device into h_counts) decides whether the
+// fp16 pass stays on for this train set.  Never waits.
+static void auto_check(knn_ctx* ctx) {
+  if (!ctx->auto_pending || hipEventQuery(ctx->done_ev) != hipSuccess) return;
+  // AUTO retires the fp16 pass for this train set when a batch leaves more
+  // than 1/16 of its queries to the rescan (data whose neighbour gaps are
+  // too fine for fp16 operands): later batches take bf16x3
+  if ((int64_t)ctx->h_counts[0] * 16 > ctx->auto_m) ctx->fp16_off = true;
+  ctx->auto_pending = false;
+}
+
+// Core search: candidate pass + merge/re-rank/certify + the device-driven
+// rescan.  Enqueue only: no host synchronisation on any path.
 int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric, const Sink& sink,
                    hipStream_t s) {
   const TrainDev& t = ctx->train;
   int rc;
-  // candidate-pass flavour: kmetric 2 = L2 via bf16x3 MFMA, else fp32
+  auto_check(ctx);
+  // candidate-pass flavour: kmetric 4 = L2 via fp16 MFMA, 2/3 = bf16x3, else fp32
   int kmetric = metric, DP = t.DP;
   const float* Xk = t.X32;
-  if (use_fp16(ctx, metric, m)) {
+  if (use_fp16(ctx, metric, m, W)) {
     if ((rc = ensure_fp16(ctx, s))) return rc;
     kmetric = 4;
     DP = ctx->DPh;
@@ -409,24 +469,14 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   // bf16x3 on the 16x16x32 MFMA layout (resident kernel, 8 waves, DP % 32 ==
   // 0): kernel metric 3, R = 4 lists, 4 lists per split.  Tuning key
   // "mfma16": -1 auto (on for batches of >= 4096 queries), 0 off, 1 on.
-  const bool m16 = ctx->tune_m16 < 0 ? m >= 4096 : ctx->tune_m16 > 0;
+  const bool m16 = ctx->tune_m16 < 0 ? m >= 4096 && W <= kQuadMaxW : ctx->tune_m16 > 0;
   if (kmetric == 2 && !s3 && m16 && DP % 32 == 0) kmetric = 3;
   int nw = 4;
   if (DP <= 256 && kmetric != 1) nw = ctx->tune_nw ? std::min(ctx->tune_nw, 8) : (m >= 4096 ? 8 : 4);
   if (kmetric >= 3) nw = 8;
+  if (kmetric == 4 && ctx->tune_nw) nw = ctx->tune_nw;  // 4, 8 or 16
   if (s3) nw = 8;
-  // fp16 MFMA shape (tuning key "f16layout": 0 = 16x16x32, 32 queries per
-  // wave (kernel flavour 4); 1 = the same with 64 queries per wave (5); 2 =
-  // 32x32x16 (6); -1 auto): one arithmetic, error bound and proxy scale, so
-  // kmetric stays 4 outside the launch
-  int lmetric = kmetric;
-  if (kmetric == 4) {
-    const int lay = ctx->tune_f16l < 0 ? 0 : ctx->tune_f16l;
-    lmetric = 4 + lay;
-    if (ctx->tune_nw && (lay == 0 || ctx->tune_nw != 16)) nw = ctx->tune_nw;
-  }
-  const bool wide = lmetric == 5;
-  const int qpb = s3 ? kS3Rows : (DP <= 256 ? 32 * nw * (wide ? 2 : 1) : kQPB);
+  const int qpb = s3 ? kS3Rows : (DP <= 256 ? 32 * nw : kQPB);
   const int n_qt = (int)((m + qpb - 1) / qpb);
   const int64_t m_pad = (int64_t)n_qt * qpb;
   const int64_t n_pad3 = (t.n + kS3Rows - 1) / kS3Rows * kS3Rows;
@@ -434,11 +484,13 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   int C = (int)std::min<int64_t>(t.n, std::max(2 * W, W + 16));
   C = std::min(C, kMaxUnion);
   int S = 1, R = 8;
-  choose_geometry(ctx, lmetric, DP, nw, n_qt, n_tiles, W, C, S, R);
-  const bool quad_lists = lmetric >= 3 && lmetric <= 5;  // 16x16 layouts: 4 lists per split
+  choose_geometry(ctx, kmetric, DP, nw, n_qt, n_tiles, W, C, S, R);
+  const bool quad_lists = kmetric == 3 || kmetric == 4;  // 16x16 layouts: 4 lists per split
   if (quad_lists) R = 4;
   const int NL = (quad_lists ? 4 : 2) * S;
   C = std::min(C, NL * R);
+  // rescan workspace: the fast path serves the first `cap` failed queries
+  const int cap = (int)std::min<int64_t>(m, kRescanFastQueries);
   if ((rc = ctx->Q32.ensure((size_t)m_pad * DP * sizeof(float)))) return rc;
   if ((rc = ctx->qvalid.ensure((size_t)m_pad * sizeof(float)))) return rc;
   if ((rc = ctx->cand_v.ensure((size_t)m_pad * NL * R * sizeof(float)))) return rc;
@@ -449,7 +501,12 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   if (use_gthr && (rc = ctx->gthr.ensure((size_t)m_pad * 4 * sizeof(uint32_t)))) return rc;
   if ((rc = ctx->rescan_q.ensure((size_t)m * sizeof(int) + 16))) return rc;
   if ((rc = ctx->rescan_tau.ensure((size_t)m * sizeof(double) + 16))) return rc;
-  if ((rc = ctx->rescan_cnt.ensure(16))) return rc;
+  if ((rc = ctx->rescan_cnt.ensure(4 * sizeof(int)))) return rc;
+  if ((rc = ctx->fr_cnt.ensure((size_t)cap * sizeof(int) + 16))) return rc;
+  if ((rc = ctx->fr_buf.ensure((size_t)cap * kRescanCap * sizeof(int) + 16))) return rc;
+  if ((rc = ctx->fr_q.ensure((size_t)cap * t.DP * sizeof(float) + 16))) return rc;
+  if ((rc = ctx->fr_thr.ensure((size_t)cap * sizeof(float) + 16))) return rc;
+  if ((rc = ctx->slow_q.ensure((size_t)m * sizeof(int) + 16))) return rc;
 
   ctx->last_kmetric = kmetric;
   ctx->geom[0] = (int64_t)n_qt * S;
@@ -457,8 +514,16 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   ctx->geom[2] = R;
   ctx->last_nw = nw;
   ctx->geom[3] = C;
-  const bool tm = ctx->timing;
-  if (tm) HIP_TRY(hipEventRecord(ctx->ev[0], s));
+  if (s3)
+    snprintf(ctx->last_kernel, sizeof ctx->last_kernel, "cand_s3_kernel<%d>", R);
+  else if (DP <= 256)
+    snprintf(ctx->last_kernel, sizeof ctx->last_kernel, "cand_kernel<%d,%d,%d,%d>", DP, R, kmetric,
+             nw);
+  else
+    snprintf(ctx->last_kernel, sizeof ctx->last_kernel, "cand_stream_kernel<%d,%d,%d>", kStreamDC,
+             R, kmetric);
+  TimedCall* tc = timing_slot(ctx);
+  if (tc) HIP_TRY(hipEventRecord(tc->ev[0], s));
   // query operands: scale * 2^jx (q - mu), scale -2 for L2; a query whose
   // operands would leave the format's range (fp16: 65000, else 2^100) is
   // marked void and goes to the exact rescan
@@ -477,9 +542,9 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
                       (unsigned short*)ctx->Q32.p, 2 * DP, nullptr, nullptr, s);
   else
     launch_prep_queries(dQ, t.mu, m, t.d, DP, m_pad, qscale, t.jx, (float*)ctx->Q32.p, s);
-  if (tm) HIP_TRY(hipEventRecord(ctx->ev[1], s));
+  if (tc) HIP_TRY(hipEventRecord(tc->ev[1], s));
   CandLaunch cl{};
-  cl.metric = lmetric;
+  cl.metric = kmetric;
   cl.DP = DP;
   cl.R = R;
   cl.S = S;
@@ -501,8 +566,8 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   else if (!launch_cand(cl, s))
     return knn_fail(KNN_ERR_ARG, "no candidate kernel for this geometry (tuning overrides?)");
   HIP_TRY(hipGetLastError());
-  if (tm) HIP_TRY(hipEventRecord(ctx->ev[2], s));
-  HIP_TRY(hipMemsetAsync(ctx->rescan_cnt.p, 0, sizeof(int), s));
+  if (tc) HIP_TRY(hipEventRecord(tc->ev[2], s));
+  HIP_TRY(hipMemsetAsync(ctx->rescan_cnt.p, 0, 4 * sizeof(int), s));
   launch_merge_rerank(metric, (const float*)ctx->cand_v.p, (const int*)ctx->cand_i.p, NL, R, t, dQ,
                       m, W, C, err_factor(kmetric, DP),
                       kmetric == 4 ? ProxyScale{qvalid, 0x1p-14, 0x1p-28,
@@ -511,81 +576,27 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
                       cl.gthr, sink, (int*)ctx->rescan_q.p,
                       (double*)ctx->rescan_tau.p, (int*)ctx->rescan_cnt.p, s);
   HIP_TRY(hipGetLastError());
-  if (tm) HIP_TRY(hipEventRecord(ctx->ev[3], s));
-  HIP_TRY(hipMemcpyAsync(ctx->h_count, ctx->rescan_cnt.p, sizeof(int), hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  const int nflag = ctx->h_count[0];
-  ctx->last_rescan = nflag;
-  // AUTO retires the fp16 pass for this train set when a batch leaves more
-  // than 1/16 of its queries to the rescan (data whose neighbour gaps are
-  // too fine for fp16 operands): later batches take bf16x3
-  if (kmetric == 4 && ctx->precision == KNN_PRECISION_AUTO && (int64_t)nflag * 16 > m)
-    ctx->fp16_off = true;
-  ctx->last_slow_rescan = 0;
-  if (tm) {
-    float ms;
-    for (int p = 0; p < 3; p++) {
-      HIP_TRY(hipEventElapsedTime(&ms, ctx->ev[p], ctx->ev[p + 1]));
-      ctx->phase_ms[p] = ms;
-    }
-    ctx->phase_ms[3] = 0.0;
-  }
-  if (nflag > 0) {
-    // fast filtered rescan (one pass over the fp32 train copy per 64 failed
-    // queries, d <= kRescanFastMaxDP); what it cannot finish goes to the full
-    // exact scan below
-    const bool fast = t.DP <= kRescanFastMaxDP;
-    const int fb = std::min(nflag, 4096);
-    if ((rc = ctx->fr_cnt.ensure((size_t)fb * sizeof(int)))) return rc;
-    if ((rc = ctx->fr_buf.ensure((size_t)fb * kRescanCap * sizeof(int)))) return rc;
-    if ((rc = ctx->fr_q.ensure((size_t)fb * (t.DP + 1) * sizeof(float)))) return rc;
-    if ((rc = ctx->slow_q.ensure((size_t)nflag * sizeof(int) + 16))) return rc;
-    // rescan_cnt is reused as the count of queries for the full scan (still
-    // nflag, with every failed query, when there is no fast path)
-    if (fast) HIP_TRY(hipMemsetAsync(ctx->rescan_cnt.p, 0, sizeof(int), s));
-    else
-      HIP_TRY(hipMemcpyAsync(ctx->slow_q.p, ctx->rescan_q.p, (size_t)nflag * sizeof(int),
-                             hipMemcpyDeviceToDevice, s));
-    for (int f0 = 0; fast && f0 < nflag; f0 += fb) {
-      const int nf = std::min(fb, nflag - f0);
-      HIP_TRY(hipMemsetAsync(ctx->fr_cnt.p, 0, (size_t)nf * sizeof(int), s));
-      launch_rescan_fast(metric, t, dQ, (const int*)ctx->rescan_q.p,
-                         (const double*)ctx->rescan_tau.p, f0, nf, W, err_factor(metric, t.DP),
-                         (float*)ctx->fr_q.p, (float*)ctx->fr_q.p + (size_t)fb * t.DP,
-                         (int*)ctx->fr_cnt.p, (int*)ctx->fr_buf.p, sink, (int*)ctx->slow_q.p,
-                         (int*)ctx->rescan_cnt.p, s);
-      HIP_TRY(hipGetLastError());
-    }
-    HIP_TRY(hipMemcpyAsync(ctx->h_count, ctx->rescan_cnt.p, sizeof(int), hipMemcpyDeviceToHost,
-                           s));
-    HIP_TRY(hipStreamSynchronize(s));
-    const int nslow = ctx->h_count[0];
-    ctx->last_slow_rescan = nslow;
-    if (getenv("KNN_DEBUG_RESCAN"))
-      fprintf(stderr, "[knn] %d queries not certified, %d sent to the full scan\n", nflag, nslow);
-    if (nslow > 0) {
-      const size_t per = rescan_scratch_entries(t.n, W);
-      int64_t batch = (int64_t)((256ull << 20) / (per * 12 + 1));
-      batch = std::max<int64_t>(1, std::min<int64_t>(batch, 4096));
-      batch = std::min<int64_t>(batch, nslow);
-      if ((rc = ctx->ra_k.ensure(per * batch * sizeof(double)))) return rc;
-      if ((rc = ctx->ra_i.ensure(per * batch * sizeof(int)))) return rc;
-      if ((rc = ctx->rb_k.ensure(per * batch * sizeof(double)))) return rc;
-      if ((rc = ctx->rb_i.ensure(per * batch * sizeof(int)))) return rc;
-      for (int f0 = 0; f0 < nslow; f0 += (int)batch) {
-        const int nf = (int)std::min<int64_t>(batch, nslow - f0);
-        launch_rescan(metric, t, dQ, (const int*)ctx->slow_q.p, f0, nf, W, (double*)ctx->ra_k.p,
-                      (int*)ctx->ra_i.p, (double*)ctx->rb_k.p, (int*)ctx->rb_i.p, sink, s);
-        HIP_TRY(hipGetLastError());
-      }
-    }
-    if (tm) {
-      HIP_TRY(hipEventRecord(ctx->ev[4], s));
-      HIP_TRY(hipEventSynchronize(ctx->ev[4]));
-      float ms;
-      HIP_TRY(hipEventElapsedTime(&ms, ctx->ev[3], ctx->ev[4]));
-      ctx->phase_ms[3] = ms;
-    }
+  if (tc) HIP_TRY(hipEventRecord(tc->ev[3], s));
+  // rescan of uncertified queries, sized on the device (knn_select.hip)
+  RescanBufs rb{};
+  rb.q = (int*)ctx->rescan_q.p;
+  rb.tau = (double*)ctx->rescan_tau.p;
+  rb.cnt = (int*)ctx->rescan_cnt.p;
+  rb.qf = (float*)ctx->fr_q.p;
+  rb.thr = (float*)ctx->fr_thr.p;
+  rb.fcnt = (int*)ctx->fr_cnt.p;
+  rb.buf = (int*)ctx->fr_buf.p;
+  rb.slow_q = (int*)ctx->slow_q.p;
+  rb.counts = ctx->d_counts;
+  rb.totals = (unsigned long long*)ctx->totals.p;
+  launch_rescan(metric, t, dQ, rb, cap, W, err_factor(metric, t.DP), sink,
+                (int)std::min<int64_t>(m, ctx->cu_count), s);
+  HIP_TRY(hipGetLastError());
+  if (tc) HIP_TRY(hipEventRecord(tc->ev[4], s));
+  HIP_TRY(hipEventRecord(ctx->done_ev, s));
+  if (kmetric == 4 && ctx->precision == KNN_PRECISION_AUTO && ctx->tune_fp16 < 0) {
+    ctx->auto_pending = true;
+    ctx->auto_m = m;
   }
   return KNN_OK;
 }
@@ -613,7 +624,6 @@ int knn_classify_device(knn_ctx* ctx, const double* dQ, int64_t m, int32_t k, in
   if ((rc = check_query_args(ctx, m, k, metric))) return rc;
   if (!d_labels) return knn_fail(KNN_ERR_ARG, "null labels output");
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
-  ctx->last_rescan = 0;
   if (m == 0) return KNN_OK;
   if (!dQ) return knn_fail(KNN_ERR_ARG, "null query pointer");
   if (k == 0) {  // cpp:324: max_label stays -1
@@ -786,10 +796,34 @@ int knn_sync(knn_ctx* ctx) {
   int rc;
   if ((rc = device_guard(ctx))) return rc;
   HIP_TRY(hipStreamSynchronize(ctx->stream));
+  HIP_TRY(hipEventSynchronize(ctx->done_ev));  // the last call, on whatever stream it ran
+  auto_check(ctx);
   return KNN_OK;
 }
 
-int64_t knn_last_rescan_count(knn_ctx* ctx) { return ctx ? ctx->last_rescan : -1; }
+int64_t knn_last_rescan_count(knn_ctx* ctx) {
+  if (!ctx || hipSetDevice(ctx->device) != hipSuccess) return -1;
+  if (hipEventSynchronize(ctx->done_ev) != hipSuccess) return -1;  // the last call's counts
+  auto_check(ctx);
+  return ctx->h_counts[0];
+}
+
+int knn_rescan_totals(knn_ctx* ctx, int64_t out[2], int reset) {
+  int rc;
+  if ((rc = device_guard(ctx))) return rc;
+  if (!out) return knn_fail(KNN_ERR_ARG, "null output");
+  unsigned long long v[2];
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  HIP_TRY(hipEventSynchronize(ctx->done_ev));
+  HIP_TRY(hipMemcpy(v, ctx->totals.p, sizeof v, hipMemcpyDeviceToHost));
+  out[0] = (int64_t)v[0];
+  out[1] = (int64_t)v[1];
+  if (reset) HIP_TRY(hipMemset(ctx->totals.p, 0, sizeof v));
+  auto_check(ctx);
+  return KNN_OK;
+}
+
+const char* knn_last_kernel_name(knn_ctx* ctx) { return ctx ? ctx->last_kernel : ""; }
 
 int knn_set_precision(knn_ctx* ctx, int mode) {
   if (!ctx) return knn_fail(KNN_ERR_ARG, "null context");
@@ -806,9 +840,6 @@ int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value) {
   if (!strcmp(key, "fp16")) {
     if (value < -1 || value > 1) return knn_fail(KNN_ERR_ARG, "fp16 must be -1, 0 or 1");
     ctx->tune_fp16 = (int)value;
-  } else if (!strcmp(key, "f16layout")) {
-    if (value < -1 || value > 2) return knn_fail(KNN_ERR_ARG, "f16layout must be -1 .. 2");
-    ctx->tune_f16l = (int)value;
   } else if (!strcmp(key, "mfma16")) {
     if (value < -1 || value > 1) return knn_fail(KNN_ERR_ARG, "mfma16 must be -1, 0 or 1");
     ctx->tune_m16 = (int)value;
@@ -834,15 +865,35 @@ int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value) {
 int knn_set_timing(knn_ctx* ctx, int enable) {
   int rc;
   if ((rc = device_guard(ctx))) return rc;
-  if (enable && !ctx->ev[0])
-    for (auto& e : ctx->ev) HIP_TRY(hipEventCreate(&e));
+  if (enable && !ctx->ring[0].ev[0])
+    for (auto& tc : ctx->ring)
+      for (auto& e : tc.ev) HIP_TRY(hipEventCreate(&e));
   ctx->timing = enable != 0;
   return KNN_OK;
 }
 
 double knn_last_phase_ms(knn_ctx* ctx, int phase) {
-  if (!ctx || phase < 0 || phase > 3) return -1.0;
-  return ctx->phase_ms[phase];
+  if (!ctx || phase < 0 || phase > 3 || ctx->ring_last < 0) return -1.0;
+  if (hipSetDevice(ctx->device) != hipSuccess) return -1.0;
+  TimedCall& tc = ctx->ring[ctx->ring_last];
+  if (hipEventSynchronize(tc.ev[4]) != hipSuccess) return -1.0;
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, tc.ev[phase], tc.ev[phase + 1]) != hipSuccess) return -1.0;
+  return ms;
+}
+
+int knn_timing_totals(knn_ctx* ctx, double out_ms[4], int64_t* calls, int reset) {
+  int rc;
+  if ((rc = device_guard(ctx))) return rc;
+  for (auto& tc : ctx->ring) fold_timing(ctx, tc);
+  if (out_ms)
+    for (int p = 0; p < 4; p++) out_ms[p] = ctx->tsum[p];
+  if (calls) *calls = ctx->tcalls;
+  if (reset) {
+    for (double& v : ctx->tsum) v = 0.0;
+    ctx->tcalls = 0;
+  }
+  return KNN_OK;
 }
 
 int knn_last_geometry(knn_ctx* ctx, int64_t out[4]) {

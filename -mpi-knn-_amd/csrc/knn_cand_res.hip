@@ -25,16 +25,6 @@ static_assert(KNN_RES_TPB * knnk::kTR == knnk::kResTileRows || KNN_RES_TPB != 2,
 #ifndef KNN_M4_SEED4
 #define KNN_M4_SEED4 1
 #endif
-// METRIC 5 = the fp16 kernel with 64 queries per wave (4 query blocks of 16):
-// each A fragment read from LDS feeds 4 MFMAs instead of 2, halving the LDS
-// read traffic per MFMA (the 32-query kernel moves 128 B/clk/CU of A
-// fragments at full MFMA rate -- the whole LDS bandwidth)
-#ifndef KNN_M5_TPB
-#define KNN_M5_TPB 4
-#endif
-#ifndef KNN_M5_WPE
-#define KNN_M5_WPE 2
-#endif
 
 namespace knnk {
 
@@ -67,7 +57,7 @@ __device__ __forceinline__ bool exchange_tile(int it) {
 
 template <int METRIC>
 constexpr int res_tpb() {
-  return METRIC == 5 ? KNN_M5_TPB : (METRIC == 4 || METRIC == 6 ? KNN_M4_TPB : KNN_RES_TPB);
+  return METRIC == 4 ? KNN_M4_TPB : KNN_RES_TPB;
 }
 
 // Train rows in HBM (X32 for fp32/L1, XB for bf16x3) share one padded row
@@ -103,8 +93,7 @@ constexpr int res_tpb() {
 // (not for R = 16 lists or DP > 160, whose registers do not fit: spills).
 template <int DP, int R, int METRIC, int NW>
 __global__ void __launch_bounds__(NW * 64)
-__attribute__((amdgpu_waves_per_eu(METRIC == 5 ? KNN_M5_WPE
-                                   : ((METRIC >= 4 ? DP / 2 : DP) <= 160 && R <= 8 ? 4 : 1))))
+__attribute__((amdgpu_waves_per_eu((METRIC == 4 ? DP / 2 : DP) <= 160 && R <= 8 ? 4 : 1)))
 cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
             int n_qt, float* __restrict__ out_v, int* __restrict__ out_i, int abl,
             uint32_t* gthr) {
@@ -113,9 +102,9 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   // keeping them in VGPRs (its waits would then also drain the LDS-DMA queue).
   // abl: timing-only ablations (results invalid): bit0 = no staging loads
   // after the first tiles, bit1 = no selection epilogue.  0 in production.
-  // fp16 operands: METRIC 4/5 on the 16x16x32 layout, 6 on 32x32x16
-  constexpr bool F16 = METRIC >= 4;
-  constexpr bool TEC = (METRIC == 4 || METRIC == 5) && KNN_M4_TE_CACHE;
+  // fp16 operands: METRIC 4 on the 16x16x32 layout
+  constexpr bool F16 = METRIC == 4;
+  constexpr bool TEC = METRIC == 4 && KNN_M4_TE_CACHE;
   constexpr int DPF = F16 ? DP / 2 : DP;    // payload floats per row
   constexpr int RSF = DPF + 4;              // row stride (floats), HBM and LDS
   constexpr int TPB = res_tpb<METRIC>();    // 32-row sub-tiles per staged tile
@@ -137,9 +126,8 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   // METRIC 3 (bf16x3 on 16x16x32) and 4 (fp16 on 16x16x32): lane l holds
   // queries wv*32 + qb*16 + (l&15), qb = 0, 1, against rows 4*(l>>4) + i of
   // each 16-row block
-  // (METRIC 5: qb = 0..3, 64 queries per wave)
-  constexpr bool M16 = METRIC >= 3 && METRIC <= 5;
-  constexpr int QB = METRIC == 5 ? 4 : 2;  // 16-query blocks per wave (M16)
+  constexpr bool M16 = METRIC == 3 || METRIC == 4;
+  constexpr int QB = 2;                    // 16-query blocks per wave (M16)
   constexpr int QW = M16 ? 16 * QB : 32;   // queries per wave
   const int c16 = lane & 15, g16 = lane >> 4;
   const int64_t qb0 = (int64_t)qt * (NW * QW) + wv * QW + c16;  // query of block 0 (+16 qb: block qb)
@@ -150,7 +138,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   // qh dims 16t+8h..16t+8h+7, float4 DP/16+t the same dims of ql.
   // METRIC 4: fp16 -2q (the train set's power-of-two scale), float4 qb*(DP/32)+ks
   // = dims 32ks + 8*g16 .. +7 of query block qb.
-  constexpr int NQF = METRIC == 1 ? 1 : (METRIC == 6 ? DP / 16 : (F16 ? QB * DP / 32 : DP / 8));
+  constexpr int NQF = METRIC == 1 ? 1 : (F16 ? QB * DP / 32 : DP / 8);
   float4 qf[NQF];
   if constexpr (METRIC != 1) {
     // Loaded with inline asm (loads + their vmcnt(0) in one statement): with
@@ -164,10 +152,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int c = c0 + u < NQF ? c0 + u : c0;
-        if constexpr (METRIC == 6) {
-          // 32x32x16 B fragment: query j, dims 16c + 8h .. +7
-          p[u] = Q32 + qg * (DP / 2) + 8 * c + 4 * h;
-        } else if constexpr (F16) {
+        if constexpr (F16) {
           const int ks = c % (DP / 32), qb = c / (DP / 32);
           p[u] = Q32 + (qb0 + 16 * qb) * (DP / 2) + 16 * ks + 4 * g16;
         } else if constexpr (M16) {
@@ -227,9 +212,8 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   // e+1 .. e+PD-1 leave those x ops in flight (counted wait + x), the
   // barrier of tile e+PD retires them and the slots are read after it -- no
   // barrier ever waits on a (contended) atomic.
-  // byte offset of gthr[query][0]: the lane's query, or for METRIC 3 query
+  // byte offset of gthr[query][0]: the lane's query, or for METRIC 3/4 query
   // (l & 31) of the wave (lanes 0-15 block 0, 16-31 block 1; 32-63 repeat)
-  // (METRIC 5: lane l <-> query l of the wave)
   const uint32_t goff =
       M16 ? (uint32_t)(((int64_t)qt * (NW * QW) + wv * QW + (lane & (QW - 1))) * 16)
           : (uint32_t)(qg * 16);
@@ -302,12 +286,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
           // (one lane per query, only when it improved), fetch its 4 slots
           uint32_t pk;
           bool pub;
-          if constexpr (QB == 4) {
-            const float m0 = quad_min(thr[0]), m1 = quad_min(thr[1]);
-            const float m2 = quad_min(thr[2]), m3 = quad_min(thr[3]);
-            pk = f2key(g16 == 0 ? m0 : g16 == 1 ? m1 : g16 == 2 ? m2 : m3);
-            pub = pk < last_pub;
-          } else if constexpr (M16) {
+          if constexpr (M16) {
             const float m0 = quad_min(thr[0]), m1 = quad_min(thr[1]);
             pk = f2key(g16 == 0 ? m0 : m1);
             pub = g16 < 2 && pk < last_pub;
@@ -412,32 +391,9 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       }
     } else {
     f32x16 acc;
-    if constexpr (METRIC == 6) {
-      // rows 8q + 4h .. +3: their seeds sit in the pad of row 8q + 4h
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 sd = *(const float4*)(base + (8 * q + 4 * h) * RSF + SEED);
-        acc[4 * q] = sd.x;
-        acc[4 * q + 1] = sd.y;
-        acc[4 * q + 2] = sd.z;
-        acc[4 * q + 3] = sd.w;
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[i] = base[((i & 3) + 8 * (i >> 2) + 4 * h) * RSF + SEED];
-    }
-    if constexpr (METRIC == 6) {
-      // fp16 on v_mfma_f32_32x32x16_f16: one MFMA per 16 dims (products
-      // exact in fp32); 24 of its 32 issue cycles are free for the epilogue's
-      // VALU work, against 8 of 16 on the 16x16x32 shape
-      const float* arow = base + j * RSF + 4 * h;
-#pragma unroll
-      for (int tt = 0; tt < DP / 16; ++tt) {
-        const f16x8 a = __builtin_bit_cast(f16x8, *(const float4*)(arow + 8 * tt));
-        const f16x8 b = __builtin_bit_cast(f16x8, qf[tt]);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc, 0, 0, 0);
-      }
-    } else if constexpr (METRIC == 0) {
+    for (int i = 0; i < 16; ++i) acc[i] = base[((i & 3) + 8 * (i >> 2) + 4 * h) * RSF + SEED];
+    if constexpr (METRIC == 0) {
       const float* arow = base + j * RSF + 4 * h;
 #pragma unroll
       for (int c = 0; c < DP / 8; ++c) {
@@ -524,9 +480,7 @@ static void with_M(int M, F f) {
   else if (M == 1) f(std::integral_constant<int, 1>{});
   else if (M == 2) f(std::integral_constant<int, 2>{});
   else if (M == 3) f(std::integral_constant<int, 3>{});
-  else if (M == 4) f(std::integral_constant<int, 4>{});
-  else if (M == 5) f(std::integral_constant<int, 5>{});
-  else f(std::integral_constant<int, 6>{});
+  else f(std::integral_constant<int, 4>{});
 }
 
 template <int DP, int R, int METRIC, int NW>
@@ -544,8 +498,7 @@ static void launch_res(const CandLaunch& c, hipStream_t s) {
 template <int DP, int R, int M, int NW>
 constexpr bool res_variant() {
   return (M != 2 || DP % 16 == 0) && (M != 1 || (NW == 4 && R != 4)) &&
-         (M < 3 || M == 6 || (DP % 32 == 0 && R == 4 && (NW == 8 || M == 5 || M == 4))) &&
-         (M != 6 || (DP % 16 == 0 && R != 16)) && (NW != 16 || M == 4);
+         (M < 3 || (DP % 32 == 0 && R == 4 && (NW == 8 || M == 4))) && (NW != 16 || M == 4);
 }
 
 template <int DP>

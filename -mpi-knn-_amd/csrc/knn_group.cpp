@@ -258,6 +258,8 @@ int knn_group_classify(knn_group* g, const double* Q, int64_t m, int32_t k, int3
     return KNN_OK;
   }
   const int w = (int)std::min<int64_t>((int64_t)k + 1, g->n);
+  if ((int64_t)G * w > 4096)  // merge_vote_partials holds the G*w entries of a query in LDS
+    return knn_fail(KNN_ERR_ARG, "train-sharded merge needs ngpus * (k+1) <= 4096");
   int rc = for_each_dev(g, [&](int i) {
     int e;
     if ((e = g->Q[i].ensure((size_t)m * d * sizeof(double)))) return e;

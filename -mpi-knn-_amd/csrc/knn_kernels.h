@@ -68,8 +68,7 @@ int cand_tile_rows(int DP);         // train rows per tile of the kernel serving
 int cand_blocks_per_cu(int metric, int DP, int R, int nw);  // resident workgroups per CU
 
 // metric: 0 = L2 fp32 MFMA, 1 = L1 fp32 VALU, 2 = L2 bf16x3 MFMA (32x32x16),
-// 3 = L2 bf16x3 on 16x16x32, 4 = L2 fp16 on 16x16x32, 5 = 4 with 64 queries
-// per wave, 6 = L2 fp16 on 32x32x16 (see knn_cand_res.hip)
+// 3 = L2 bf16x3 on 16x16x32, 4 = L2 fp16 on 16x16x32 (see knn_cand_res.hip)
 struct CandLaunch {
   int metric, DP, R, S, n_qt;
   int64_t n_pad;
@@ -89,7 +88,9 @@ int col_mean_blocks(int64_t n);  // rows of the `partial` scratch (x d doubles)
 void launch_col_mean(const double* X64, int64_t n, int d, double* partial, double* mu,
                      hipStream_t s);
 void launch_absmax(const double* X64, const double* mu, int64_t n, int d, unsigned long long* out,
-                   hipStream_t s);
+                   unsigned long long* nonfinite, hipStream_t s);
+void launch_label_check(const int32_t* lab, int64_t n, int class_cnt, unsigned long long* bad,
+                        hipStream_t s);
 void launch_prep_train(const double* X64, const double* mu, int64_t n, int d, int DP,
                        int64_t n_pad, int jx, float* X32, float* xl2, float* xl1,
                        unsigned long long* stats, hipStream_t s);
@@ -120,20 +121,28 @@ void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int
                          const TrainDev& t, const double* Q64, int64_t m, int W, int C,
                          double f_err, ProxyScale ps, const uint32_t* gthr, const Sink& sink,
                          int* rescan_q, double* rescan_tau, int* rescan_cnt, hipStream_t s);
-constexpr int kRescanCap = 1024;  // rows a fast rescan may append per query
-constexpr int kRescanFastMaxDP = 256;  // fast rescan: resident-kernel dimensions
-// Fast rescan of failed queries [f0, f0+nf): scratch qf[nf * t.DP], thr[nf],
-// cnt[nf] (zeroed by the caller), buf[nf * kRescanCap]; queries it cannot
-// finish land in slow_q/slow_cnt (for launch_rescan).  f_err: the fp32
-// candidate error factor of t.DP.
-void launch_rescan_fast(int metric, const TrainDev& t, const double* Q64, const int* rescan_q,
-                        const double* tau, int f0, int nf, int W, double f_err, float* qf,
-                        float* thr, int* cnt, int* buf, const Sink& sink, int* slow_q,
-                        int* slow_cnt, hipStream_t s);
-void launch_rescan(int metric, const TrainDev& t, const double* Q64, const int* rescan_q,
-                   int f0, int nf, int W, double* pa_k, int* pa_i, double* pb_k, int* pb_i,
-                   const Sink& sink, hipStream_t s);
-size_t rescan_scratch_entries(int64_t n, int W);  // per flagged query, per buffer
+constexpr int kRescanCap = 1024;        // rows a fast rescan may append per query
+constexpr int kRescanStageMaxDP = 256;  // fast rescan stages rows in LDS up to this DP
+constexpr int kRescanFastQueries = 65536;  // failed queries per call the fast path serves
+// Device-driven rescan (knn_select.hip): every buffer sized for `cap` fast-
+// path queries (cap <= m); the merge fills q/tau and counts cnt[0].
+struct RescanBufs {
+  int* q;                    // [m] failed queries (merge)
+  double* tau;               // [m] W-th exact distance among the re-ranked rows (+inf unknown)
+  int* cnt;                  // [2] failed queries (merge) / passed on to the full scan
+  float* qf;                 // [cap][DP] fp32 query operands of the fast path
+  float* thr;                // [cap] proxy thresholds
+  int* fcnt;                 // [cap] rows appended per query
+  int* buf;                  // [cap][kRescanCap] appended rows
+  int* slow_q;               // [m] queries for the full scan
+  int* counts;               // host-mapped {cnt[0], full scans} of the call (nullable)
+  unsigned long long* totals;  // device running sums of the same (nullable)
+};
+// Enqueues the whole rescan path (prep, filter, exact finish, full scan);
+// every kernel reads the counts on the device.  f_err: the fp32 candidate
+// error factor of t.DP; full_blocks: workgroups of the full-scan kernel.
+void launch_rescan(int metric, const TrainDev& t, const double* Q64, const RescanBufs& rb, int cap,
+                   int W, double f_err, const Sink& sink, int full_blocks, hipStream_t s);
 void launch_merge_vote_partials(const double* dist, const int64_t* idx, const int32_t* lab,
                                 int parts, int64_t m, int w, int k, int32_t* out_lab,
                                 int64_t* out_idx, double* out_dist, int32_t* out_flags,

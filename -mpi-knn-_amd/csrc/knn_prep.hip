@@ -53,23 +53,59 @@ void launch_col_mean(const double* X64, int64_t n, int d, double* partial, doubl
 
 // max |x_i - mu_i| over the train set (fp64, non-negative -> ordered as
 // u64 bits): fixes the operand scale 2^jx before any rounding to fp32.
+// Also counts the non-finite train values (exponent bits all ones: a bit
+// test, this file is built with -fno-honor-nans) into nonfinite[0] --
+// set_train rejects such a train set.
+__device__ __forceinline__ bool nonfinite_bits(double x) {
+  return (__double_as_longlong(x) & 0x7FF0000000000000ll) == 0x7FF0000000000000ll;
+}
+
 __global__ void __launch_bounds__(256)
 absmax_kernel(const double* __restrict__ X64, const double* __restrict__ mu, int64_t n, int d,
-              unsigned long long* __restrict__ out) {
+              unsigned long long* __restrict__ out, unsigned long long* __restrict__ nonfinite) {
   double m = 0.0;
+  int bad = 0;
   const int64_t total = n * d;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * 256)
-    m = fmax(m, __builtin_fabs(X64[e] - mu[e % d]));
+       e += (int64_t)gridDim.x * 256) {
+    const double x = X64[e];
+    bad += nonfinite_bits(x);
+    m = fmax(m, __builtin_fabs(x - mu[e % d]));
+  }
   m = wave_max_d(m);
-  if ((threadIdx.x & 63) == 0) atomicMax(out, (unsigned long long)__double_as_longlong(m));
+  bad = wave_sum_i(bad);
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(out, (unsigned long long)__double_as_longlong(m));
+    if (bad) atomicAdd(nonfinite, (unsigned long long)bad);
+  }
 }
 
 void launch_absmax(const double* X64, const double* mu, int64_t n, int d, unsigned long long* out,
-                   hipStream_t s) {
+                   unsigned long long* nonfinite, hipStream_t s) {
   int64_t blocks = (n * d + 255) / 256;
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(absmax_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X64, mu, n, d, out);
+  hipLaunchKernelGGL(absmax_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X64, mu, n, d, out,
+                     nonfinite);
+}
+
+// Train labels outside [0, class_cnt) (the reference indexes label_cnt[label]
+// unchecked, cpp:330): counted into bad[0], set_train rejects them.
+__global__ void __launch_bounds__(256)
+label_check_kernel(const int32_t* __restrict__ lab, int64_t n, int class_cnt,
+                   unsigned long long* __restrict__ bad) {
+  int b = 0;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256)
+    b += (lab[e] < 0 || lab[e] >= class_cnt);
+  b = wave_sum_i(b);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(bad, (unsigned long long)b);
+}
+
+void launch_label_check(const int32_t* lab, int64_t n, int class_cnt, unsigned long long* bad,
+                        hipStream_t s) {
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(label_check_kernel, dim3((unsigned)blocks), dim3(256), 0, s, lab, n, class_cnt,
+                     bad);
 }
 
 // Operand scale.  Every candidate-pass operand is 2^jx (x - mu), jx putting
@@ -138,19 +174,24 @@ void launch_prep_train(const double* X64, const double* mu, int64_t n, int d, in
 
 // Per query: valid[row] = 1 when every |scale * 2^jx (q_i - mu_i)| stays below
 // `limit` (the operand format's safe range), else 0: the query's proxies are
-// then void and the merge sends it to the exact rescan (pad rows: 1).
+// then void and the merge sends it to the exact rescan (pad rows: 1); -1
+// when a coordinate is NaN or infinite (bit test): no neighbours reported.
 __global__ void __launch_bounds__(256)
 query_check_kernel(const double* __restrict__ Q64, const double* __restrict__ mu, int64_t m, int d,
                    int64_t m_pad, double scale, int jx, double limit, float* __restrict__ valid) {
   const int lane = threadIdx.x & 63;
   const int64_t wstride = (int64_t)gridDim.x * 4;
   for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < m_pad; row += wstride) {
-    bool ok = true;
+    bool ok = true, fin = true;
     if (row < m)
-      for (int c = lane; c < d; c += 64)
-        ok = ok && __builtin_fabs(__builtin_ldexp(scale * (Q64[row * d + c] - mu[c]), jx)) < limit;
+      for (int c = lane; c < d; c += 64) {
+        const double x = Q64[row * d + c];
+        fin = fin && !nonfinite_bits(x);
+        ok = ok && __builtin_fabs(__builtin_ldexp(scale * (x - mu[c]), jx)) < limit;
+      }
     ok = __ballot(!ok) == 0;
-    if (lane == 0) valid[row] = ok ? 1.0f : 0.0f;
+    fin = __ballot(!fin) == 0;
+    if (lane == 0) valid[row] = !fin ? -1.0f : (ok ? 1.0f : 0.0f);
   }
 }
 

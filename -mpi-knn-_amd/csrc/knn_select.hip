@@ -44,6 +44,28 @@ __device__ void finish_single(int64_t q, const double* dk, const int* di, const 
   }
 }
 
+// A query with a non-finite coordinate: label -1, KNN_FLAG_NONFINITE, no
+// neighbours (idx -1, dist NaN); partial lists empty.  One wave.
+__device__ void finish_nonfinite(int64_t q, const Sink& sink) {
+  const int lane = threadIdx.x & 63;
+  if (sink.mode == MODE_SINGLE) {
+    if (lane == 0) {
+      sink.labels[q] = -1;
+      if (sink.flags) sink.flags[q] = 16;  // KNN_FLAG_NONFINITE
+    }
+    for (int t = lane; t < sink.k; t += 64) {
+      if (sink.idx) sink.idx[q * sink.k + t] = -1;
+      if (sink.dist) sink.dist[q * sink.k + t] = __longlong_as_double(0x7FF8000000000000ll);  // quiet NaN
+    }
+  } else {
+    for (int t = lane; t < sink.w; t += 64) {
+      sink.dist[q * sink.w + t] = KNN_INF_D;
+      sink.idx[q * sink.w + t] = -1;
+      sink.plab[q * sink.w + t] = -1;
+    }
+  }
+}
+
 __device__ void finish_partial(int64_t q, const double* dk, const int* di, const int* ls,
                                int cnt, int w, int64_t idx_off, const Sink& sink) {
   const int lane = threadIdx.x & 63;
@@ -193,7 +215,11 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
     q1 = wave_sum_d(q1) * (1.0 + 1e-12);
     if (METRIC == 0) E += ps.ue * 1.001 * (2.0 * q1 + t.x1max) * sinv + t.DP * ps.up * pinv;
     else E += 2.0 * ps.ue * 1.001 * t.DP * sinv;
-    const bool void_q = ps.valid && !(ps.valid[q] > 0.0f);
+    // valid: 1 usable, 0 operands out of the format's range (exact rescan),
+    // -1 a non-finite input value (no neighbours are reported)
+    const float vq = ps.valid ? ps.valid[q] : 1.0f;
+    const bool void_q = !(vq > 0.0f);
+    const bool nonfinite = vq < 0.0f;
     // union in registers; min over full lists of their R-th (worst kept) entry
     const float* lv = cv + q * U;
     const int* li = ci + q * U;
@@ -281,7 +307,8 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
       tq = key2f(max(max(g[0], g[1]), max(g[2], g[3])));
     }
     if (lane == 0) {
-      s_cn = void_q ? Cmax + 1 : cn;  // void proxies: exact rescan below
+      // void proxies: exact rescan below; non-finite query: no neighbours
+      s_cn = nonfinite ? -1 : (void_q ? Cmax + 1 : cn);
       s_lb = (double)fminf(fminf(lbx, mlr), tq) * pinv;
       s_qa = qa;
       s_e = E;
@@ -289,6 +316,10 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
   }
   __syncthreads();
   const int cn = s_cn;
+  if (cn < 0) {  // a NaN / inf coordinate: the reference's distances are undefined
+    if (tid < 64) finish_nonfinite(q, sink);
+    return;
+  }
   if (cn > Cmax) {  // void proxies (the window overflow is handled above): exact rescan
     if (tid == 0) {
       const int f = atomicAdd(rescan_cnt, 1);
@@ -305,9 +336,10 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
   if (tid == 0) {
     const double LB = s_lb;
     bool cert;
-    if (!(LB < KNN_INF_D)) {
+    if (cn < W) {
+      cert = false;  // fewer rows than the top W re-ranked (e.g. non-finite proxies)
+    } else if (!(LB < KNN_INF_D)) {
       cert = true;  // nothing was left out: every row was re-ranked exactly
-    } else if (cn < W) {
       cert = false;
     } else {
       const double dw = dk[W - 1], qa = s_qa, E = s_e;
@@ -376,327 +408,436 @@ void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int
 #undef KNN_MR
 }
 
-// ------------------------------------------------- fast rescan (filtered)
+// ------------------------------------------------- rescan (device-driven)
 // Queries whose candidate set was not certified (a list overflowed near the
-// top, heavy ties).  tau = the W-th exact distance among the query's
-// re-ranked rows, >= the true W-th.  rescan_filter streams the fp32 train
-// copy once per 4 or 16 such queries (lane = train row, queries broadcast
-// from LDS) and appends every row whose centred fp32 proxy --
-// an fmaf chain with the candidate pass's certified error bound -- is within
-// reach of tau; the appended set therefore holds every row with exact
-// distance <= tau, i.e. the exact top-W with all its ties.  rescan_finish
-// re-ranks it exactly.  Unknown tau or more than kRescanCap rows: the full
-// exact scan below.
+// top, heavy ties, operands out of the candidate format's range).  The
+// whole path is enqueued on every call and sized on the device: the merge
+// counts the failed queries in cnt[0] (their ids in rescan_q, their bound in
+// rescan_tau); every kernel below reads the counts itself and exits at once
+// when there is nothing to do, so a classify call never waits for the host.
+//
+//  1. fast path, for the first `cap` failed queries: tau = the W-th exact
+//     distance among the query's re-ranked rows (>= the true W-th).
+//     rescan_filter streams the fp32 train copy (lane = train row; queries
+//     broadcast from LDS) and appends every row whose centred fp32 proxy --
+//     an fmaf chain with the candidate pass's certified error bound -- is
+//     within reach of tau; the appended set therefore holds every row with
+//     exact distance <= tau, i.e. the exact top-W with all its ties.
+//     rescan_finish_fast re-ranks it exactly.
+//  2. full scan, for the queries the fast path cannot finish (tau unknown,
+//     more than kRescanCap rows within reach, or failed queries beyond
+//     `cap`): one 1024-thread workgroup per query computes every row's exact
+//     distance and keeps the top W by (dist, idx) with a threshold-filtered
+//     LDS buffer.
 
-// Block = NWB waves, wave w owns the 64 consecutive train rows starting at
-// blockIdx.x*64*NWB + 64w (lane = row).  The wave copies its rows (the
-// padded fp32 X32 layout, odd 16-B stride -> conflict-free ds_read_b128) into
-// LDS by LDS-DMA, then runs kFiltQ accumulators per lane against the block's
-// queries, read as LDS broadcasts.
 // One wave per failed query: the centred fp32 query row (x -2 for L2, the
 // candidate pass's operand) and the proxy threshold every row with exact
 // distance <= tau passes (fp32 fmaf-chain error bound f_err of t.DP).
 template <int METRIC>
 __global__ void __launch_bounds__(64)
 rescan_prep_kernel(TrainDev t, const double* __restrict__ Q64, const int* __restrict__ rescan_q,
-                   const double* __restrict__ tau, int f0, double f_err, float* __restrict__ qf,
-                   float* __restrict__ thr) {
-  const int s = blockIdx.x, lane = threadIdx.x, d = t.d, DP = t.DP;
-  const double* qr = Q64 + (int64_t)rescan_q[f0 + s] * d;
-  double qa = 0.0, q1 = 0.0;
-  for (int i = lane; i < DP; i += 64) {
-    float v = 0.0f;
-    if (i < d) {
-      const double x = qr[i] - t.mu[i];
-      qa += METRIC == 0 ? x * x : __builtin_fabs(x);
-      q1 += __builtin_fabs(x);
-      v = (float)__builtin_ldexp(x * (METRIC == 0 ? -2.0 : 1.0), t.jx);  // X32's scale
+                   const double* __restrict__ tau, const int* __restrict__ cnt, int cap,
+                   double f_err, float* __restrict__ qf, float* __restrict__ thr,
+                   int* __restrict__ fcnt) {
+  const int nf = min(cnt[0], cap);
+  const int lane = threadIdx.x, d = t.d, DP = t.DP;
+  for (int s = blockIdx.x; s < nf; s += gridDim.x) {
+    const double* qr = Q64 + (int64_t)rescan_q[s] * d;
+    double qa = 0.0, q1 = 0.0;
+    for (int i = lane; i < DP; i += 64) {
+      float v = 0.0f;
+      if (i < d) {
+        const double x = qr[i] - t.mu[i];
+        qa += METRIC == 0 ? x * x : __builtin_fabs(x);
+        q1 += __builtin_fabs(x);
+        v = (float)__builtin_ldexp(x * (METRIC == 0 ? -2.0 : 1.0), t.jx);  // X32's scale
+      }
+      qf[(int64_t)s * DP + i] = v;
     }
-    qf[(int64_t)s * DP + i] = v;
-  }
-  qa = wave_sum_d(qa) * (1.0 + 1e-12);
-  q1 = wave_sum_d(q1) * (1.0 + 1e-12);
-  if (lane == 0) {
-    const double tq = tau[f0 + s];
-    const double sinv = __builtin_ldexp(1.0, -t.jx);
-    double T;
-    // unscaled threshold (+ the fp32 absolute terms of the merge), then
-    // scaled to the proxies' units
-    if (METRIC == 0) {
-      const double E = f_err * (t.x2max + 2.1 * __builtin_sqrt(qa) * __builtin_sqrt(t.x2max)) +
-                       0x1p-125 * 1.001 * (2.0 * q1 + t.x1max) * sinv +
-                       DP * 0x1p-124 * sinv * sinv + 1e-300;
-      T = __builtin_ldexp(tq * tq * (1.0 + 1e-12) - qa * (1.0 - 2e-12) + E, 2 * t.jx);
-    } else {
-      const double E = f_err * (qa + t.x1max) + 2.0 * 0x1p-125 * 1.001 * DP * sinv + 1e-300;
-      T = __builtin_ldexp(tq * (1.0 + 1e-12) + E, t.jx);
+    qa = wave_sum_d(qa) * (1.0 + 1e-12);
+    q1 = wave_sum_d(q1) * (1.0 + 1e-12);
+    if (lane == 0) {
+      const double tq = tau[s];
+      const double sinv = __builtin_ldexp(1.0, -t.jx);
+      double T;
+      // unscaled threshold (+ the fp32 absolute terms of the merge), then
+      // scaled to the proxies' units
+      if (METRIC == 0) {
+        const double E = f_err * (t.x2max + 2.1 * __builtin_sqrt(qa) * __builtin_sqrt(t.x2max)) +
+                         0x1p-125 * 1.001 * (2.0 * q1 + t.x1max) * sinv +
+                         DP * 0x1p-124 * sinv * sinv + 1e-300;
+        T = __builtin_ldexp(tq * tq * (1.0 + 1e-12) - qa * (1.0 - 2e-12) + E, 2 * t.jx);
+      } else {
+        const double E = f_err * (qa + t.x1max) + 2.0 * 0x1p-125 * 1.001 * DP * sinv + 1e-300;
+        T = __builtin_ldexp(tq * (1.0 + 1e-12) + E, t.jx);
+      }
+      // round T up to a float (the order-preserving key's successor is the next float up)
+      float tf = (float)T;
+      if ((double)tf < T && tf < KNN_INF_F) tf = key2f(f2key(tf) + 1u);
+      thr[s] = tq < KNN_INF_D ? tf : -KNN_INF_F;  // unknown tau: nothing passes, full scan
+      fcnt[s] = 0;
     }
-    // round T up to a float (the order-preserving key's successor is the next float up)
-    float tf = (float)T;
-    if ((double)tf < T && tf < KNN_INF_F) tf = key2f(f2key(tf) + 1u);
-    thr[s] = tq < KNN_INF_D ? tf : -KNN_INF_F;  // unknown tau: nothing passes, full scan
   }
 }
 
-template <int METRIC, int kFiltQ>  // kFiltQ: failed queries per block (LDS broadcasts)
+// Appends row `row` to query s's list if its proxy passes.
+__device__ __forceinline__ void rescan_append(float acc, float th, int s, int64_t row,
+                                              int* __restrict__ fcnt, int* __restrict__ buf) {
+  if (acc <= th) {
+    const int pos = atomicAdd(&fcnt[s], 1);
+    if (pos < kRescanCap) buf[(int64_t)s * kRescanCap + pos] = (int)row;
+  }
+}
+
+// DP <= 256: block = NWB waves, wave w owns the 64 consecutive train rows
+// starting at blockIdx.x*64*NWB + 64w (lane = row), copied once into LDS by
+// LDS-DMA (the padded X32 layout, odd 16-B stride -> conflict-free
+// ds_read_b128) and reused for every group of FQ failed queries.
+template <int METRIC, int FQ>
 __global__ void __launch_bounds__(256)
 rescan_filter_kernel(TrainDev t, const float* __restrict__ qf, const float* __restrict__ thr,
-                     int nf, int* __restrict__ cnt, int* __restrict__ buf) {
+                     const int* __restrict__ cnt, int cap, int* __restrict__ fcnt,
+                     int* __restrict__ buf) {
+  const int nf = min(cnt[0], cap);
+  if (nf == 0) return;
   extern __shared__ __attribute__((aligned(16))) float fsm[];
   const int DP = t.DP, RSF = DP + 4;
   const int NWB = blockDim.x >> 6;
-  float* qs = fsm;                          // [kFiltQ][DP] centred queries (x -2 for L2)
-  float* thr_s = qs + kFiltQ * DP;          // [kFiltQ] proxy thresholds
-  float* rows = thr_s + kFiltQ;             // [NWB][64][RSF]
-  __shared__ int s_dummy;
-  (void)s_dummy;
-  const int g0 = blockIdx.y * kFiltQ;
-  const int nfg = min(kFiltQ, nf - g0);
+  float* qs = fsm;                          // [FQ][DP] centred queries (x -2 for L2)
+  float* thr_s = qs + FQ * DP;              // [FQ] proxy thresholds
+  float* rows = thr_s + FQ;                 // [NWB][64][RSF]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t row0 = ((int64_t)blockIdx.x * NWB + wv) * 64;
   const bool active = row0 < t.n_pad;
 
-  // this wave's 64 rows -> LDS (X32 carries 1 KiB of slack past the last row)
   float* my_rows = rows + (size_t)wv * 64 * RSF;
-  if (active) {
+  if (active) {  // X32 carries 1 KiB of slack past the last row
     const int bytes = 64 * RSF * 4;
     const char* src = (const char*)(t.X32 + row0 * RSF) + lane * 16;
     const uint32_t dst = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)my_rows;
     for (int p = 0; p * 1024 < bytes; ++p) glds16(src + p * 1024, dst + p * 1024);
   }
-  for (int e = tid; e < kFiltQ * DP; e += blockDim.x) {
-    const int qi = e / DP;
-    qs[e] = qi < nfg ? qf[(int64_t)g0 * DP + e] : 0.0f;
-  }
-  if (tid < kFiltQ) thr_s[tid] = tid < nfg ? thr[g0 + tid] : -KNN_INF_F;  // absent: no row passes
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (!active) return;
-
   const float* xr = my_rows + lane * RSF;
-  const float seed = xr[METRIC == 0 ? DP : DP + 1];  // +inf on pad rows: never passes
-  float acc[kFiltQ];
-#pragma unroll
-  for (int qi = 0; qi < kFiltQ; ++qi) acc[qi] = seed;
-  for (int c = 0; c < DP / 4; ++c) {
-    const float4 x4 = *(const float4*)(xr + 4 * c);
-#pragma unroll
-    for (int qi = 0; qi < kFiltQ; ++qi) {
-      const float4 q4 = *(const float4*)(qs + qi * DP + 4 * c);
-      float a = acc[qi];
-      if (METRIC == 0) {  // the candidate pass's fp32 model: an fmaf chain
-        a = __builtin_fmaf(q4.x, x4.x, a);
-        a = __builtin_fmaf(q4.y, x4.y, a);
-        a = __builtin_fmaf(q4.z, x4.z, a);
-        a = __builtin_fmaf(q4.w, x4.w, a);
-      } else {
-        a = a + __builtin_fabsf(q4.x - x4.x);
-        a = a + __builtin_fabsf(q4.y - x4.y);
-        a = a + __builtin_fabsf(q4.z - x4.z);
-        a = a + __builtin_fabsf(q4.w - x4.w);
-      }
-      acc[qi] = a;
+  for (int g0 = 0; g0 < nf; g0 += FQ) {
+    const int nfg = min(FQ, nf - g0);
+    __syncthreads();  // the previous group's reads of qs are done
+    for (int e = tid; e < FQ * DP; e += blockDim.x) {
+      const int qi = e / DP;
+      qs[e] = qi < nfg ? qf[(int64_t)g0 * DP + e] : 0.0f;
     }
-  }
+    if (tid < FQ) thr_s[tid] = tid < nfg ? thr[g0 + tid] : -KNN_INF_F;  // absent: no row passes
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (active) {
+      const float seed = xr[METRIC == 0 ? DP : DP + 1];  // +inf on pad rows: never passes
+      float acc[FQ];
 #pragma unroll
-  for (int qi = 0; qi < kFiltQ; ++qi) {
-    if (acc[qi] <= thr_s[qi]) {
-      const int pos = atomicAdd(&cnt[g0 + qi], 1);
-      if (pos < kRescanCap) buf[(int64_t)(g0 + qi) * kRescanCap + pos] = (int)(row0 + lane);
+      for (int qi = 0; qi < FQ; ++qi) acc[qi] = seed;
+      for (int c = 0; c < DP / 4; ++c) {
+        const float4 x4 = *(const float4*)(xr + 4 * c);
+#pragma unroll
+        for (int qi = 0; qi < FQ; ++qi) {
+          const float4 q4 = *(const float4*)(qs + qi * DP + 4 * c);
+          float a = acc[qi];
+          if (METRIC == 0) {  // the candidate pass's fp32 model: an fmaf chain
+            a = __builtin_fmaf(q4.x, x4.x, a);
+            a = __builtin_fmaf(q4.y, x4.y, a);
+            a = __builtin_fmaf(q4.z, x4.z, a);
+            a = __builtin_fmaf(q4.w, x4.w, a);
+          } else {
+            a = a + __builtin_fabsf(q4.x - x4.x);
+            a = a + __builtin_fabsf(q4.y - x4.y);
+            a = a + __builtin_fabsf(q4.z - x4.z);
+            a = a + __builtin_fabsf(q4.w - x4.w);
+          }
+          acc[qi] = a;
+        }
+      }
+#pragma unroll
+      for (int qi = 0; qi < FQ; ++qi)
+        if (qi < nfg) rescan_append(acc[qi], thr_s[qi], g0 + qi, row0 + lane, fcnt, buf);
     }
   }
 }
 
-// One block per fast-rescanned query: exact re-rank of its appended rows.
+// DP > 256 (rows too long to stage 64 per wave): lane = train row, read in
+// place from X32 (each lane walks its own row in 16-B steps; the lines it
+// touches are reused from L1/L2 by its next loads), queries from LDS.
+template <int METRIC, int FQ>
+__global__ void __launch_bounds__(256)
+rescan_filter_wide_kernel(TrainDev t, const float* __restrict__ qf, const float* __restrict__ thr,
+                          const int* __restrict__ cnt, int cap, int* __restrict__ fcnt,
+                          int* __restrict__ buf) {
+  const int nf = min(cnt[0], cap);
+  if (nf == 0) return;
+  extern __shared__ __attribute__((aligned(16))) float fsm[];
+  const int DP = t.DP, RSF = DP + 4;
+  float* qs = fsm;             // [FQ][DP]
+  float* thr_s = qs + FQ * DP; // [FQ]
+  const int tid = threadIdx.x;
+  const int64_t row = (int64_t)blockIdx.x * blockDim.x + tid;
+  const bool active = row < t.n_pad;
+  const float* xr = t.X32 + (active ? row : 0) * RSF;
+  for (int g0 = 0; g0 < nf; g0 += FQ) {
+    const int nfg = min(FQ, nf - g0);
+    __syncthreads();
+    for (int e = tid; e < FQ * DP; e += blockDim.x) {
+      const int qi = e / DP;
+      qs[e] = qi < nfg ? qf[(int64_t)g0 * DP + e] : 0.0f;
+    }
+    if (tid < FQ) thr_s[tid] = tid < nfg ? thr[g0 + tid] : -KNN_INF_F;
+    __syncthreads();
+    if (active) {
+      const float seed = xr[METRIC == 0 ? DP : DP + 1];
+      float acc[FQ];
+#pragma unroll
+      for (int qi = 0; qi < FQ; ++qi) acc[qi] = seed;
+      for (int c = 0; c < DP / 4; ++c) {
+        const float4 x4 = *(const float4*)(xr + 4 * c);
+#pragma unroll
+        for (int qi = 0; qi < FQ; ++qi) {
+          const float4 q4 = *(const float4*)(qs + qi * DP + 4 * c);
+          float a = acc[qi];
+          if (METRIC == 0) {
+            a = __builtin_fmaf(q4.x, x4.x, a);
+            a = __builtin_fmaf(q4.y, x4.y, a);
+            a = __builtin_fmaf(q4.z, x4.z, a);
+            a = __builtin_fmaf(q4.w, x4.w, a);
+          } else {
+            a = a + __builtin_fabsf(q4.x - x4.x);
+            a = a + __builtin_fabsf(q4.y - x4.y);
+            a = a + __builtin_fabsf(q4.z - x4.z);
+            a = a + __builtin_fabsf(q4.w - x4.w);
+          }
+          acc[qi] = a;
+        }
+      }
+#pragma unroll
+      for (int qi = 0; qi < FQ; ++qi)
+        if (qi < nfg) rescan_append(acc[qi], thr_s[qi], g0 + qi, row, fcnt, buf);
+    }
+  }
+}
+
+// Exact re-rank of each fast-rescanned query's appended rows (a loop over
+// the failed queries; the block's LDS is reused).  Queries it cannot finish
+// are appended to slow_q (count cnt[1]) for the full scan.
 // Dynamic LDS: qv[d] | dk[kRescanCap] | tb[NT][17] | di[kRescanCap] | ls[kRescanCap].
 template <int METRIC, int NT>
 __global__ void __launch_bounds__(NT)
 rescan_finish_fast_kernel(TrainDev t, const double* __restrict__ Q64,
-                          const int* __restrict__ rescan_q, const double* __restrict__ tau, int f0,
-                          int W, const int* __restrict__ cnt, const int* __restrict__ buf,
-                          Sink sink, int* __restrict__ slow_q, int* __restrict__ slow_cnt) {
+                          const int* __restrict__ rescan_q, const double* __restrict__ tau,
+                          int* __restrict__ cnt, int cap, int W, const int* __restrict__ fcnt,
+                          const int* __restrict__ buf, Sink sink, int* __restrict__ slow_q) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int nf = min(cnt[0], cap);
   const int d = t.d;
   const bool q_in_lds = d <= 1024;  // keeps the block's LDS under 64 KiB
   double* dk = (double*)smem + (q_in_lds ? d : 0);
   double* tb = dk + kRescanCap;
   int* di = (int*)(tb + NT * 17);
   int* ls = di + kRescanCap;
-  const int s = blockIdx.x, tid = threadIdx.x;
-  const int64_t q = rescan_q[f0 + s];
-  const int c = cnt[s];
+  const int tid = threadIdx.x;
   const int need_rows = (int)min((int64_t)W, t.n);
-  if (!(tau[f0 + s] < KNN_INF_D) || c > kRescanCap || c < need_rows) {
-    if (tid == 0) slow_q[atomicAdd(slow_cnt, 1)] = (int)q;
-    return;
-  }
-  const double* qrow = Q64 + q * d;
-  const double* qv = q_in_lds ? (const double*)smem : qrow;
-  if (q_in_lds)
-    for (int i = tid; i < d; i += NT) ((double*)smem)[i] = qrow[i];
-  for (int i = tid; i < c; i += NT) di[i] = buf[(int64_t)s * kRescanCap + i];
-  __syncthreads();
-  int C2 = 1;
-  while (C2 < c) C2 <<= 1;
-  exact_sorted<METRIC, NT>(t, qv, di, dk, tb, c, C2, tid);
-  const int need = sink.mode == MODE_SINGLE ? sink.k : sink.w;
-  for (int i = tid; i < need && i < c; i += NT) ls[i] = t.lab[di[i]];
-  __syncthreads();
-  if (tid < 64) {
-    if (sink.mode == MODE_SINGLE)
-      finish_single(q, dk, di, ls, c, sink.k, sink.idx_off, 1 /*KNN_FLAG_EXACT_RESCAN*/, sink);
-    else
-      finish_partial(q, dk, di, ls, c, sink.w, sink.idx_off, sink);
-  }
-}
-
-void launch_rescan_fast(int metric, const TrainDev& t, const double* Q64, const int* rescan_q,
-                        const double* tau, int f0, int nf, int W, double f_err, float* qf,
-                        float* thr, int* cnt, int* buf, const Sink& sink, int* slow_q,
-                        int* slow_cnt, hipStream_t s) {
-  if (nf <= 0) return;
-  if (metric == 0)
-    hipLaunchKernelGGL(rescan_prep_kernel<0>, dim3((unsigned)nf), dim3(64), 0, s, t, Q64,
-                       rescan_q, tau, f0, f_err, qf, thr);
-  else
-    hipLaunchKernelGGL(rescan_prep_kernel<1>, dim3((unsigned)nf), dim3(64), 0, s, t, Q64,
-                       rescan_q, tau, f0, f_err, qf, thr);
-  // queries per block: 4 for a handful of failed queries (list overflows),
-  // else 16; waves per block: as many 64-row tiles as fit in ~150 KiB
-  const int fq = nf <= 4 ? 4 : 16;
-  const size_t tile = (size_t)64 * (t.DP + 4) * 4, qbytes = (size_t)fq * (t.DP + 1) * 4;
-  const int nwb = (int)std::max<size_t>(1, std::min<size_t>(4, (150 * 1024 - qbytes) / tile));
-  const int64_t rpb = 64 * nwb;
-  const dim3 fg((unsigned)((t.n_pad + rpb - 1) / rpb), (unsigned)((nf + fq - 1) / fq));
-  const size_t flds = qbytes + nwb * tile;
-#define KNN_FILT(M_, Q_)                                                                      \
-  hipLaunchKernelGGL((rescan_filter_kernel<M_, Q_>), fg, dim3(64 * nwb), flds, s, t, qf, thr, nf, \
-                     cnt, buf)
-  if (metric == 0) {
-    if (fq == 4) KNN_FILT(0, 4); else KNN_FILT(0, 16);
-  } else {
-    if (fq == 4) KNN_FILT(1, 4); else KNN_FILT(1, 16);
-  }
-#undef KNN_FILT
-  const size_t lds = (size_t)(t.d <= 1024 ? t.d : 0) * 8 + (size_t)kRescanCap * 8 +
-                     (size_t)256 * 17 * 8 + (size_t)kRescanCap * 8;
-  if (metric == 0)
-    hipLaunchKernelGGL((rescan_finish_fast_kernel<0, 256>), dim3((unsigned)nf), dim3(256), lds, s,
-                       t, Q64, rescan_q, tau, f0, W, cnt, buf, sink, slow_q, slow_cnt);
-  else
-    hipLaunchKernelGGL((rescan_finish_fast_kernel<1, 256>), dim3((unsigned)nf), dim3(256), lds, s,
-                       t, Q64, rescan_q, tau, f0, W, cnt, buf, sink, slow_q, slow_cnt);
-}
-
-// ------------------------------------------------------ exact rescan path
-// Queries whose candidate set is not certified (near-duplicate clusters,
-// large exact-tie groups, adversarial row orders) are re-done exactly:
-// every row's fp64 reference distance, kSortN rows per block sorted in LDS,
-// the best W per block kept, then lists reduced by the same sort until one
-// remains.  Rare by construction; correctness path, not the fast path.
-template <int METRIC>
-__global__ void __launch_bounds__(256)
-rescan_chunk_kernel(TrainDev t, const double* __restrict__ Q64, const int* __restrict__ rescan_q,
-                    int f0, int W, int n_chunks, double* __restrict__ pk, int* __restrict__ pi) {
-  __shared__ double sk[kSortN];
-  __shared__ int si[kSortN];
-  const int chunk = blockIdx.x;
-  const int64_t q = rescan_q[f0 + blockIdx.y];
-  const double* qrow = Q64 + q * t.d;
-  for (int e = threadIdx.x; e < kSortN; e += 256) {
-    const int64_t row = (int64_t)chunk * kSortN + e;
-    double v = KNN_INF_D;
-    int id = INT_MAX;
-    if (row < t.n) {
-      v = exact_dist<METRIC>(qrow, t.X64 + row * t.d, t.d);
-      id = (int)row;
+  for (int s = blockIdx.x; s < nf; s += gridDim.x) {
+    __syncthreads();  // the previous query's LDS reads are done
+    const int64_t q = rescan_q[s];
+    const int c = fcnt[s];
+    if (!(tau[s] < KNN_INF_D) || c > kRescanCap || c < need_rows) {
+      if (tid == 0) slow_q[atomicAdd(&cnt[1], 1)] = (int)q;
+      continue;
     }
-    sk[e] = v;
-    si[e] = id;
-  }
-  bitonic_sort_lds(sk, si, kSortN, threadIdx.x, 256);
-  const int64_t o = ((int64_t)blockIdx.y * n_chunks + chunk) * W;
-  for (int e = threadIdx.x; e < W; e += 256) {
-    pk[o + e] = sk[e];
-    pi[o + e] = si[e];
-  }
-}
-
-__global__ void __launch_bounds__(256)
-rescan_reduce_kernel(const double* __restrict__ ik, const int* __restrict__ ii, int P, int W,
-                     int G, double* __restrict__ ok, int* __restrict__ oi, int P2) {
-  __shared__ double sk[kSortN];
-  __shared__ int si[kSortN];
-  const int b = blockIdx.x, f = blockIdx.y;
-  const int l0 = b * G, l1 = min(P, l0 + G);
-  const int ne = (l1 - l0) * W;
-  const int64_t src = ((int64_t)f * P + l0) * W;
-  for (int e = threadIdx.x; e < kSortN; e += 256) {
-    sk[e] = e < ne ? ik[src + e] : KNN_INF_D;
-    si[e] = e < ne ? ii[src + e] : INT_MAX;
-  }
-  bitonic_sort_lds(sk, si, kSortN, threadIdx.x, 256);
-  const int64_t o = ((int64_t)f * P2 + b) * W;
-  for (int e = threadIdx.x; e < W; e += 256) {
-    ok[o + e] = sk[e];
-    oi[o + e] = si[e];
+    const double* qrow = Q64 + q * d;
+    const double* qv = q_in_lds ? (const double*)smem : qrow;
+    if (q_in_lds)
+      for (int i = tid; i < d; i += NT) ((double*)smem)[i] = qrow[i];
+    for (int i = tid; i < c; i += NT) di[i] = buf[(int64_t)s * kRescanCap + i];
+    __syncthreads();
+    int C2 = 1;
+    while (C2 < c) C2 <<= 1;
+    exact_sorted<METRIC, NT>(t, qv, di, dk, tb, c, C2, tid);
+    const int need = sink.mode == MODE_SINGLE ? sink.k : sink.w;
+    for (int i = tid; i < need && i < c; i += NT) ls[i] = t.lab[di[i]];
+    __syncthreads();
+    if (tid < 64) {
+      if (sink.mode == MODE_SINGLE)
+        finish_single(q, dk, di, ls, c, sink.k, sink.idx_off, 1 /*KNN_FLAG_EXACT_RESCAN*/, sink);
+      else
+        finish_partial(q, dk, di, ls, c, sink.w, sink.idx_off, sink);
+    }
   }
 }
 
-__global__ void __launch_bounds__(64)
-rescan_finish_kernel(TrainDev t, const double* __restrict__ pk, const int* __restrict__ pi,
-                     const int* __restrict__ rescan_q, int f0, int W, Sink sink) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  double* dk = (double*)smem;
-  int* di = (int*)(dk + W);
-  int* ls = di + W;
-  const int f = blockIdx.x;
-  const int64_t q = rescan_q[f0 + f];
-  const int lane = threadIdx.x;
-  const int cnt = (int)(t.n < W ? t.n : W);
-  for (int e = lane; e < W; e += 64) {
-    dk[e] = pk[(int64_t)f * W + e];
-    di[e] = pi[(int64_t)f * W + e];
-    ls[e] = e < cnt ? t.lab[di[e]] : -1;
+// Full exact scan: one 1024-thread workgroup per query (a loop over the
+// queries the fast path passed on, then the failed queries beyond `cap`).
+// Each wave takes 64 rows per step: coalesced 64-B row pieces (8 lanes per
+// row) go into the wave's own LDS tile as squared (L1: absolute)
+// differences, and lane r adds its row's terms in dimension order -- the
+// reference's operation order -- with no workgroup barrier inside the
+// row's dimensions.  Rows with distance <= tau (the current W-th) are
+// appended to an LDS buffer that holds the running top W in its first W
+// slots; when it cannot take another step it is sorted by (dist, idx) and
+// cut back to W.
+// counts (host-mapped, nullable): {failed queries, full scans} of this call;
+// totals (device): running sums of the same.
+constexpr int kFullN = 4096;    // LDS candidate buffer (entries)
+constexpr int kFullDC = 8;      // dims per staged row piece (64 B)
+constexpr int kFullThreads = 1024;
+template <int METRIC>
+__global__ void __launch_bounds__(kFullThreads)
+rescan_full_kernel(TrainDev t, const double* __restrict__ Q64, const int* __restrict__ rescan_q,
+                   const int* __restrict__ cnt, int cap, const int* __restrict__ slow_q, int W,
+                   Sink sink, int* __restrict__ counts, unsigned long long* __restrict__ totals) {
+  __shared__ double sk[kFullN];
+  __shared__ int si[kFullN];
+  __shared__ double tiles[kFullThreads / 64][64 * (kFullDC + 1)];
+  __shared__ int ls[kMaxK + 1];
+  __shared__ int s_nb;
+  __shared__ double s_tau;
+  const int nslow = cnt[1];
+  const int nover = max(0, cnt[0] - cap);
+  const int total = nslow + nover;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (blockIdx.x == 0 && tid == 0) {
+    if (counts) {
+      counts[0] = cnt[0];
+      counts[1] = total;
+    }
+    if (totals) {
+      atomicAdd(&totals[0], (unsigned long long)cnt[0]);
+      atomicAdd(&totals[1], (unsigned long long)total);
+    }
   }
-  __syncthreads();
-  if (sink.mode == MODE_SINGLE)
-    finish_single(q, dk, di, ls, cnt, sink.k, sink.idx_off, 1 /*KNN_FLAG_EXACT_RESCAN*/, sink);
-  else
-    finish_partial(q, dk, di, ls, cnt, sink.w, sink.idx_off, sink);
+  const int d = t.d;
+  const int64_t n = t.n;
+  double* tb = tiles[wv];
+  for (int f = blockIdx.x; f < total; f += gridDim.x) {
+    const int64_t q = f < nslow ? slow_q[f] : rescan_q[cap + f - nslow];
+    const double* qrow = Q64 + q * d;
+    __syncthreads();  // the previous query's LDS reads are done
+    for (int e = tid; e < W; e += kFullThreads) {
+      sk[e] = KNN_INF_D;
+      si[e] = INT_MAX;
+    }
+    if (tid == 0) {
+      s_nb = W;
+      s_tau = KNN_INF_D;
+    }
+    __syncthreads();
+    for (int64_t s0 = 0; s0 < n; s0 += kFullThreads) {
+      const int64_t r0 = s0 + wv * 64;  // this wave's 64 rows
+      const int nr = (int)max((int64_t)0, min((int64_t)64, n - r0));
+      double r = 0.0;
+      for (int c0 = 0; c0 < d && nr > 0; c0 += kFullDC) {
+        const int nd = min(kFullDC, d - c0);
+#pragma unroll
+        for (int i = 0; i < kFullDC; ++i) {
+          const int e = lane + 64 * i, rr = e / kFullDC, j = e % kFullDC;
+          double val = 0.0;
+          if (rr < nr && j < nd) {
+            const double tq = qrow[c0 + j] - t.X64[(r0 + rr) * d + c0 + j];
+            val = METRIC == 0 ? tq * tq : __builtin_fabs(tq);
+          }
+          tb[rr * (kFullDC + 1) + j] = val;
+        }
+        // the wave's own tile: LDS operations of one wave complete in order
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (lane < nr) {
+          const double* row = tb + lane * (kFullDC + 1);
+          for (int j = 0; j < nd; ++j) r = r + row[j];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
+      if (lane < nr) {
+        const double dd = METRIC == 0 ? __builtin_sqrt(r) : r;
+        if (dd <= s_tau) {
+          const int pos = atomicAdd(&s_nb, 1);
+          sk[pos] = dd;  // pos < kFullN: at most kFullThreads appends per step and
+          si[pos] = (int)(r0 + lane);  // the buffer is cut back below kFullN - kFullThreads
+        }
+      }
+      __syncthreads();
+      const int nb = s_nb;
+      if (nb > kFullN - kFullThreads || s0 + kFullThreads >= n) {
+        for (int e = nb + tid; e < kFullN; e += kFullThreads) {
+          sk[e] = KNN_INF_D;
+          si[e] = INT_MAX;
+        }
+        bitonic_sort_lds(sk, si, kFullN, tid, kFullThreads);
+        if (tid == 0) {
+          s_nb = W;
+          s_tau = sk[W - 1];
+        }
+        __syncthreads();
+      }
+    }
+    const int cntq = (int)min((int64_t)W, n);
+    const int need = sink.mode == MODE_SINGLE ? sink.k : sink.w;
+    for (int i = tid; i < need && i < cntq; i += kFullThreads) ls[i] = t.lab[si[i]];
+    __syncthreads();
+    if (tid < 64) {
+      if (sink.mode == MODE_SINGLE)
+        finish_single(q, sk, si, ls, cntq, sink.k, sink.idx_off, 1 /*KNN_FLAG_EXACT_RESCAN*/, sink);
+      else
+        finish_partial(q, sk, si, ls, cntq, sink.w, sink.idx_off, sink);
+    }
+  }
 }
 
-size_t rescan_scratch_entries(int64_t n, int W) {
-  const int64_t n_chunks = (n + kSortN - 1) / kSortN;
-  return (size_t)n_chunks * W;
-}
-
-void launch_rescan(int metric, const TrainDev& t, const double* Q64, const int* rescan_q,
-                   int f0, int nf, int W, double* pa_k, int* pa_i, double* pb_k, int* pb_i,
-                   const Sink& sink, hipStream_t s) {
-  const int n_chunks = (int)((t.n + kSortN - 1) / kSortN);
+void launch_rescan(int metric, const TrainDev& t, const double* Q64, const RescanBufs& rb, int cap,
+                   int W, double f_err, const Sink& sink, int full_blocks, hipStream_t s) {
+  if (cap > 0) {
+    const int gp = std::min(cap, 256);
+    if (metric == 0)
+      hipLaunchKernelGGL(rescan_prep_kernel<0>, dim3(gp), dim3(64), 0, s, t, Q64, rb.q, rb.tau,
+                         rb.cnt, cap, f_err, rb.qf, rb.thr, rb.fcnt);
+    else
+      hipLaunchKernelGGL(rescan_prep_kernel<1>, dim3(gp), dim3(64), 0, s, t, Q64, rb.q, rb.tau,
+                         rb.cnt, cap, f_err, rb.qf, rb.thr, rb.fcnt);
+    constexpr int FQ = 16;
+    const size_t qbytes = (size_t)FQ * (t.DP + 1) * 4;
+    if (t.DP <= kRescanStageMaxDP) {
+      // waves per block: as many 64-row tiles as fit beside the queries in ~150 KiB
+      const size_t tile = (size_t)64 * (t.DP + 4) * 4;
+      const int nwb = (int)std::max<size_t>(1, std::min<size_t>(4, (150 * 1024 - qbytes) / tile));
+      const int64_t rpb = 64 * nwb;
+      const dim3 fg((unsigned)((t.n_pad + rpb - 1) / rpb));
+      const size_t flds = qbytes + nwb * tile;
+      if (metric == 0)
+        hipLaunchKernelGGL((rescan_filter_kernel<0, FQ>), fg, dim3(64 * nwb), flds, s, t, rb.qf,
+                           rb.thr, rb.cnt, cap, rb.fcnt, rb.buf);
+      else
+        hipLaunchKernelGGL((rescan_filter_kernel<1, FQ>), fg, dim3(64 * nwb), flds, s, t, rb.qf,
+                           rb.thr, rb.cnt, cap, rb.fcnt, rb.buf);
+    } else {
+      const dim3 fg((unsigned)((t.n_pad + 255) / 256));
+      if (metric == 0)
+        hipLaunchKernelGGL((rescan_filter_wide_kernel<0, FQ>), fg, dim3(256), qbytes, s, t, rb.qf,
+                           rb.thr, rb.cnt, cap, rb.fcnt, rb.buf);
+      else
+        hipLaunchKernelGGL((rescan_filter_wide_kernel<1, FQ>), fg, dim3(256), qbytes, s, t, rb.qf,
+                           rb.thr, rb.cnt, cap, rb.fcnt, rb.buf);
+    }
+    const size_t lds = (size_t)(t.d <= 1024 ? t.d : 0) * 8 + (size_t)kRescanCap * 8 +
+                       (size_t)256 * 17 * 8 + (size_t)kRescanCap * 8;
+    const int gf = std::min(cap, 512);
+    if (metric == 0)
+      hipLaunchKernelGGL((rescan_finish_fast_kernel<0, 256>), dim3(gf), dim3(256), lds, s, t, Q64,
+                         rb.q, rb.tau, rb.cnt, cap, W, rb.fcnt, rb.buf, sink, rb.slow_q);
+    else
+      hipLaunchKernelGGL((rescan_finish_fast_kernel<1, 256>), dim3(gf), dim3(256), lds, s, t, Q64,
+                         rb.q, rb.tau, rb.cnt, cap, W, rb.fcnt, rb.buf, sink, rb.slow_q);
+  }
+  const int gs = std::max(1, full_blocks);
   if (metric == 0)
-    hipLaunchKernelGGL((rescan_chunk_kernel<0>), dim3(n_chunks, nf), dim3(256), 0, s, t, Q64,
-                       rescan_q, f0, W, n_chunks, pa_k, pa_i);
+    hipLaunchKernelGGL(rescan_full_kernel<0>, dim3(gs), dim3(kFullThreads), 0, s, t, Q64, rb.q,
+                       rb.cnt, cap, rb.slow_q, W, sink, rb.counts, rb.totals);
   else
-    hipLaunchKernelGGL((rescan_chunk_kernel<1>), dim3(n_chunks, nf), dim3(256), 0, s, t, Q64,
-                       rescan_q, f0, W, n_chunks, pa_k, pa_i);
-  int P = n_chunks;
-  double* ik = pa_k; int* ii = pa_i;
-  double* ok = pb_k; int* oi = pb_i;
-  const int G = kSortN / W;  // W <= kMaxK + 1 <= kSortN / 2
-  while (P > 1) {
-    const int P2 = (P + G - 1) / G;
-    hipLaunchKernelGGL(rescan_reduce_kernel, dim3(P2, nf), dim3(256), 0, s, ik, ii, P, W, G, ok,
-                       oi, P2);
-    double* tk = ik; ik = ok; ok = tk;
-    int* ti = ii; ii = oi; oi = ti;
-    P = P2;
-  }
-  const size_t lds = (size_t)W * 16;
-  hipLaunchKernelGGL(rescan_finish_kernel, dim3(nf), dim3(64), lds, s, t, ik, ii, rescan_q, f0,
-                     W, sink);
+    hipLaunchKernelGGL(rescan_full_kernel<1>, dim3(gs), dim3(kFullThreads), 0, s, t, Q64, rb.q,
+                       rb.cnt, cap, rb.slow_q, W, sink, rb.counts, rb.totals);
 }
 
 // ------------------------------------------ train-sharded k-way merge + vote
@@ -724,6 +865,7 @@ merge_vote_partials_kernel(const double* __restrict__ dist, const int64_t* __res
     }
     dk[e] = v;
     gi[e] = id;
+    ls[e] = -1;  // fewer than k entries (tiny shards, non-finite queries): label -1
   }
   bitonic_sort_lds(dk, gi, P2, lane, 64);
   // labels travel with the lists: place each one at its entry's sorted slot

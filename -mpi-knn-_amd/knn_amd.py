@@ -3,8 +3,9 @@
 The reference (Jason-Woo/-MPI-KNN-, knn_mpi.cpp) has no library API: its
 interface is the constant block (cpp:108-119), the CSV formats and the
 outputs.  `KnnConfig` carries those constants under the same names;
-`Classifier` is the per-GPU hot path (set_train / classify); `run_reference_
-program` reproduces main() end to end through the native host driver.
+`Classifier` is the per-GPU hot path (set_train / classify); `run_driver`
+reproduces the reference's main() end to end through the native drop-in
+driver (bin/knn_mpi_amd) -- the product, not the reference program.
 
 There is no CPU compute path: every call goes through the HIP library and
 fails loudly (KnnError) when the library or the GPU is missing.
@@ -26,6 +27,7 @@ DRIVER_PATH = os.path.join(HERE, "bin", "knn_mpi_amd")
 
 L2, L1 = 0, 1
 FLAG_EXACT_RESCAN, FLAG_TIE_BOUNDARY, FLAG_TIE_VOTE, FLAG_TIE_ORDER = 1, 2, 4, 8
+FLAG_NONFINITE = 16
 EXPORTED = (
     "knn_version", "knn_last_error", "knn_device_count", "knn_create", "knn_destroy",
     "knn_set_train", "knn_set_train_device", "knn_classify", "knn_classify_device",
@@ -34,6 +36,7 @@ EXPORTED = (
     "knn_group_last_compute_seconds", "knn_set_timing", "knn_last_phase_ms",
     "knn_last_geometry", "knn_set_precision", "knn_last_candidate_path", "knn_set_tuning",
     "knn_minmax_device", "knn_normalize_device", "knn_normalize", "knn_group_normalize",
+    "knn_timing_totals", "knn_rescan_totals", "knn_last_kernel_name",
 )
 PRECISION_AUTO, PRECISION_FP32, PRECISION_BF16X3, PRECISION_FP16 = 0, 1, 2, 3
 PHASE_PREP, PHASE_CANDIDATE, PHASE_RERANK, PHASE_RESCAN = 0, 1, 2, 3
@@ -114,6 +117,10 @@ def lib():
         "knn_normalize_device": ([P, P, i64, i32, P, P, P], ctypes.c_int),
         "knn_normalize": ([P, P, P, i32, i32, P, P], ctypes.c_int),
         "knn_group_normalize": ([P, P, P, i32, i32], ctypes.c_int),
+        "knn_timing_totals": ([P, ctypes.POINTER(f64), ctypes.POINTER(i64), ctypes.c_int],
+                              ctypes.c_int),
+        "knn_rescan_totals": ([P, ctypes.POINTER(i64), ctypes.c_int], ctypes.c_int),
+        "knn_last_kernel_name": ([P], ctypes.c_char_p),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -228,7 +235,26 @@ class Classifier:
         _check(lib().knn_sync(self._h))
 
     def last_rescan_count(self):
+        """Queries of the last call that failed certification (waits for it)."""
         return int(lib().knn_last_rescan_count(self._h))
+
+    def rescan_totals(self, reset=False):
+        """(failed certification, finished by the full exact scan) summed over
+        the calls since the last reset (waits for them)."""
+        out = (ctypes.c_int64 * 2)()
+        _check(lib().knn_rescan_totals(self._h, out, int(bool(reset))))
+        return int(out[0]), int(out[1])
+
+    def timing_totals(self, reset=False):
+        """(per-phase ms summed over timed calls since the last reset, calls)."""
+        ms = (ctypes.c_double * 4)()
+        calls = ctypes.c_int64()
+        _check(lib().knn_timing_totals(self._h, ms, ctypes.byref(calls), int(bool(reset))))
+        return [float(v) for v in ms], int(calls.value)
+
+    def last_kernel_name(self):
+        """Candidate kernel of the last call, rocprofv3-style ("cand_kernel<128,4,4,8>")."""
+        return lib().knn_last_kernel_name(self._h).decode()
 
     def set_precision(self, mode):
         """PRECISION_AUTO (bf16x3 where supported), PRECISION_FP32, PRECISION_BF16X3.
@@ -236,7 +262,8 @@ class Classifier:
         _check(lib().knn_set_precision(self._h, int(mode)))
 
     def set_tuning(self, key, value):
-        """Experiment overrides: key "R" (0/4/8/16) or "S" (0..64); 0 = automatic."""
+        """Experiment overrides (knn_amd.h): "R", "S", "nw", "ablate", "fp16",
+        "mfma16"; 0 (or -1 where stated) = automatic."""
         _check(lib().knn_set_tuning(self._h, key.encode(), int(value)))
 
     def last_candidate_path(self):
@@ -320,9 +347,9 @@ class Group:
         _check(lib().knn_group_normalize(self._h, ptrs, rows, ns, d))
 
 
-def run_reference_program(cfg: KnnConfig, workdir, gpus=1, mode="query", extra=()):
-    """Runs the native drop-in driver (bin/knn_mpi_amd) like `mpiexec knn_mpi`
-    in `workdir`; returns its stdout."""
+def run_driver(cfg: KnnConfig, workdir, gpus=1, mode="query", extra=()):
+    """Runs the native drop-in driver (bin/knn_mpi_amd) the way `mpiexec
+    knn_mpi` runs the reference, in `workdir`; returns its stdout."""
     if not os.path.exists(DRIVER_PATH):
         raise KnnError("driver not built: " + DRIVER_PATH)
     args = [DRIVER_PATH]

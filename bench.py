@@ -5,24 +5,36 @@ Metric (BASELINE.json): queries/sec (node) + % MFMA peak on configs[1] =
 1M train x 10k queries, d=128, k=10 (L2), per GPU.  A step is one
 knn_classify_device call over the rank's 10k queries: fused MFMA distance +
 top-R candidate kernel, fp64 exact re-rank + certification + first-to-max
-vote, exact rescan of uncertified queries if any.  Inputs are synthetic
-(seeded Gaussian mixture, min-max normalised, fp64 like the reference's
-Data_train) and resident in HBM before timing starts.
+vote, and the device-driven exact rescan of uncertified queries.  Inputs are
+synthetic (seeded Gaussian mixture, fp64 like the reference's Data_train)
+and resident in HBM before timing starts.
 
-Multi-GPU (--mode query, default; north_star mode a): the train set is
-broadcast from rank 0 with torch.distributed (RCCL over xGMI) before timing;
-every rank classifies its own 10k queries (weak scaling, no data-path
-collective).  --mode train (mode b, cfg4 shape: --n-train 100000000 --dim 96):
-rank r holds train rows [n r/W, n (r+1)/W); a step = local exact top-(k+1)
-+ RCCL all-gather of the lists + k-way merge/vote of the rank's query slice.
+Multi-GPU: `--gpus N` launches N ranks itself (one process per GPU through
+torch.distributed.run, started before anything touches the GPU) unless it
+already runs under a launcher (WORLD_SIZE set, e.g. the driver's own
+torch.distributed.run).
+  --mode query (default; north_star mode a, ≙ MPI_Bcast + MPI_Scatter,
+    cpp:224-227): the train set is RCCL-broadcast from rank 0 (timed and
+    reported separately: train_broadcast_ms) and every rank classifies its
+    own 10k queries -- weak scaling, no data-path collective.  The same line
+    carries the configs[2] strong-scaling leg (`cfg3_strong`): a fixed 1M
+    queries split 1M/N per rank (≙ the batch split cpp:136-138).
+  --mode train (mode b, cfg4 shape: --n-train 100000000 --dim 96): rank r
+    holds train rows [n r/N, n (r+1)/N); a step = local exact top-(k+1) + RCCL
+    all-gather of the lists + k-way merge/vote of the rank's query slice.
+`--dry-run` (CPU, gloo): plumbing check of the launcher and the
+decomposition only -- a plain torch brute force stands in for the HIP
+library and the line reports value null.
 
 Run: python bench.py [--gpus N --steps K --warmup W]
-     (N>1: python -m torch.distributed.run --nproc-per-node N bench.py ...)
 """
 import argparse
+import glob
+import hashlib
 import importlib.util
 import json
 import os
+import socket
 import subprocess
 import sys
 import time
@@ -34,8 +46,9 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "-mpi-knn-_amd")
 PEAK_FP32_TFLOPS = 157.3   # MI355X dense fp32 MFMA (= vector) peak, MI355X_MICROARCH.md
-PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA peak (no sparsity), MI355X_MICROARCH.md
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16/fp16 MFMA peak (no sparsity), MI355X_MICROARCH.md
 METRIC = "queries/sec (node) + % MFMA peak, 1M train x 10k query d=128 k=10, 1/2/4/8 GPU"
+REF_SAMPLE = 512  # queries the reference program classifies in the bench's baseline leg
 
 
 def log(*a):
@@ -58,13 +71,6 @@ def load_knn():
     return _load("knn_amd")
 
 
-def pad_dim(d):
-    for v in (16, 32, 48, 64, 96, 128, 160, 192, 256):
-        if d <= v:
-            return v
-    return d
-
-
 def _grid(x, lo, hi):
     """Scale into [0,1) and quantise to the 8-bit grid k/256 (SIFT-like byte
     features): exact in fp64 and in an 8-digit decimal CSV, so the reference
@@ -72,81 +78,147 @@ def _grid(x, lo, hi):
     return ((x - lo) / (hi - lo) * 256.0).floor_().clamp_(0.0, 255.0).div_(256.0)
 
 
-def synth(n, m, d, classes, seed_train, seed_query, device, row0=0, n_total=None):
-    """Gaussian mixture (class = cluster), values scaled into [0,1) like the
-    reference's min-max normalisation (cpp:229-306) and quantised to 8-bit
-    grid values k/256, fp64.  Rows [row0, row0+n) of a virtual n_total-row
-    train set (train sharding), generated in chunks so a 100M-row shard
-    needs no temporaries of its size."""
+CHUNK = 1 << 20  # rows per generator chunk (a chunk's values depend only on its index)
+
+
+def _rows(centres, n, row0, seed, device, classes):
+    """Rows [row0, row0+n) of a virtual Gaussian-mixture set, raw (unscaled)
+    fp64, generated chunk by chunk: any shard of the set is reproduced exactly
+    whatever the shard boundaries (row0 must be a multiple of CHUNK or 0)."""
+    d = centres.shape[1]
+    X = torch.empty((n, d), device=device, dtype=torch.float64)
+    lab = torch.empty(n, device=device, dtype=torch.int32)
+    for c0 in range(0, n, CHUNK):
+        c1 = min(n, c0 + CHUNK)
+        gc = torch.Generator(device=device)
+        gc.manual_seed(seed * 1000003 + (row0 + c0) // CHUNK)
+        lc = torch.randint(0, classes, (c1 - c0,), generator=gc, device=device, dtype=torch.int32)
+        X[c0:c1] = centres[lc.long()] + torch.randn((c1 - c0, d), generator=gc, device=device,
+                                                    dtype=torch.float64)
+        lab[c0:c1] = lc
+    return X, lab
+
+
+def minmax_normalize_(sets, reduce=None):
+    """The reference's transductive min-max normalisation (cpp:229-306) on
+    device tensors, in place: per-dim max/min over every set, starting from
+    the quirky -1 / 999999 (cpp:239-243), then (x - min) / (max - min) on
+    dims with max != min (cpp:279-305) -- the same fp64 subtract and divide.
+    reduce(mx, mn): optional cross-rank MAX / MIN all-reduce (≙ cpp:276-277)."""
+    d = sets[0].shape[1]
+    dev = sets[0].device
+    mx = torch.full((d,), -1.0, dtype=torch.float64, device=dev)
+    mn = torch.full((d,), 999999.0, dtype=torch.float64, device=dev)
+    for s in sets:
+        for c0 in range(0, s.shape[0], CHUNK):
+            c = s[c0:c0 + CHUNK]
+            mx = torch.maximum(mx, c.amax(0))
+            mn = torch.minimum(mn, c.amin(0))
+    if reduce is not None:
+        reduce(mx, mn)
+    rng = mx - mn
+    keep = rng != 0
+    rng = torch.where(keep, rng, torch.ones_like(rng))
+    for s in sets:
+        for c0 in range(0, s.shape[0], CHUNK):
+            c = s[c0:c0 + CHUNK]
+            c.copy_(torch.where(keep, (c - mn) / rng, c))
+    return mx, mn
+
+
+def synth(n, m, d, classes, seed_train, seed_query, device, row0=0, n_total=None, data="grid",
+          q0=0, reduce=None):
+    """Gaussian mixture (class = cluster), fp64.  Train rows [row0, row0+n)
+    and query rows [q0, q0+m) of virtual sets (train / query sharding),
+    generated in chunks so a 100M-row shard needs no temporaries of its size.
+      data="grid":       scaled into [0,1) with a fixed range and quantised to
+                         the 8-bit grid k/256 (SIFT-like byte features);
+      data="continuous": min-max normalised exactly as the reference does
+                         (cpp:229-306, over train and queries), no quantisation:
+                         values are not on any power-of-two grid (MNIST-style
+                         (x - min) / (max - min) features).  With sharded sets
+                         pass reduce= for the cross-rank MAX/MIN."""
     g = torch.Generator(device=device)
     g.manual_seed(seed_train)
     centres = torch.rand((classes, d), generator=g, device=device, dtype=torch.float64) * 4 - 2
-    lo, hi = -2.0 - 4.5, 2.0 + 4.5  # fixed scale (centres in [-2,2] + N(0,1) tails)
-    X = torch.empty((n, d), device=device, dtype=torch.float64)
-    lab = torch.empty(n, device=device, dtype=torch.int32)
-    chunk = 1 << 20
-    for c0 in range(0, n, chunk):
-        c1 = min(n, c0 + chunk)
-        gc = torch.Generator(device=device)
-        gc.manual_seed(seed_train * 1000003 + (row0 + c0) // chunk)
-        lc = torch.randint(0, classes, (c1 - c0,), generator=gc, device=device, dtype=torch.int32)
-        xc = centres[lc.long()] + torch.randn((c1 - c0, d), generator=gc, device=device,
-                                              dtype=torch.float64)
-        X[c0:c1] = _grid(xc, lo, hi)
-        lab[c0:c1] = lc
-    gq = torch.Generator(device=device)
-    gq.manual_seed(seed_query)
-    qlab = torch.randint(0, classes, (m,), generator=gq, device=device, dtype=torch.int32)
-    Q = centres[qlab.long()] + torch.randn((m, d), generator=gq, device=device, dtype=torch.float64)
-    Q = _grid(Q, lo, hi).contiguous()
+    X, lab = _rows(centres, n, row0, seed_train, device, classes)
+    Q, qlab = _rows(centres, m, q0, seed_query, device, classes)
+    if data == "grid":
+        lo, hi = -2.0 - 4.5, 2.0 + 4.5  # fixed scale (centres in [-2,2] + N(0,1) tails)
+        for s in (X, Q):
+            for c0 in range(0, s.shape[0], CHUNK):
+                s[c0:c0 + CHUNK] = _grid(s[c0:c0 + CHUNK], lo, hi)
+    elif data == "continuous":
+        minmax_normalize_([X, Q], reduce)
+    else:
+        raise ValueError("data must be grid or continuous")
     return X, lab, Q, qlab
 
 
-def pmc_traffic(kernel, n, m, d, k):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC pass
-    (profiles/*_traffic_*.json, made by tools/traffic_json.py: 2*FETCH_SIZE +
-    WRITE_SIZE, KiB -> B) when it profiled this exact workload; else None.
-    Counters cannot be read from inside the timed process itself."""
-    import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic_*.json")), reverse=True):
+def kernel_src_sha():
+    """Identity of the kernel build: sha1 over the library's sources.  PMC
+    traffic files record it, and a bench line only cites a profile of the
+    same sources (profiles/*_traffic_*.json, tools/traffic_json.py)."""
+    h = hashlib.sha1()
+    for p in sorted(glob.glob(os.path.join(PKG, "csrc", "*"))):
+        h.update(os.path.basename(p).encode())
+        h.update(open(p, "rb").read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(kernel, workload, src_sha):
+    """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC pass of
+    this exact workload and kernel build (2*FETCH_SIZE + WRITE_SIZE, KiB -> B);
+    (None, reason) when no such profile exists.  Counters cannot be read from
+    inside the timed process itself."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic_*.json"))):
         try:
             rec = json.load(open(path))
         except (OSError, ValueError):
             continue
         wl = rec.get("workload", {})
-        if (wl.get("n_train"), wl.get("queries"), wl.get("dim"), wl.get("k")) != (n, m, d, k):
+        if any(wl.get(key) != workload[key] for key in ("n_train", "queries", "dim", "k")):
+            continue
+        if rec.get("kernel_src_sha") != src_sha:
             continue
         kr = rec.get("kernels", {}).get(kernel)
         if kr:
             return kr["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
-    return None, None
+    return None, "no PMC profile of %s for this workload and kernel build (%s)" % (kernel, src_sha)
+
+
+def host_cores():
+    """(CPUs this process may run on, the CPU share granted to it): on the GPU
+    box the affinity mask shows the whole machine while the share is set in
+    OMP_NUM_THREADS (16 per GPU)."""
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    share = int(os.environ.get("OMP_NUM_THREADS") or cores)
+    return cores, max(1, min(cores, share))
 
 
 def cpu_baseline(X, lab, Q, k, classes, gpu_labels, budget_s=12.0):
     """Oracle (CPU restatement of the reference, bit-identical on the golden
-    fixtures) on a bounded query sample using all host cores."""
+    fixtures) on a bounded query sample using the granted host cores."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    cores = max(1, min(cores, 16))
+    cores, share = host_cores()
     Xh, lh, Qh = X.cpu().numpy(), lab.cpu().numpy(), Q.cpu().numpy()
     t0 = time.perf_counter()
-    oracle.knn(Xh, lh, Qh[:cores], k, True, classes, nthreads=cores)  # calibrate
+    oracle.knn(Xh, lh, Qh[:share], k, True, classes, nthreads=share)  # calibrate
     per_round = time.perf_counter() - t0
     rounds = int(max(1, min(32, (budget_s - per_round) / max(per_round, 1e-6))))
-    sample = min(Qh.shape[0], cores * rounds)
+    sample = min(Qh.shape[0], share * rounds)
     t0 = time.perf_counter()
-    want, _, _ = oracle.knn(Xh, lh, Qh[:sample], k, True, classes, nthreads=cores)
+    want, _, _ = oracle.knn(Xh, lh, Qh[:sample], k, True, classes, nthreads=share)
     el = time.perf_counter() - t0
     match = bool((want == gpu_labels[:sample]).all())
-    return {"value": sample / el, "unit": "queries/s", "cores": cores, "kind": "port",
+    return {"value": sample / el, "unit": "queries/s", "cores": share, "host_cores": cores,
+            "cpu_share": share, "kind": "port",
             "sample": "%d of the %d queries (first ones) against all %d train rows, "
-                      "oracle/knn_oracle.cpp with %d threads, %.1f s; labels match GPU: %s"
-                      % (sample, Qh.shape[0], Xh.shape[0], cores, el, match),
+                      "oracle/knn_oracle.cpp with %d threads (%d host CPUs visible, share %d), "
+                      "%.1f s; labels match GPU: %s"
+                      % (sample, Qh.shape[0], Xh.shape[0], share, cores, share, el, match),
             "labels_match_gpu": match}
-
-
-REF_SAMPLE = 512  # queries the reference program classifies in the bench's baseline leg
 
 
 def ref_config(n, d, k, classes, sample=REF_SAMPLE):
@@ -159,18 +231,19 @@ def ref_config(n, d, k, classes, sample=REF_SAMPLE):
 def cpu_baseline_reference(X, lab, Q, k, classes, gpu_labels):
     """The reference program itself (knn_mpi.cpp, compiled unmodified apart
     from its constants and a timer around the test-query loop) under mpirun
-    on the host cores, on the first REF_SAMPLE queries against the full train
-    set.  value = queries / test-loop seconds (max over ranks); the CSV parse
-    and MPI_Bcast are in running_time_s."""
+    on the granted host cores, on the first REF_SAMPLE queries against the
+    full train set.  Ranks = the largest P <= the CPU share that divides
+    N_train and the sample (the reference aborts otherwise, cpp:127-129).
+    value = queries / test-loop seconds (max over ranks); the CSV parse and
+    MPI_Bcast are in running_time_s."""
     import shutil
     import tempfile
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import build_ref
     import ref_runner
     n, d = X.shape
-    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    nprocs = next(p for p in (16, 8, 4, 2) if p <= max(2, cores) and n % p == 0
-                  and REF_SAMPLE % p == 0)
+    cores, share = host_cores()
+    nprocs = max(p for p in range(2, max(2, share) + 1) if n % p == 0 and REF_SAMPLE % p == 0)
     exe = build_ref.build_ref(ref_config(n, d, k, classes), instrument=False, timing=True)
     codes = (X * 256.0).round().to(torch.uint8).cpu().numpy()
     qcodes = (Q[:REF_SAMPLE] * 256.0).round().to(torch.uint8).cpu().numpy()
@@ -183,13 +256,80 @@ def cpu_baseline_reference(X, lab, Q, k, classes, gpu_labels):
     finally:
         shutil.rmtree(wd, ignore_errors=True)
     match = bool((labels == gpu_labels[:REF_SAMPLE]).all())
-    return {"value": REF_SAMPLE / loop_s, "unit": "queries/s", "cores": nprocs, "kind": "reference",
+    return {"value": REF_SAMPLE / loop_s, "unit": "queries/s", "cores": nprocs,
+            "host_cores": cores, "cpu_share": share, "ranks": nprocs, "kind": "reference",
             "sample": "%d of the %d queries (first ones) against all %d train rows: "
                       "/root/reference/knn_mpi.cpp (constants set, Normalize=false, timer around "
-                      "the test loop) under mpirun -np %d; test loop %.2f s, whole run %.1f s "
-                      "incl. CSV parse + MPI_Bcast; labels match GPU: %s"
-                      % (REF_SAMPLE, Q.shape[0], n, nprocs, loop_s, run_s, match),
+                      "the test loop) under mpirun -np %d on the box's host CPUs (%d visible, "
+                      "share %d); test loop %.2f s, whole run %.1f s incl. CSV parse + "
+                      "MPI_Bcast; labels match GPU: %s"
+                      % (REF_SAMPLE, Q.shape[0], n, nprocs, cores, share, loop_s, run_s, match),
             "running_time_s": run_s, "labels_match_gpu": match}
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n):
+    """One process per GPU: re-run this script under torch.distributed.run as
+    a CHILD process (nothing here has touched the GPU) and return its exit
+    code.  The env (HSA_ENABLE_IPC_MODE_LEGACY=0 etc.) is inherited."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+           str(n), "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
+class CpuStandIn:
+    """--dry-run only: a plain torch fp64 brute force in place of the HIP
+    library, so the launcher and the decomposition can be exercised on CPU
+    (gloo).  Not a measurement; the bench line reports value null."""
+    L2 = 0
+    PRECISION_AUTO = PRECISION_FP32 = 0
+
+    def set_train(self, X, lab, classes):
+        self.X, self.lab = X, lab
+
+    def classify(self, Q, k):
+        d2 = (Q * Q).sum(1)[:, None] + (self.X * self.X).sum(1)[None, :] - 2.0 * Q @ self.X.T
+        nb = torch.topk(d2, k, dim=1, largest=False).indices
+        nl = self.lab[nb]
+        out = torch.empty(Q.shape[0], dtype=torch.int32)
+        for q in range(Q.shape[0]):  # cpp:324-337
+            cnt, best, bl = {}, 0, -1
+            for t in range(k):
+                lb = int(nl[q, t])
+                cnt[lb] = cnt.get(lb, 0) + 1
+                if cnt[lb] > best:
+                    best, bl = cnt[lb], lb
+            out[q] = bl
+        return out
+
+
+def timed_run(kd, clf, step, steps, warmup, sync, dev, precision=None):
+    """W untimed steps, then exactly K timed steps bracketed by barrier + sync
+    (max over ranks); HIP-event phase times and rescan counts of the K timed
+    calls are read back only after the timed region."""
+    if precision is not None:
+        clf.set_precision(precision)
+    for _ in range(warmup):
+        step()
+    sync()
+    clf.timing_totals(reset=True)
+    clf.rescan_totals(reset=True)
+    el = kd.timed(step, steps, 0, sync, dev)
+    ms, calls = clf.timing_totals(reset=True)
+    resc = clf.rescan_totals(reset=True)
+    calls = max(1, calls)
+    return dict(el=el, t_cand=ms[1] / calls * 1e-3, rr=ms[2] / calls, rescan_ms=ms[3] / calls,
+                prep_ms=ms[0] / calls, calls=calls, resc=resc[0], full_scans=resc[1],
+                path=clf.last_candidate_path(), geom=clf.last_geometry(),
+                kernel=clf.last_kernel_name())
 
 
 def main():
@@ -204,91 +344,173 @@ def main():
     ap.add_argument("--dim", type=int, default=128)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--classes", type=int, default=10)
+    ap.add_argument("--data", choices=("grid", "continuous"), default="grid")
+    ap.add_argument("--cfg3-queries", type=int, default=1_000_000,
+                    help="configs[2] strong-scaling leg: total queries split over the ranks "
+                         "(0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fp32-path", action="store_true")
+    ap.add_argument("--no-continuous", action="store_true",
+                    help="skip the continuous-data leg of the default run")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU/gloo plumbing check with a torch stand-in (no measurement)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log("note: --gpus %d but the launcher started %d ranks; reporting %d"
+            % (args.gpus, world, world))
+    kd = _load("knn_dist")
+    if args.dry_run:
+        return dry_run(args, kd, world, rank)
+
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
-    kd = _load("knn_dist")
     knn = load_knn()
     n, m, d, k, C = args.n_train, args.queries, args.dim, args.k, args.classes
     sync = torch.cuda.synchronize
     stream = torch.cuda.current_stream().cuda_stream
     clf = knn.Classifier(local)
     clf.set_timing(True)
+    extra = {}
+
+    def allreduce_minmax(mx, mn):
+        if world > 1:
+            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+            dist.all_reduce(mn, op=dist.ReduceOp.MIN)
 
     if args.mode == "query":
-        # train generated on rank 0 and RCCL-broadcast (≙ MPI_Bcast cpp:224-225)
-        X, lab, Q, _ = synth(n, m, d, C, 1234, 5678 + rank, dev)
-        kd.broadcast_train(X, lab)
+        # train generated on rank 0 and RCCL-broadcast (≙ MPI_Bcast cpp:224-225);
+        # rank r's weak-scaling queries are rows [r m, (r+1) m) of one query set
+        X, lab, Q, _ = synth(n, m, d, C, 1234, 5678, dev, data=args.data, q0=rank * m,
+                             reduce=allreduce_minmax)
         sync()
-        log("synthetic train ready: %d rows x %d" % (n, d))
+        if world > 1:
+            dist.barrier()
+            sync()
+            t0 = time.perf_counter()
+            kd.broadcast_train(X, lab)
+            sync()
+            dist.barrier()
+            bt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+            dist.all_reduce(bt, op=dist.ReduceOp.MAX)
+            extra["train_broadcast_ms"] = float(bt.item()) * 1e3
+            extra["train_broadcast_gbps"] = (X.numel() * 8 + lab.numel() * 4) / float(bt.item()) / 1e9
+        log("synthetic train ready: %d rows x %d (%s data)" % (n, d, args.data))
+        t0 = time.perf_counter()
         clf.set_train_device(X.data_ptr(), lab.data_ptr(), n, d, C, keep=(X, lab))
+        sync()
+        extra["set_train_ms"] = (time.perf_counter() - t0) * 1e3
         out_lab = torch.empty(m, dtype=torch.int32, device=dev)
         out_flags = torch.empty(m, dtype=torch.int32, device=dev)
-        stats = {"cand": [], "rr": [], "resc": 0}
 
         def step():
             clf.classify_device(Q.data_ptr(), m, k, knn.L2, out_lab.data_ptr(), None, None,
                                 out_flags.data_ptr(), stream)
-            stats["cand"].append(clf.last_phase_ms(knn.PHASE_CANDIDATE))
-            stats["rr"].append(clf.last_phase_ms(knn.PHASE_RERANK))
-            stats["resc"] += clf.last_rescan_count()
-
-        def run(precision, steps, warmup):
-            clf.set_precision(precision)
-            for key in ("cand", "rr"):
-                stats[key] = []
-            stats["resc"] = 0
-            el = kd.timed(step, steps, warmup, sync, dev)
-            cand = stats["cand"][warmup:]
-            return dict(el=el, t_cand=float(np.mean(cand)) * 1e-3,
-                        rr=float(np.mean(stats["rr"][warmup:])), resc=stats["resc"],
-                        path=clf.last_candidate_path(), geom=clf.last_geometry())
 
         n_rank, m_rank = n, m
         flops = 2.0 * n * d * m  # algorithmic, per launch per GPU (norm terms excluded)
-        main_r = run(knn.PRECISION_AUTO, args.steps, args.warmup)
+        main_r = timed_run(kd, clf, step, args.steps, args.warmup, sync, dev, knn.PRECISION_AUTO)
         log("default path done: %.3f ms/step" % (main_r["el"] / args.steps * 1e3))
         labels_auto = out_lab.clone()
-        fp32_r = None
-        if not args.no_fp32_path:
-            fp32_r = run(knn.PRECISION_FP32, max(3, args.steps // 2), 1)
-        same = bool(torch.equal(labels_auto, out_lab))
+        flags_auto = out_flags.clone()
+        tie_vote = int(((flags_auto & knn.FLAG_TIE_VOTE) != 0).sum().item())
+        if world > 1:
+            tv = torch.tensor([tie_vote], dtype=torch.int64, device=dev)
+            dist.all_reduce(tv)
+            tie_vote = int(tv.item())
+        extra["tie_vote_queries"] = tie_vote
+        fp32_r = same = None
+        if not args.no_fp32_path and world == 1:
+            fp32_r = timed_run(kd, clf, step, max(3, args.steps // 2), 1, sync, dev,
+                               knn.PRECISION_FP32)
+            same = bool(torch.equal(labels_auto, out_lab))
+            clf.set_precision(knn.PRECISION_AUTO)
         total_q = m * world * args.steps
-        tag = {(1_000_000, 128, 10): "cfg2", (1_000_000, 960, 100): "cfg5"}.get(
-            (n, d, k), "custom")
+        tag = {(1_000_000, 128, 10): "cfg2", (1_000_000, 960, 100): "cfg5"}.get((n, d, k), "custom")
         workload = ("%s: %d train x %d queries per GPU, d=%d, k=%d, L2, %d classes"
                     % (tag, n, m, d, k, C))
         parallelism = "query-sharded dp%d" % world
+        scaling = "weak"
+
+        if args.cfg3_queries > 0 and d == 128 and n == 1_000_000:
+            # configs[2]: a fixed query count split over the ranks (strong scaling)
+            M = args.cfg3_queries
+            q0, q1 = kd.shard_range(M, world, rank)
+            _, _, Q3, _ = synth(0, q1 - q0, d, C, 1234, 91011, dev, data=args.data, q0=q0)
+            if args.data == "continuous":  # the train set's normalisation bounds are already applied
+                Q3 = None
+            if Q3 is not None:
+                lab3 = torch.empty(q1 - q0, dtype=torch.int32, device=dev)
+
+                def step3():
+                    clf.classify_device(Q3.data_ptr(), q1 - q0, k, knn.L2, lab3.data_ptr(), None,
+                                        None, None, stream)
+
+                s3 = max(2, args.steps // 4)
+                r3 = timed_run(kd, clf, step3, s3, 1, sync, dev, knn.PRECISION_AUTO)
+                extra["cfg3_strong"] = {
+                    "workload": "cfg3: %d train x %d queries in total split over %d GPU(s) "
+                                "(%d per rank), d=%d, k=%d" % (n, M, world, q1 - q0, d, k),
+                    "value": M * s3 / r3["el"], "unit": "queries/s", "n_gpus": world,
+                    "steps": s3, "ms_per_step": r3["el"] / s3 * 1e3, "scaling": "strong",
+                    "kernel_ms": r3["t_cand"] * 1e3, "rescanned_queries": r3["resc"],
+                    "candidate_path": r3["path"]}
+                log("cfg3 strong leg: %.1f ms/step" % (r3["el"] / s3 * 1e3))
+                del Q3, lab3
+
+        if not args.no_continuous and args.data == "grid" and world == 1:
+            # the same workload on continuous (min-max normalised, off-grid) data
+            Xc, labc, Qc, _ = synth(n, m, d, C, 4242, 2424, dev, data="continuous")
+            clf.set_train_device(Xc.data_ptr(), labc.data_ptr(), n, d, C, keep=(Xc, labc))
+            outc = torch.empty(m, dtype=torch.int32, device=dev)
+
+            def stepc():
+                clf.classify_device(Qc.data_ptr(), m, k, knn.L2, outc.data_ptr(), None, None,
+                                    None, stream)
+
+            sc = max(3, args.steps // 2)
+            rc = timed_run(kd, clf, stepc, sc, 1, sync, dev, knn.PRECISION_AUTO)
+            ac = flops / rc["t_cand"] / 1e12
+            extra["continuous_data"] = {
+                "data": "same Gaussian mixture, min-max normalised as cpp:229-306 (train and "
+                        "queries), not quantised: values on no power-of-two grid",
+                "value": m * sc / rc["el"], "unit": "queries/s", "ms_per_step": rc["el"] / sc * 1e3,
+                "kernel_ms": rc["t_cand"] * 1e3, "frac": ac / (PEAK_BF16_TFLOPS if rc["path"] in
+                                                               (2, 3, 4) else PEAK_FP32_TFLOPS),
+                "candidate_path": rc["path"], "rescanned_queries": rc["resc"],
+                "rescanned_per_step": rc["resc"] / rc["calls"], "full_scans": rc["full_scans"]}
+            log("continuous-data leg: %.3f ms/step, %d rescans" % (rc["el"] / sc * 1e3, rc["resc"]))
+            del Xc, labc, Qc
+            clf.set_train_device(X.data_ptr(), lab.data_ptr(), n, d, C, keep=(X, lab))
     else:
         # train-sharded: this rank's rows only; the same queries on every rank
         r0, r1 = kd.shard_range(n, world, rank)
-        X, lab, Q, _ = synth(r1 - r0, m, d, C, 1234, 5678, dev, row0=r0, n_total=n)
+        X, lab, Q, _ = synth(r1 - r0, m, d, C, 1234, 5678, dev, row0=r0, n_total=n,
+                             data=args.data, reduce=allreduce_minmax)
         sync()
         log("synthetic shard ready: %d rows x %d" % (r1 - r0, d))
+        t0 = time.perf_counter()
         clf.set_train_device(X.data_ptr(), lab.data_ptr(), r1 - r0, d, C, idx_offset=r0,
                              keep=(X, lab))
+        sync()
+        extra["set_train_ms"] = (time.perf_counter() - t0) * 1e3
         w = k + 1
         pd_ = torch.empty((m, w), dtype=torch.float64, device=dev)
         pi_ = torch.empty((m, w), dtype=torch.int64, device=dev)
         pl_ = torch.empty((m, w), dtype=torch.int32, device=dev)
         q0, q1 = kd.shard_range(m, world, rank)
         out_lab = torch.empty(max(1, q1 - q0), dtype=torch.int32, device=dev)
-        stats = {"cand": [], "rr": [], "resc": 0}
 
         def search_partial(Qt):
             clf.search_partial_device(Qt.data_ptr(), m, w, knn.L2, pd_.data_ptr(), pi_.data_ptr(),
                                       pl_.data_ptr(), stream)
-            stats["cand"].append(clf.last_phase_ms(knn.PHASE_CANDIDATE))
-            stats["rr"].append(clf.last_phase_ms(knn.PHASE_RERANK))
-            stats["resc"] += clf.last_rescan_count()
             return pd_, pi_, pl_
 
         def merge_vote(gd, gi, gl, parts, a, b):  # k-way merge + vote of this rank's slice
@@ -298,27 +520,16 @@ def main():
 
         def step():
             kd.train_sharded(search_partial, merge_vote, Q, m, w, k, dev)
-            log("train-sharded step: cand %.2f ms rerank %.2f ms rescans %d"
-                % (stats["cand"][-1], stats["rr"][-1], stats["resc"]))
-
-        def run(precision, steps, warmup):
-            clf.set_precision(precision)
-            for key in ("cand", "rr"):
-                stats[key] = []
-            stats["resc"] = 0
-            el = kd.timed(step, steps, warmup, sync, dev)
-            return dict(el=el, t_cand=float(np.mean(stats["cand"][warmup:])) * 1e-3,
-                        rr=float(np.mean(stats["rr"][warmup:])), resc=stats["resc"],
-                        path=clf.last_candidate_path(), geom=clf.last_geometry())
 
         n_rank, m_rank = r1 - r0, m
         flops = 2.0 * (r1 - r0) * d * m
-        main_r = run(knn.PRECISION_AUTO, args.steps, args.warmup)
+        main_r = timed_run(kd, clf, step, args.steps, args.warmup, sync, dev, knn.PRECISION_AUTO)
         fp32_r, same = None, None
         total_q = m * args.steps
         workload = ("cfg4-shape: %d train (sharded) x %d queries, d=%d, k=%d, L2, %d classes"
                     % (n, m, d, k, C))
         parallelism = "train-sharded tp%d" % world
+        scaling = "strong"
 
     path = main_r["path"]
     bf16 = path in (2, 3)
@@ -333,12 +544,10 @@ def main():
         4: "fp16 operands (power-of-two scaled, centred) on MFMA 16x16x32 f16",
     }.get(path, "kernel metric %d" % path)
     achieved = flops / main_r["t_cand"] / 1e12
-    geom = main_r["geom"]
-    n_qt = max(1, geom["workgroups"] // max(1, geom["splits"]))
-    nw = 8 if -(-m_rank // n_qt) > 128 else 4  # waves per workgroup (32 queries each)
-    kname = ("cand_kernel<%d,%d,%d,%d>" % (pad_dim(d), geom["lists"], main_r["path"], nw)
-             if d <= 256 else "cand_stream_kernel<32,%d,%d>" % (geom["lists"], main_r["path"]))
-    traffic, traffic_src = pmc_traffic(kname, n_rank, m_rank, d, k)
+    kname = main_r["kernel"]
+    src_sha = kernel_src_sha()
+    wl = {"n_train": n_rank, "queries": m_rank, "dim": d, "k": k}
+    traffic, traffic_src = pmc_traffic(kname, wl, src_sha)
     result = {
         "metric": METRIC,
         "value": total_q / main_r["el"],
@@ -348,47 +557,89 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": main_r["el"] / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak" if args.mode == "query" else "strong",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": {2: "bf16x3", 3: "bf16x3", 4: "fp16"}.get(path, "fp32"),
-        "data": "synthetic (seeded Gaussian mixture scaled to [0,1) on the 8-bit grid k/256, "
-                "SIFT-like; fp64 inputs)",
+        "data": ("synthetic (seeded Gaussian mixture scaled to [0,1) on the 8-bit grid k/256, "
+                 "SIFT-like; fp64 inputs)" if args.data == "grid" else
+                 "synthetic (seeded Gaussian mixture, min-max normalised as cpp:229-306, "
+                 "continuous values; fp64 inputs)"),
         "config": {"workload": workload, "n_train": n, "queries": m, "dim": d, "k": k,
                    "parallelism": parallelism,
                    "candidate_pass": cand_desc + " + fused top-R per lane, certified bound",
                    "rerank": "fp64 exact (reference arithmetic), certified; labels exact",
-                   "geometry": geom, "rescanned_queries": main_r["resc"]},
+                   "geometry": main_r["geom"], "rescanned_queries": main_r["resc"],
+                   "full_scan_queries": main_r["full_scans"]},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                      "frac": achieved / peak, "traffic": traffic,
                      "traffic_unit": "bytes per launch (HBM, PMC)", "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": (n_rank + m_rank) * d * 4 + m_rank * k * 8,
-                     "kernel": kname,
+                     "kernel": kname, "kernel_src_sha": src_sha,
                      "kernel_ms": main_r["t_cand"] * 1e3, "rerank_ms": main_r["rr"],
+                     "rescan_ms": main_r["rescan_ms"], "prep_ms": main_r["prep_ms"],
+                     "timed_launches": main_r["calls"],
                      "algorithmic_flops_per_launch": flops,
                      "mfma_flops_per_algorithmic_flop": mfma_mult,
                      "frac_of_issued_mfma": achieved * mfma_mult / peak},
         "cpu_baseline": None,
     }
+    result.update(extra)
     if fp32_r is not None:
         a32 = flops / fp32_r["t_cand"] / 1e12
         result["fp32_path"] = {
-            "value": m * world * max(3, args.steps // 2) / fp32_r["el"], "unit": "queries/s",
-            "kernel_ms": fp32_r["t_cand"] * 1e3, "achieved": a32, "peak": PEAK_FP32_TFLOPS,
-            "frac": a32 / PEAK_FP32_TFLOPS, "rescanned_queries": fp32_r["resc"],
-            "geometry": fp32_r["geom"], "labels_equal_default_path": same}
+            "value": m * world * fp32_r["calls"] / fp32_r["el"], "unit": "queries/s",
+            "kernel": fp32_r["kernel"], "kernel_ms": fp32_r["t_cand"] * 1e3, "achieved": a32,
+            "peak": PEAK_FP32_TFLOPS, "frac": a32 / PEAK_FP32_TFLOPS,
+            "rescanned_queries": fp32_r["resc"], "geometry": fp32_r["geom"],
+            "labels_equal_default_path": same}
     if rank == 0 and world == 1 and args.mode == "query" and not args.no_cpu_baseline:
         log("cpu baseline (oracle port) ...")
         port = cpu_baseline(X, lab, Q, k, C, labels_auto.cpu().numpy(), budget_s=6.0)
         result["cpu_baseline"] = port
-        try:
-            log("cpu baseline (reference program under mpirun) ...")
-            result["cpu_baseline"] = cpu_baseline_reference(X, lab, Q, k, C,
-                                                            labels_auto.cpu().numpy())
-            result["cpu_baseline_port"] = port
-        except (OSError, RuntimeError, StopIteration, subprocess.SubprocessError) as e:
-            log("reference baseline unavailable (%s); reporting the oracle port" % e)
+        if args.data == "grid":
+            try:
+                log("cpu baseline (reference program under mpirun) ...")
+                result["cpu_baseline"] = cpu_baseline_reference(X, lab, Q, k, C,
+                                                                labels_auto.cpu().numpy())
+                result["cpu_baseline_port"] = port
+            except (OSError, RuntimeError, ValueError, subprocess.SubprocessError) as e:
+                log("reference baseline unavailable (%s); reporting the oracle port" % e)
     if rank == 0:
         print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def dry_run(args, kd, world, rank):
+    """Launcher + decomposition on CPU (gloo) with the torch stand-in: the
+    line carries n_gpus and a checksum of the gathered labels, value null."""
+    if world > 1:
+        dist.init_process_group("gloo")
+    n, m, d, k, C = args.n_train, args.queries, args.dim, args.k, args.classes
+    cpu = torch.device("cpu")
+    X, lab, Q, _ = synth(n, m * world, d, C, 1234, 5678, cpu, data=args.data)
+    kd.broadcast_train(X, lab)
+    q0, q1 = kd.shard_range(m * world, world, rank)
+    clf = CpuStandIn()
+    clf.set_train(X, lab, C)
+    out = {}
+
+    def step():
+        out["lab"] = clf.classify(Q[q0:q1], k)
+
+    el = kd.timed(step, args.steps, args.warmup, lambda: None, None)
+    labels = kd.gather_slices(out["lab"], m * world)
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "value": None, "unit": "queries/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (%s)" % args.data, "dry_run": True,
+            "note": "CPU plumbing check (torch stand-in, gloo); not a measurement",
+            "config": {"workload": "dry-run: %d train x %d queries per rank, d=%d, k=%d"
+                                   % (n, m, d, k), "parallelism": "query-sharded dp%d" % world},
+            "labels_sha1": hashlib.sha1(labels.numpy().astype(np.int32).tobytes()).hexdigest(),
+        }), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

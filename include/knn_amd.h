@@ -67,6 +67,9 @@ extern "C" {
 #define KNN_FLAG_TIE_VOTE 4     /* equal distances with different labels inside top-k */
 #define KNN_FLAG_TIE_ORDER 8    /* equal distances inside top-k (order unspecified in
                                    the reference's std::sort; ours: by train index) */
+#define KNN_FLAG_NONFINITE 16   /* the query has a NaN / inf coordinate: label -1, no
+                                   neighbours (idx -1, dist NaN); the reference's
+                                   distances are undefined there */
 
 typedef struct knn_ctx knn_ctx;
 typedef struct knn_group knn_group;
@@ -84,13 +87,17 @@ int knn_destroy(knn_ctx* ctx);
 
 /* Train set from host memory: X row-major n x d fp64 (Data_train, cpp:140),
  * labels (Train_label, cpp:141) with 0 <= label < class_cnt.  The library
- * copies both to HBM (≙ MPI_Bcast cpp:224-225). */
+ * copies both to HBM (≙ MPI_Bcast cpp:224-225).  KNN_ERR_ARG for a label out
+ * of range or a non-finite value (NaN / inf) anywhere in X. */
 int knn_set_train(knn_ctx* ctx, const double* X, const int32_t* labels, int64_t n,
                   int32_t d, int32_t class_cnt);
 /* Same from device memory on ctx's GPU (e.g. after an RCCL broadcast).
  * dX/dlabels are borrowed and must stay valid until the next set_train or
  * destroy.  idx_offset is added to every reported neighbour index (train
- * sharding: global index of this shard's first row). */
+ * sharding: global index of this shard's first row).  Labels and values are
+ * checked on the device (same errors as knn_set_train).  The work runs on
+ * the context's stream, which is ordered after the device's legacy default
+ * stream: producers on other streams must be synchronised by the caller. */
 int knn_set_train_device(knn_ctx* ctx, const double* dX, const int32_t* dlabels, int64_t n,
                          int32_t d, int32_t class_cnt, int64_t idx_offset);
 
@@ -102,8 +109,11 @@ int knn_classify(knn_ctx* ctx, const double* Q, int64_t m, int32_t k, int32_t me
                  int32_t* out_labels, int64_t* out_idx, double* out_dist,
                  int32_t* out_flags);
 /* Device-pointer variant; enqueued on `stream` (hipStream_t, NULL = ctx
- * stream).  Returns after enqueueing when no exact rescan is needed; may
- * synchronise the stream once to size the rescan. */
+ * stream) and returns without waiting for the device on every path: the
+ * exact rescan of uncertified queries is enqueued too and sized on the
+ * device.  Outputs are complete once the stream reaches the end of the call
+ * (knn_sync, or any later work on the same stream).  One stream at a time
+ * per context (the context's workspace is shared by its calls). */
 int knn_classify_device(knn_ctx* ctx, const double* dQ, int64_t m, int32_t k, int32_t metric,
                         int32_t* d_labels, int64_t* d_idx, double* d_dist, int32_t* d_flags,
                         void* stream);
@@ -147,13 +157,17 @@ int knn_normalize(knn_ctx* ctx, double* const* sets, const int64_t* rows, int32_
 /* Per-phase device timing with HIP events recorded on the stream the
  * kernels run on (off by default).  Phases: 0 = query prep, 1 = candidate
  * kernel (fused MFMA distance + top-R), 2 = merge/re-rank/vote, 3 = exact
- * rescan.  Values refer to the last classify/search call (0 if not run). */
+ * rescan.  knn_last_phase_ms: the last classify/search call (waits for it;
+ * -1 if none).  knn_timing_totals: per-phase sums over every timed call
+ * since the last reset, and their number (waits for them); reset != 0
+ * starts a new sum.  Recording never makes a call wait. */
 #define KNN_PHASE_PREP 0
 #define KNN_PHASE_CANDIDATE 1
 #define KNN_PHASE_RERANK 2
 #define KNN_PHASE_RESCAN 3
 int knn_set_timing(knn_ctx* ctx, int enable);
 double knn_last_phase_ms(knn_ctx* ctx, int phase);
+int knn_timing_totals(knn_ctx* ctx, double out_ms[4], int64_t* calls, int reset);
 /* Geometry of the last candidate launch: out[0]=workgroups, out[1]=splits
  * per query tile, out[2]=list entries per lane (R), out[3]=re-rank count C. */
 int knn_last_geometry(knn_ctx* ctx, int64_t out[4]);
@@ -177,6 +191,9 @@ int knn_set_precision(knn_ctx* ctx, int mode);
 /* Candidate kernel flavour of the last search: 0 fp32 L2, 1 fp32 L1, 2 bf16x3
  * L2 (32x32x16 MFMA), 3 bf16x3 L2 (16x16x32), 4 fp16 L2 (16x16x32). */
 int knn_last_candidate_path(knn_ctx* ctx);
+/* Name of the last candidate kernel launched, as rocprofv3 reports it
+ * without namespace, spaces and argument list (e.g. "cand_kernel<128,4,4,8>"). */
+const char* knn_last_kernel_name(knn_ctx* ctx);
 
 /* Tuning overrides for experiments (0 = automatic): "R" list entries per
  * lane (4, 8, 16), "S" train splits per query tile (1..64), "nw" waves per
@@ -189,8 +206,13 @@ int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value);
 
 /* Synchronise the context's stream. */
 int knn_sync(knn_ctx* ctx);
-/* Last classify's count of queries that needed the exact rescan. */
+/* Last classify's count of queries that needed the exact rescan (waits for
+ * that call; -1 on error). */
 int64_t knn_last_rescan_count(knn_ctx* ctx);
+/* Rescan counts summed over calls since the last reset: out[0] = queries
+ * that failed certification, out[1] = of those, queries finished by the full
+ * exact scan.  Waits for the context's work; reset != 0 zeroes the sums. */
+int knn_rescan_totals(knn_ctx* ctx, int64_t out[2], int reset);
 
 /* ---- single-process multi-GPU group over RCCL (xGMI) ---------------------
  * mode 0 = query-sharded: the train set is RCCL-broadcast from device

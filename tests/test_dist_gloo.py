@@ -125,3 +125,26 @@ def test_shard_ranges_cover_ragged():
             assert spans[0][0] == 0 and spans[-1][1] == n
             assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
             assert max(b - a for a, b in spans) - min(b - a for a, b in spans) <= 1
+
+
+def _bench_line(args):
+    import json
+    import subprocess
+    import sys
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args,
+                         capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+def test_bench_launches_its_own_ranks():
+    """bench.py --gpus 2 starts two ranks itself (torch.distributed.run as a
+    child, gloo in --dry-run): the line reports n_gpus 2 and the gathered
+    labels equal the one-rank run of the same total query set."""
+    common = ["--dry-run", "--n-train", "3000", "--dim", "24", "--steps", "2", "--warmup", "1"]
+    one = _bench_line(common + ["--gpus", "1", "--queries", "96"])
+    two = _bench_line(common + ["--gpus", "2", "--queries", "48"])
+    assert one["n_gpus"] == 1 and two["n_gpus"] == 2
+    assert two["dry_run"] and two["value"] is None
+    assert two["labels_sha1"] == one["labels_sha1"]

@@ -1,0 +1,124 @@
+"""configs[3] at full size: 100M train rows x 10k queries, d=96, k=10, L2,
+through the train-sharded building blocks of the C ABI on one GPU.
+
+The reference cannot run this configuration at all (int overflow of
+N_train*dim at cpp:140/249; 76.8 GB of fp64 per rank).  The 100M x 96 train
+set (fp64, 76.8 GB in HBM) is split into 4 shards of 25M rows; each shard
+gets its own context (knn_set_train_device with its global row offset) and
+returns its exact local top-(k+1) per query (knn_search_partial_device) into
+the [parts][m][w] layout an all-gather would produce; knn_merge_vote_device
+k-way merges them and votes (≙ cpp:324-337).  Checks:
+  * every query: the reported distances are the reference formula for the
+    reported rows (cpp:33-50, sequential fp64, recomputed on the host from
+    rows gathered on the GPU), ascending, distinct rows, first-to-max vote;
+  * optimality on a sample: the k distances equal the k smallest over all
+    100M rows of an independent fp64 brute force on the GPU (1e-10 rel);
+  * the oracle (oracle/knn_oracle.cpp) bit for bit on a sample of queries,
+    streamed over 4M-row chunks of the train set (each chunk's exact top-w,
+    merged by (dist, idx) -- the oracle restates cpp:33-50 + std::sort, whose
+    first w entries per chunk contain the chunk's part of the global top-w).
+Data: bench.synth (Gaussian mixture on the 8-bit grid k/256), seeded."""
+import numpy as np
+import pytest
+import torch
+
+import bench
+import oracle
+from test_gpu_fullsize import brute_force_kdist, vote
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def knn():
+    mod = bench.load_knn()
+    if mod.lib().knn_device_count() < 1:
+        pytest.fail("no HIP device visible: the KNN path has no CPU fallback")
+    return mod
+
+
+def ref_distances_gathered(X, Q, idx_t):
+    """cpp:33-50 for (query, reported row) pairs, rows gathered on the GPU
+    (77 GB stay in HBM), the sum formed on the host in reference order."""
+    rows = X[idx_t.reshape(-1)].reshape(idx_t.shape[0], idx_t.shape[1], X.shape[1]).cpu().numpy()
+    Qn = Q.cpu().numpy()
+    r = np.zeros(idx_t.shape, np.float64)
+    for j in range(Qn.shape[1]):
+        t = Qn[:, None, j] - rows[:, :, j]
+        r = r + t * t
+    return np.sqrt(r)
+
+
+def oracle_streamed(X, lab_all, Q, k, qs, chunk=4_000_000):
+    """Oracle top-k of queries qs over all rows, streamed in row chunks."""
+    w = k + 1
+    Qh = Q[qs].cpu().numpy()
+    dd, ii = [], []
+    for c0 in range(0, X.shape[0], chunk):
+        Xc = X[c0:c0 + chunk].cpu().numpy()
+        _, idx, dist = oracle.knn(Xc, lab_all[c0:c0 + chunk], Qh, w, True, int(lab_all.max()) + 1,
+                                  n_out=w, nthreads=16)
+        dd.append(dist)
+        ii.append(idx + c0)
+    dd, ii = np.concatenate(dd, 1), np.concatenate(ii, 1)
+    order = np.lexsort((ii, dd), axis=1)
+    dd = np.take_along_axis(dd, order, 1)[:, :k]
+    ii = np.take_along_axis(ii, order, 1)[:, :k]
+    return vote(lab_all[ii], k), ii, dd
+
+
+@pytest.mark.timeout(900)
+def test_cfg4_100m_train_sharded(knn):
+    n, m, d, k, C = 100_000_000, 10_000, 96, 10, 10
+    parts = 4
+    X, lab, Q, _ = bench.synth(n, m, d, C, 2468, 1357, DEV)
+    torch.cuda.synchronize()
+    w = k + 1
+    gd = torch.empty((parts, m, w), dtype=torch.float64, device=DEV)
+    gi = torch.empty((parts, m, w), dtype=torch.int64, device=DEV)
+    gl = torch.empty((parts, m, w), dtype=torch.int32, device=DEV)
+    paths = []
+    for p in range(parts):
+        r0, r1 = n * p // parts, n * (p + 1) // parts
+        c = knn.Classifier(0)
+        Xs, Ls = X[r0:r1], lab[r0:r1]
+        c.set_train_device(Xs.data_ptr(), Ls.data_ptr(), r1 - r0, d, C, idx_offset=r0,
+                           keep=(Xs, Ls))
+        c.search_partial_device(Q.data_ptr(), m, w, knn.L2, gd[p].data_ptr(), gi[p].data_ptr(),
+                                gl[p].data_ptr())
+        c.sync()
+        paths.append(c.last_candidate_path())
+        c.close()
+    assert paths == [4] * parts, "cfg4 shards should run the fp16 candidate pass"
+    ol = torch.empty(m, dtype=torch.int32, device=DEV)
+    oi = torch.empty((m, k), dtype=torch.int64, device=DEV)
+    od = torch.empty((m, k), dtype=torch.float64, device=DEV)
+    of = torch.empty(m, dtype=torch.int32, device=DEV)
+    mc = knn.Classifier(0)
+    mc.merge_vote_device(gd.data_ptr(), gi.data_ptr(), gl.data_ptr(), parts, m, w, k,
+                         ol.data_ptr(), oi.data_ptr(), od.data_ptr(), of.data_ptr())
+    mc.sync()
+    mc.close()
+    got, idx, dist = ol.cpu().numpy(), oi.cpu().numpy(), od.cpu().numpy()
+    assert idx.min() >= 0 and idx.max() < n
+    lab_all = lab.cpu().numpy()
+    # every query: reference distances of the reported rows, order, vote
+    want_d = ref_distances_gathered(X, Q, oi)
+    assert (want_d.view(np.int64) == dist.view(np.int64)).all(), "distances not bit-exact"
+    assert (np.diff(dist, axis=1) >= 0).all()
+    assert (np.diff(np.sort(idx, axis=1), axis=1) > 0).all()
+    np.testing.assert_array_equal(got, vote(lab_all[idx], k))
+    # optimality over all 100M rows on a sample
+    qs = np.arange(0, m, m // 64)
+    bf = brute_force_kdist(X, Q[qs], k)
+    np.testing.assert_allclose(dist[qs], bf, rtol=1e-10, atol=0)
+    # the oracle, bit for bit, on a few queries
+    qs = np.arange(0, m, m // 4)
+    wl, wi, wdd = oracle_streamed(X, lab_all, Q, k, qs)
+    np.testing.assert_array_equal(got[qs], wl)
+    assert (dist[qs].view(np.int64) == wdd.view(np.int64)).all()
+    for a, q in enumerate(qs):
+        for t in np.nonzero(idx[q] != wi[a])[0]:
+            assert (dist[q] == dist[q][t]).sum() > 1, "query %d: index differs without a tie" % q

@@ -221,3 +221,29 @@ def test_cfg4_train_sharded_merge(knn):
     check_optimal(X, Q, k, dist, np.arange(0, m, m // 128))
     for c in ctxs:
         c.close()
+
+
+def test_cfg2_full_continuous(knn):
+    """configs[1] on continuous data: the same mixture min-max normalised as
+    the reference does (cpp:229-306, over train and queries), no
+    quantisation -- values on no power-of-two grid, so the fp16 operands carry
+    a real representation error that the certified bound must absorb."""
+    n, m, d, k, C = 1_000_000, 10_000, 128, 10, 10
+    X, lab, Q, _ = bench.synth(n, m, d, C, 4242, 2424, DEV, data="continuous")
+    torch.cuda.synchronize()
+    clf = knn.Classifier(0)
+    clf.set_train_device(X.data_ptr(), lab.data_ptr(), n, d, C, keep=(X, lab))
+    got, idx, dist, flags = classify(knn, clf, Q, k)
+    assert clf.last_candidate_path() == 4
+    resc = clf.last_rescan_count()
+    assert resc * 16 <= m, "fp16 pass certified too few queries (%d rescans)" % resc
+    lab_all = lab.cpu().numpy()
+    check_properties(X, lab_all, Q, k, got, idx, dist, np.arange(m))
+    check_oracle(X, lab_all, Q, k, got, idx, dist, np.arange(0, m, m // 32))
+    check_optimal(X, Q, k, dist, np.arange(0, m, m // 512))
+    # the fp32 path gives the same exact answer
+    clf.set_precision(knn.PRECISION_FP32)
+    got32, _, dist32, _ = classify(knn, clf, Q, k)
+    np.testing.assert_array_equal(got32, got)
+    assert (dist32.view(np.int64) == dist.view(np.int64)).all()
+    clf.close()

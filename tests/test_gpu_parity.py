@@ -34,19 +34,16 @@ def knn():
     return mod
 
 
-@pytest.fixture(scope="module", params=["auto", "fp32", "m16", "fp16", "f16w", "f16l"])
+@pytest.fixture(scope="module", params=["auto", "fp32", "m16", "fp16"])
 def clf(knn, request):
     """Every parity test runs with the default candidate path (AUTO: fp16 for
     batches of >= 4096 queries at d <= 256, else bf16x3 on 32x32x16 for L2),
     with the fp32 path forced, with bf16x3 on the 16x16x32 MFMA layout forced,
-    and with the fp16 path forced (every batch size) on each of its MFMA
-    layouts (16x16x32 with 32 or 64 queries per wave, 32x32x16)."""
+    and with the fp16 path forced (every batch size)."""
     c = knn.Classifier(0)
     c.set_precision({"auto": knn.PRECISION_AUTO, "fp32": knn.PRECISION_FP32,
-                     "m16": knn.PRECISION_BF16X3, "fp16": knn.PRECISION_FP16,
-                     "f16w": knn.PRECISION_FP16, "f16l": knn.PRECISION_FP16}[request.param])
+                     "m16": knn.PRECISION_BF16X3, "fp16": knn.PRECISION_FP16}[request.param])
     c.set_tuning("mfma16", 1 if request.param == "m16" else -1)
-    c.set_tuning("f16layout", {"fp16": 0, "f16w": 1, "f16l": 2}.get(request.param, -1))
     yield c
     c.close()
 
@@ -277,7 +274,7 @@ def test_driver_matches_reference_outputs(tmp_path, knn):
                             Validation=s["Validation"])
         fx.write_inputs(str(d), names=(cfg.train_file_name, cfg.validation_file_name,
                                        cfg.test_file_name))
-        out = knn.run_reference_program(cfg, str(d))
+        out = knn.run_driver(cfg, str(d))
         labels = np.loadtxt(d / "Test_label.csv", dtype=np.int64, ndmin=1)
         np.testing.assert_array_equal(labels, fx.test_labels)
         if s["Validation"]:
@@ -298,3 +295,126 @@ def test_fp16_workgroup_sizes(knn, nw):
         c.set_tuning("nw", nw)
         run_case(c, knn, tr, lab, te, 10, 0, 6)
         c.close()
+
+
+def test_nonfinite_inputs(knn):
+    """NaN / inf: a train set holding one is refused (host and device entry
+    points; the reference's distances would be undefined for every query);
+    a query holding one gets label -1 and KNN_FLAG_NONFINITE with no
+    neighbours, and every other query of the batch is unaffected."""
+    import torch
+    rng = np.random.default_rng(23)
+    tr, lab, te = _mix(rng, 3000, 80, 32, 4)
+    c = knn.Classifier(0)
+    for bad in (np.nan, np.inf, -np.inf):
+        t2 = tr.copy()
+        t2[1234, 7] = bad
+        with pytest.raises(knn.KnnError, match="non-finite"):
+            c.set_train(t2, lab, 4)
+        dev = torch.device("cuda", 0)
+        Xd, Ld = torch.from_numpy(t2).to(dev), torch.from_numpy(lab).to(dev)
+        with pytest.raises(knn.KnnError, match="non-finite"):
+            c.set_train_device(Xd.data_ptr(), Ld.data_ptr(), 3000, 32, 4, keep=(Xd, Ld))
+    dev = torch.device("cuda", 0)
+    Xd, Ld = torch.from_numpy(tr).to(dev), torch.from_numpy(lab).to(dev)
+    Ld[17] = 4  # label out of range, checked on the device
+    with pytest.raises(knn.KnnError, match="labels outside"):
+        c.set_train_device(Xd.data_ptr(), Ld.data_ptr(), 3000, 32, 4, keep=(Xd, Ld))
+    te2 = te.copy()
+    te2[3, 0] = np.nan
+    te2[40, 31] = np.inf
+    for prec in (knn.PRECISION_AUTO, knn.PRECISION_FP32, knn.PRECISION_FP16):
+        c.set_precision(prec)
+        c.set_train(tr, lab, 4)
+        got, idx, dist, flags = c.classify(te2, 5, knn.L2, return_neighbors=True)
+        bad = np.array([3, 40])
+        assert (got[bad] == -1).all() and (flags[bad] & knn.FLAG_NONFINITE).all()
+        assert (idx[bad] == -1).all() and np.isnan(dist[bad]).all()
+        ok = np.setdiff1d(np.arange(te2.shape[0]), bad)
+        want, widx, wdist = oracle.knn(tr, lab, te2[ok], 5, True, 4, n_out=5)
+        np.testing.assert_array_equal(got[ok], want)
+        assert_neighbors_match(idx[ok], dist[ok], widx, wdist, flags[ok])
+    c.close()
+
+
+def test_rescan_paths_large_d(clf, knn):
+    """d > 256: uncertified queries go through the device-driven fast rescan
+    (fp32 filter reading the rows in place) and, with 400 duplicates of the
+    nearest row (more rows within reach than the fast path keeps), the full
+    exact scan; exact results either way."""
+    rng = np.random.default_rng(29)
+    tr, lab, te = _mix(rng, 3000, 64, 300, 4)
+    tr[1000:1400] = tr[5]
+    lab[1000:1400] = rng.integers(0, 4, 400)
+    te[:16] = tr[5]
+    got, want, flags = run_case(clf, knn, tr, lab, te, 9, 0, 4)
+    assert clf.last_rescan_count() >= 16
+    assert (flags[:16] & knn.FLAG_EXACT_RESCAN).all()
+    # heavy near-ties without exact duplicates: fast rescan finishes them
+    tr2 = tr.copy()
+    tr2[1000:1400] = tr[5] + rng.standard_normal((400, 300)) * 1e-9
+    run_case(clf, knn, tr2, lab, te, 9, 0, 4)
+
+
+def test_rescan_totals_and_async(knn):
+    """knn_classify_device returns without waiting for the device; the rescan
+    counts and phase times of a batch of calls are read back afterwards, and
+    the last call's outputs equal the host API's and the oracle's."""
+    import torch
+    rng = np.random.default_rng(31)
+    tr, lab, te = _mix(rng, 4000, 256, 64, 5)
+    tr[100:300] = tr[7]
+    te[:8] = tr[7]
+    dev = torch.device("cuda", 0)
+    c = knn.Classifier(0)
+    c.set_timing(True)
+    c.set_train(tr, lab, 5)
+    Q = torch.from_numpy(te).to(dev)
+    out = torch.empty(256, dtype=torch.int32, device=dev)
+    fl = torch.empty(256, dtype=torch.int32, device=dev)
+    c.rescan_totals(reset=True)
+    c.timing_totals(reset=True)
+    for _ in range(5):
+        c.classify_device(Q.data_ptr(), 256, 10, knn.L2, out.data_ptr(), d_flags=fl.data_ptr())
+    failed, full = c.rescan_totals(reset=True)
+    ms, calls = c.timing_totals(reset=True)
+    assert calls == 5 and all(v >= 0 for v in ms) and ms[1] > 0
+    assert failed >= 5 * 8 and 0 <= full <= failed
+    assert c.last_kernel_name().startswith("cand_")
+    got, idx, dist, flags = c.classify(te, 10, knn.L2, return_neighbors=True)
+    np.testing.assert_array_equal(out.cpu().numpy(), got)
+    np.testing.assert_array_equal(fl.cpu().numpy(), flags)
+    want, widx, wdist = oracle.knn(tr, lab, te, 10, True, 5, n_out=10)
+    untied = (flags & knn.FLAG_TIE_VOTE) == 0
+    np.testing.assert_array_equal(got[untied], want[untied])
+    assert_neighbors_match(idx, dist, widx, wdist, flags)
+    c.close()
+
+
+def test_group_two_gpus(knn):
+    """knn_group with 2 GPUs (RCCL broadcast / all-gather / all-reduce over
+    xGMI): both modes and the sharded normalisation against the oracle, with
+    ragged shards.  Skipped on a one-GPU box."""
+    if knn.lib().knn_device_count() < 2:
+        pytest.skip("needs 2 GPUs")
+    rng = np.random.default_rng(37)
+    tr, lab, te = _mix(rng, 5001, 333, 48, 6, grid=None)
+    va = te[::2].copy()
+    t_n, e_n, v_n = tr.copy(), te.copy(), va.copy()
+    oracle.normalize(t_n, e_n, v_n)
+    g = knn.Group([0, 1], 0)
+    g.normalize(tr, te, va)
+    for a, b in ((tr, t_n), (te, e_n), (va, v_n)):
+        assert a.tobytes() == b.tobytes()
+    want, widx, wdist = oracle.knn(tr, lab, te, 7, True, 6, n_out=7)
+    g.set_train(tr, lab, 6)
+    got, idx, dist, flags = g.classify(te, 7, knn.L2, return_neighbors=True)
+    np.testing.assert_array_equal(got, want)
+    assert_neighbors_match(idx, dist, widx, wdist, flags)
+    g.close()
+    g = knn.Group([0, 1], 1)
+    g.set_train(tr, lab, 6)
+    got, idx, dist, flags = g.classify(te, 7, knn.L2, return_neighbors=True)
+    np.testing.assert_array_equal(got, want)
+    assert_neighbors_match(idx, dist, widx, wdist, flags)
+    g.close()

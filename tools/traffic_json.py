@@ -11,11 +11,17 @@ TCC instances of a dispatch and averaged over dispatches.
 
 Usage: traffic_json.py <fetch-dir> <write-dir> <workload-json> > profiles/rN_traffic.json
   workload-json: '{"n_train":..,"queries":..,"dim":..,"k":..}' of the profiled run.
+The file records kernel_src_sha (bench.kernel_src_sha() of the tree that was
+profiled): bench.py cites a traffic file only for the same kernel build.
 """
 import collections
 import csv
 import json
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
 
 
 def per_launch(d, counter):
@@ -35,7 +41,7 @@ def main():
     fetch = per_launch(sys.argv[1], "FETCH_SIZE")
     write = per_launch(sys.argv[2], "WRITE_SIZE")
     wl = json.loads(sys.argv[3])
-    out = {"workload": wl, "formula": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE "
+    out = {"workload": wl, "kernel_src_sha": bench.kernel_src_sha(), "formula": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE "
            "half-count correction; KiB units)", "kernels": {}}
     for k in sorted(set(fetch) | set(write)):
         f, nf = fetch.get(k, (0.0, 0))

@@ -4,8 +4,7 @@
 Usage: python tools/tune.py [--rounds 5] [--n 1000000 --m 10000 --d 128 --k 10]
 Variants: "prec:R:S[:ablate[:nw]]" e.g. auto:0:0 fp32:8:0 auto:8:0:1:8
 (prec: auto | fp32 | bf16x3 | m16 = bf16x3 on the 16x16x32 MFMA layout | fp16
- = fp16 with 32 queries per wave | f16w = fp16 with 64 queries per wave
- | f16l = fp16 on the 32x32x16 MFMA)
+ = fp16 on the 16x16x32 MFMA)
 (ablate bits: 1 = no staging loads, 2 = no selection epilogue; timing only;
 nw = waves per candidate workgroup, 0 auto / 4 / 8)"""
 import argparse
@@ -27,11 +26,12 @@ def main():
     ap.add_argument("--m", type=int, default=10_000)
     ap.add_argument("--d", type=int, default=128)
     ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--data", default="grid", choices=("grid", "continuous"))
     ap.add_argument("variants", nargs="*", default=["auto:0:0", "auto:4:0", "auto:8:0", "fp32:0:0"])
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     knn = bench.load_knn()
-    X, lab, Q, _ = bench.synth(a.n, a.m, a.d, 10, 1234, 5678, dev)
+    X, lab, Q, _ = bench.synth(a.n, a.m, a.d, 10, 1234, 5678, dev, data=a.data)
     clf = knn.Classifier(0)
     clf.set_train_device(X.data_ptr(), lab.data_ptr(), a.n, a.d, 10, keep=(X, lab))
     clf.set_timing(True)
@@ -42,8 +42,7 @@ def main():
     ph = {}
     info = {}
     prec = {"auto": knn.PRECISION_AUTO, "fp32": knn.PRECISION_FP32, "bf16x3": knn.PRECISION_BF16X3,
-            "m16": knn.PRECISION_BF16X3, "fp16": knn.PRECISION_FP16,
-            "f16w": knn.PRECISION_FP16, "f16l": knn.PRECISION_FP16}
+            "m16": knn.PRECISION_BF16X3, "fp16": knn.PRECISION_FP16}
     for r in range(a.rounds + 1):
         for v in a.variants:
             parts = v.split(":")
@@ -53,7 +52,6 @@ def main():
             clf.set_tuning("nw", nw)
             clf.set_precision(prec[p])
             clf.set_tuning("mfma16", 1 if p == "m16" else (0 if p == "bf16x3" else -1))
-            clf.set_tuning("f16layout", {"fp16": 0, "f16w": 1, "f16l": 2}.get(p, -1))
             clf.set_tuning("R", int(R))
             clf.set_tuning("S", int(S))
             clf.set_tuning("ablate", abl)
