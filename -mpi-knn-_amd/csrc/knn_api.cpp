@@ -266,17 +266,47 @@ static int ensure_fp16(knn_ctx* ctx, hipStream_t s) {
   return KNN_OK;
 }
 
-// fp16 candidate pass (kernel metric 4): PRECISION_FP16, or AUTO for batches
-// of >= 4096 queries (8-wave workgroups) until a batch certifies poorly.
+// The fp16 S3 image (d > 256, cand_s3_kernel<R, true>): 2^jx (x - mu) in
+// fp16 tile-chunk images + the L2 seeds; the representation error measured
+// as for the resident copy.
+static int ensure_fp16_s3(knn_ctx* ctx, hipStream_t s) {
+  const TrainDev& t = ctx->train;
+  const int DPs = pad_dim_fp16_s3(t.d);
+  if (DPs <= 0) return knn_fail(KNN_ERR_ARG, "fp16 S3 path needs d > 256");
+  if (ctx->DPs == DPs) return KNN_OK;
+  int rc;
+  const int64_t n3 = (t.n + kS3Rows - 1) / kS3Rows * kS3Rows;
+  if ((rc = ctx->XT16.ensure((size_t)n3 * DPs * 2))) return rc;
+  if ((rc = ctx->XS16.ensure((size_t)n3 * sizeof(float)))) return rc;
+  unsigned long long* st_d = (unsigned long long*)ctx->stats.p + 3;
+  HIP_TRY(hipMemsetAsync(st_d, 0, 8, s));
+  launch_prep_half_tiled(t.X64, t.mu, t.n, t.d, DPs, n3, t.jx, 1.0, (unsigned short*)ctx->XT16.p,
+                         t.xinit_l2, (float*)ctx->XS16.p, nullptr, st_d, s);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(ctx->h_stats + 3, st_d, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  double dx2;
+  memcpy(&dx2, &ctx->h_stats[3], 8);
+  ctx->train.dxmax = std::sqrt(dx2) * (1.0 + 1e-12) + 0x1p-50 * std::sqrt(t.x2max);
+  ctx->DPs = DPs;
+  return KNN_OK;
+}
+
+// fp16 candidate pass (kernel metric 4): PRECISION_FP16, or AUTO -- at
+// d <= 256 for batches of >= 4096 queries (8-wave workgroups of the resident
+// kernel), at d > 256 (S3 kernel) always -- until a batch certifies poorly.
 // Tuning key "fp16": -1 auto, 0 off, 1 on.
 // (W > kQuadMaxW: the R = 4 lists of the 16x16 layouts would overflow too
 // often -- AUTO keeps those for the 32x32 bf16x3 kernel with R = 8/16 lists)
 constexpr int kQuadMaxW = 64;
 static bool use_fp16(const knn_ctx* ctx, int metric, int64_t m, int W) {
-  if (metric != KNN_METRIC_L2 || pad_dim_fp16(ctx->train.d) <= 0) return false;
+  if (metric != KNN_METRIC_L2) return false;
+  const bool streamed = pad_dim_fp16_s3(ctx->train.d) > 0;
+  if (!streamed && pad_dim_fp16(ctx->train.d) <= 0) return false;
   if (ctx->tune_fp16 >= 0) return ctx->tune_fp16 > 0;
   if (ctx->precision == KNN_PRECISION_FP16) return true;
-  return ctx->precision == KNN_PRECISION_AUTO && !ctx->fp16_off && m >= 4096 && W <= kQuadMaxW;
+  if (ctx->precision != KNN_PRECISION_AUTO || ctx->fp16_off) return false;
+  return streamed || (m >= 4096 && W <= kQuadMaxW);
 }
 
 static bool use_bf16x3(const knn_ctx* ctx, int metric) {
@@ -333,11 +363,11 @@ int knn_set_train_device(knn_ctx* ctx, const double* dX, const int32_t* dlabels,
 // kernel (occupancy x CUs): a mostly-empty final round costs up to a whole
 // workgroup duration.  The union of the 2S lists must hold the C re-rank
 // candidates; R grows to 16 when the expected per-list share of C is large.
-static void choose_geometry(knn_ctx* ctx, int metric, int DP, int nw, int n_qt, int64_t n_tiles,
-                            int W, int C, int& S_out, int& R_out) {
+static void choose_geometry(knn_ctx* ctx, int metric, bool streamed, int DP, int nw, int n_qt,
+                            int64_t n_tiles, int W, int C, int& S_out, int& R_out) {
   const int S_hi = (int)std::max<int64_t>(1, std::min<int64_t>(64, n_tiles));
   int bestS = 1, bestR = 8;
-  const bool quad = metric == 3 || metric == 4;  // 16x16 layouts
+  const bool quad = !streamed && (metric == 3 || metric == 4);  // 16x16 layouts
   const int lps = quad ? 4 : 2;  // lists per query per split
   for (int R : {4, 8, 16}) {
     // kernel metrics 3, 4 (16x16x32 layout) have R = 4 only; elsewhere R = 4
@@ -451,11 +481,18 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   // candidate-pass flavour: kmetric 4 = L2 via fp16 MFMA, 2/3 = bf16x3, else fp32
   int kmetric = metric, DP = t.DP;
   const float* Xk = t.X32;
+  bool s3h = false;  // fp16 on the S3 stream kernel (d > 256)
   if (use_fp16(ctx, metric, m, W)) {
-    if ((rc = ensure_fp16(ctx, s))) return rc;
     kmetric = 4;
-    DP = ctx->DPh;
-    Xk = (const float*)ctx->XH.p;
+    if (pad_dim_fp16(t.d) > 0) {
+      if ((rc = ensure_fp16(ctx, s))) return rc;
+      DP = ctx->DPh;
+      Xk = (const float*)ctx->XH.p;
+    } else {
+      if ((rc = ensure_fp16_s3(ctx, s))) return rc;
+      DP = ctx->DPs;
+      s3h = true;
+    }
   } else if (use_bf16x3(ctx, metric)) {
     if ((rc = ensure_bf16x3(ctx, s))) return rc;
     kmetric = 2;
@@ -465,7 +502,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   // waves per workgroup of the resident kernel: 8 (256 queries share each
   // staged tile) when there are enough queries, else 4; the large-d fp32
   // stream kernel always takes 128 queries, the bf16x3 one (S3) 256
-  const bool s3 = kmetric == 2 && bf16x3_streamed(DP);
+  const bool s3 = (kmetric == 2 && bf16x3_streamed(DP)) || s3h;
   // bf16x3 on the 16x16x32 MFMA layout (resident kernel, 8 waves, DP % 32 ==
   // 0): kernel metric 3, R = 4 lists, 4 lists per split.  Tuning key
   // "mfma16": -1 auto (on for batches of >= 4096 queries), 0 off, 1 on.
@@ -474,7 +511,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   int nw = 4;
   if (DP <= 256 && kmetric != 1) nw = ctx->tune_nw ? std::min(ctx->tune_nw, 8) : (m >= 4096 ? 8 : 4);
   if (kmetric >= 3) nw = 8;
-  if (kmetric == 4 && ctx->tune_nw) nw = ctx->tune_nw;  // 4, 8 or 16
+  if (kmetric == 4 && !s3 && ctx->tune_nw) nw = ctx->tune_nw;  // 4, 8 or 16
   if (s3) nw = 8;
   const int qpb = s3 ? kS3Rows : (DP <= 256 ? 32 * nw : kQPB);
   const int n_qt = (int)((m + qpb - 1) / qpb);
@@ -484,8 +521,8 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   int C = (int)std::min<int64_t>(t.n, std::max(2 * W, W + 16));
   C = std::min(C, kMaxUnion);
   int S = 1, R = 8;
-  choose_geometry(ctx, kmetric, DP, nw, n_qt, n_tiles, W, C, S, R);
-  const bool quad_lists = kmetric == 3 || kmetric == 4;  // 16x16 layouts: 4 lists per split
+  choose_geometry(ctx, kmetric, s3, DP, nw, n_qt, n_tiles, W, C, S, R);
+  const bool quad_lists = !s3 && (kmetric == 3 || kmetric == 4);  // 16x16: 4 lists per split
   if (quad_lists) R = 4;
   const int NL = (quad_lists ? 4 : 2) * S;
   C = std::min(C, NL * R);
@@ -515,7 +552,8 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   ctx->last_nw = nw;
   ctx->geom[3] = C;
   if (s3)
-    snprintf(ctx->last_kernel, sizeof ctx->last_kernel, "cand_s3_kernel<%d>", R);
+    snprintf(ctx->last_kernel, sizeof ctx->last_kernel, "cand_s3_kernel<%d,%s>", R,
+             s3h ? "true" : "false");
   else if (DP <= 256)
     snprintf(ctx->last_kernel, sizeof ctx->last_kernel, "cand_kernel<%d,%d,%d,%d>", DP, R, kmetric,
              nw);
@@ -531,7 +569,10 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   float* qvalid = (float*)ctx->qvalid.p;
   launch_query_check(dQ, t.mu, m, t.d, m_pad, qscale, t.jx,
                      kmetric == 4 ? 65000.0 : std::ldexp(1.0, 100), qvalid, s);
-  if (s3)
+  if (s3h)
+    launch_prep_half_tiled(dQ, t.mu, m, t.d, DP, m_pad, t.jx, -2.0, (unsigned short*)ctx->Q32.p,
+                           nullptr, nullptr, qvalid, nullptr, s);
+  else if (s3)
     launch_prep_split_tiled(dQ, t.mu, m, t.d, DP, m_pad, std::ldexp(qscale, t.jx),
                             (unsigned short*)ctx->Q32.p, nullptr, nullptr, s);
   else if (kmetric == 4)
@@ -559,7 +600,11 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   cl.nw = nw;
   cl.gthr = use_gthr ? (uint32_t*)ctx->gthr.p : nullptr;
   if (use_gthr) launch_fill_i32((int32_t*)ctx->gthr.p, m_pad * 4, (int32_t)kGthrInit, s);
-  if (s3)
+  if (s3h)
+    launch_cand_s3h((const unsigned short*)ctx->XT16.p, (const float*)ctx->XS16.p,
+                    (const unsigned short*)ctx->Q32.p, DP, n_pad3, R, S, n_qt, cl.out_v, cl.out_i,
+                    cl.ablate, s);
+  else if (s3)
     launch_cand_s3((const unsigned short*)ctx->XB.p, (const float*)ctx->XS.p,
                    (const unsigned short*)ctx->Q32.p, DP, n_pad3, R, S, n_qt, cl.out_v, cl.out_i,
                    cl.ablate, s);
@@ -570,8 +615,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   HIP_TRY(hipMemsetAsync(ctx->rescan_cnt.p, 0, 4 * sizeof(int), s));
   launch_merge_rerank(metric, (const float*)ctx->cand_v.p, (const int*)ctx->cand_i.p, NL, R, t, dQ,
                       m, W, C, err_factor(kmetric, DP),
-                      kmetric == 4 ? ProxyScale{qvalid, 0x1p-14, 0x1p-28,
-                                                (const unsigned short*)ctx->Q32.p, DP}
+                      kmetric == 4 ? ProxyScale{qvalid, 0x1p-14, 0x1p-28, true}
                                    : ProxyScale{qvalid, 0x1p-125, 0x1p-124},
                       cl.gthr, sink, (int*)ctx->rescan_q.p,
                       (double*)ctx->rescan_tau.p, (int*)ctx->rescan_cnt.p, s);
@@ -589,8 +633,10 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   rb.slow_q = (int*)ctx->slow_q.p;
   rb.counts = ctx->d_counts;
   rb.totals = (unsigned long long*)ctx->totals.p;
-  launch_rescan(metric, t, dQ, rb, cap, W, err_factor(metric, t.DP), sink,
-                (int)std::min<int64_t>(m, ctx->cu_count), s);
+  // (timing-only ablations leave every query uncertified: no rescan then)
+  const bool abl = ctx->tune_ablate & 11;
+  launch_rescan(metric, t, dQ, rb, abl ? 0 : cap, W, err_factor(metric, t.DP), sink,
+                abl ? 0 : (int)std::min<int64_t>(m, ctx->cu_count), s);
   HIP_TRY(hipGetLastError());
   if (tc) HIP_TRY(hipEventRecord(tc->ev[4], s));
   HIP_TRY(hipEventRecord(ctx->done_ev, s));

@@ -60,7 +60,7 @@ struct knn_ctx {
   int64_t tcalls = 0;
   int64_t geom[4] = {0, 0, 0, 0};
   // train-side HBM
-  DevBuf X64_own, lab_own, X32, xl2, xl1, stats, XB, XS, XH, mu, mu_part;
+  DevBuf X64_own, lab_own, X32, xl2, xl1, stats, XB, XS, XH, XT16, XS16, mu, mu_part;
   // per-classify workspace
   DevBuf Q64, Q32, qvalid, cand_v, cand_i, gthr, rescan_q, rescan_tau, rescan_cnt, fr_cnt, fr_buf,
       fr_q, fr_thr, slow_q, totals;
@@ -70,7 +70,7 @@ struct knn_ctx {
   DevBuf nrm_part, nrm_mm, nrm_X;
   std::vector<DevBuf*> all_bufs() {
     return {&X64_own, &lab_own, &X32,   &xl2,   &xl1,    &stats,  &XB,       &XS,
-            &XH,      &mu,      &mu_part, &Q64, &Q32,    &qvalid, &cand_v,   &cand_i,
+            &XH,      &XT16,    &XS16,  &mu,      &mu_part, &Q64, &Q32,    &qvalid, &cand_v,   &cand_i,
             &gthr,    &rescan_q, &rescan_tau, &rescan_cnt, &fr_cnt, &fr_buf, &fr_q, &fr_thr,
             &slow_q,  &totals,  &o_lab, &o_idx, &o_dist, &o_flags, &nrm_part, &nrm_mm, &nrm_X};
   }

@@ -213,7 +213,27 @@ cand_stream_kernel(const float* __restrict__ X32, const float* __restrict__ xini
 // (lanes on rows {0-3,12-15,20-27} etc.) touch 16 distinct 16-B bank groups.
 // Seeds (fl32 ||x32||^2, +inf on pad rows) travel as one 1-KiB piece with
 // chunk 0 of each tile.
-template <int R>
+//
+// F16 (cand_s3h_kernel, the fp16 candidate pass at d > 256): the same images
+// with a chunk of 32 dims in fp16 -- slots {k0-7, k8-15, k16-23, k24-31} --
+// and two v_mfma_f32_32x32x16_f16 per block and chunk (one per 16 dims,
+// products exact in fp32) instead of three bf16 ones per 16 dims: 3x fewer
+// MFMAs per algorithmic flop and half the staged bytes per MFMA.
+#ifndef KNN_S3_NB
+#define KNN_S3_NB 4
+#endif
+// s_waitcnt vmcnt(n) + s_barrier with a run-time n (vmcnt takes an immediate)
+__device__ __forceinline__ void s3_wait_barrier(int n) {
+  switch (n) {
+#define KNN_W(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")\n\ts_barrier" ::: "memory"); break;
+    KNN_W(1) KNN_W(2) KNN_W(3) KNN_W(4) KNN_W(5) KNN_W(6) KNN_W(7) KNN_W(8) KNN_W(9) KNN_W(10)
+    KNN_W(11) KNN_W(12) KNN_W(13) KNN_W(14) KNN_W(15)
+#undef KNN_W
+    default: asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+}
+
+template <int R, bool F16>
 __global__ void __launch_bounds__(512)
 cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* QT, int nch,
                int n_tiles, int S, int n_qt, float* __restrict__ out_v, int* __restrict__ out_i,
@@ -222,7 +242,9 @@ cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* 
   // first steps, bit1 no selection epilogue); 0 in production.
   constexpr int BLK = kS3R * 64;        // bytes of one operand image
   constexpr int BUFB = 2 * BLK + 1024;  // A (rows) | B (queries) | seeds
-  constexpr int NB = 3;
+  constexpr int NB = KNN_S3_NB;  // LDS buffers: prefetch distance NB - 1 steps
+  constexpr int PD = NB - 1;
+  static_assert(4 * (PD - 1) + PD <= 15, "vmcnt wait range");
   __shared__ __attribute__((aligned(16))) unsigned char lds[NB * BUFB];
 
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -256,7 +278,7 @@ cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* 
     glds16(gB + (wv + 8) * 1024, l + BLK + (wv + 8) * 1024);
     if (ic == 0 && wv == 0)
       glds16((const char*)(XS + (int64_t)itile * kS3R) + lane * 16, l + 2 * BLK);
-    if (++ic == nch) { ic = 0; itile += S; }
+    if (++ic == nch) { ic = 0; itile += (abl & 8) ? 0 : S; }  // abl bit 3: see cand_kernel
     if (++ib == NB) ib = 0;
   };
 
@@ -266,8 +288,9 @@ cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* 
   for (int t = 0; t < R; ++t) { L[t] = KNN_INF_F; I[t] = -1; }
   float thr = KNN_INF_F;
 
-  if (total > 0) issue();
-  if (total > 1) issue();
+#pragma unroll
+  for (int p = 0; p < PD; ++p)
+    if (total > p) issue();
 
   f32x16 acc[8];
   int c = 0, t = split, cb = 0;
@@ -275,16 +298,18 @@ cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* 
     // own pieces of step st landed (those of st+1 may still be in flight),
     // then the barrier publishes every wave's pieces and retires all reads
     // of the buffer that the issue below refills.
-    if (st + 1 < total) {
-      if (wv == 0 && c + 1 == nch)
-        asm volatile("s_waitcnt vmcnt(5)\n\ts_barrier" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    // (the younger steps st+1 .. st+y stay in flight: 4 pieces each, wave 0
+    // one more -- the seeds -- for a step that opens a tile)
+    {
+      const int y = min(PD - 1, total - 1 - st);
+      int n = 4 * y;
+      if (wv == 0)
+        for (int jj = 1; jj <= y; ++jj) n += (c + jj) % nch == 0;
+      if (abl & 1) n = 0;
+      s3_wait_barrier(n);
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (st + 2 < total && !(abl & 1)) issue();
+    if (st + PD < total && !(abl & 1)) issue();
 
     const unsigned char* buf = lds + cb * BUFB;
     if (c == 0) {
@@ -301,15 +326,28 @@ cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* 
         }
       }
     }
-    const bf16x8 bh = *(const bf16x8*)(buf + BLK + off_q + off_hi);
-    const bf16x8 bl = *(const bf16x8*)(buf + BLK + off_q + off_lo);
+    if constexpr (F16) {
+      // k-step 0 = dims 0-15 of the chunk (slots 0, 1), k-step 1 = 16-31 (2, 3)
+      const f16x8 b0 = *(const f16x8*)(buf + BLK + off_q + off_hi);
+      const f16x8 b1 = *(const f16x8*)(buf + BLK + off_q + off_lo);
 #pragma unroll
-    for (int bb = 0; bb < 8; ++bb) {
-      const bf16x8 ah = *(const bf16x8*)(buf + bb * 32 * 64 + off_hi);
-      const bf16x8 al = *(const bf16x8*)(buf + bb * 32 * 64 + off_lo);
-      acc[bb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[bb], 0, 0, 0);
-      acc[bb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[bb], 0, 0, 0);
-      acc[bb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[bb], 0, 0, 0);
+      for (int bb = 0; bb < 8; ++bb) {
+        const f16x8 a0 = *(const f16x8*)(buf + bb * 32 * 64 + off_hi);
+        const f16x8 a1 = *(const f16x8*)(buf + bb * 32 * 64 + off_lo);
+        acc[bb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, acc[bb], 0, 0, 0);
+        acc[bb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b1, acc[bb], 0, 0, 0);
+      }
+    } else {
+      const bf16x8 bh = *(const bf16x8*)(buf + BLK + off_q + off_hi);
+      const bf16x8 bl = *(const bf16x8*)(buf + BLK + off_q + off_lo);
+#pragma unroll
+      for (int bb = 0; bb < 8; ++bb) {
+        const bf16x8 ah = *(const bf16x8*)(buf + bb * 32 * 64 + off_hi);
+        const bf16x8 al = *(const bf16x8*)(buf + bb * 32 * 64 + off_lo);
+        acc[bb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[bb], 0, 0, 0);
+        acc[bb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[bb], 0, 0, 0);
+        acc[bb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[bb], 0, 0, 0);
+      }
     }
     if (c == nch - 1) {
       if (!(abl & 2)) {
@@ -354,8 +392,20 @@ int pad_dim_fp16(int d) {
   return (DP <= 256 && DP % 32 == 0) ? DP : -1;
 }
 
+// fp16 S3 kernel above 256 dims: any multiple of 32
+int pad_dim_fp16_s3(int d) {
+  const int DP = (d + 31) / 32 * 32;
+  return DP > 256 ? DP : -1;
+}
+
 int s3_blocks_per_cu(int R) {
-  return R == 8 ? occupancy_of(cand_s3_kernel<8>, 512) : occupancy_of(cand_s3_kernel<16>, 512);
+  return R == 8 ? occupancy_of(cand_s3_kernel<8, false>, 512)
+                : occupancy_of(cand_s3_kernel<16, false>, 512);
+}
+
+int s3h_blocks_per_cu(int R) {
+  return R == 8 ? occupancy_of(cand_s3_kernel<8, true>, 512)
+                : occupancy_of(cand_s3_kernel<16, true>, 512);
 }
 
 void launch_cand_s3(const unsigned short* XT, const float* XS, const unsigned short* QT, int DP,
@@ -364,11 +414,24 @@ void launch_cand_s3(const unsigned short* XT, const float* XS, const unsigned sh
   const int nch = DP / kS3DC;
   const int n_tiles = (int)(n_pad / kS3R);
   if (R == 8)
-    hipLaunchKernelGGL(cand_s3_kernel<8>, dim3((unsigned)(n_qt * S)), dim3(512), 0, s, XT, XS, QT,
-                       nch, n_tiles, S, n_qt, out_v, out_i, ablate);
+    hipLaunchKernelGGL((cand_s3_kernel<8, false>), dim3((unsigned)(n_qt * S)), dim3(512), 0, s, XT,
+                       XS, QT, nch, n_tiles, S, n_qt, out_v, out_i, ablate);
   else
-    hipLaunchKernelGGL(cand_s3_kernel<16>, dim3((unsigned)(n_qt * S)), dim3(512), 0, s, XT, XS, QT,
-                       nch, n_tiles, S, n_qt, out_v, out_i, ablate);
+    hipLaunchKernelGGL((cand_s3_kernel<16, false>), dim3((unsigned)(n_qt * S)), dim3(512), 0, s, XT,
+                       XS, QT, nch, n_tiles, S, n_qt, out_v, out_i, ablate);
+}
+
+void launch_cand_s3h(const unsigned short* XT, const float* XS, const unsigned short* QT, int DP,
+                     int64_t n_pad, int R, int S, int n_qt, float* out_v, int* out_i, int ablate,
+                     hipStream_t s) {
+  const int nch = DP / 32;
+  const int n_tiles = (int)(n_pad / kS3R);
+  if (R == 8)
+    hipLaunchKernelGGL((cand_s3_kernel<8, true>), dim3((unsigned)(n_qt * S)), dim3(512), 0, s, XT,
+                       XS, QT, nch, n_tiles, S, n_qt, out_v, out_i, ablate);
+  else
+    hipLaunchKernelGGL((cand_s3_kernel<16, true>), dim3((unsigned)(n_qt * S)), dim3(512), 0, s, XT,
+                       XS, QT, nch, n_tiles, S, n_qt, out_v, out_i, ablate);
 }
 
 template <int R, int METRIC>
@@ -380,6 +443,7 @@ static void launch_str(const CandLaunch& c, hipStream_t s) {
 
 int cand_blocks_per_cu(int metric, int DP, int R, int nw) {
   if (metric == 2 && bf16x3_streamed(DP)) return s3_blocks_per_cu(R);
+  if (metric == 4 && DP > 256) return s3h_blocks_per_cu(R);
 #define KNN_CASE(v) if (DP == v) return blocks_res_##v(R, metric, nw);
   KNN_DP_LIST(KNN_CASE)
 #undef KNN_CASE

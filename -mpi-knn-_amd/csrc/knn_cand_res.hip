@@ -22,6 +22,9 @@ static_assert(KNN_RES_TPB * knnk::kTR == knnk::kResTileRows || KNN_RES_TPB != 2,
 #ifndef KNN_M4_TE_CACHE
 #define KNN_M4_TE_CACHE 1
 #endif
+#ifndef KNN_SETPRIO
+#define KNN_SETPRIO 0
+#endif
 #ifndef KNN_M4_SEED4
 #define KNN_M4_SEED4 1
 #endif
@@ -97,6 +100,11 @@ __attribute__((amdgpu_waves_per_eu((METRIC == 4 ? DP / 2 : DP) <= 160 && R <= 8 
 cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
             int n_qt, float* __restrict__ out_v, int* __restrict__ out_i, int abl,
             uint32_t* gthr) {
+#if KNN_SETPRIO
+  // the second-dispatched half of the workgroup at priority 1 (MI355X_MICROARCH
+  // "Two waves per SIMD", item 4)
+  if ((threadIdx.x >> 6) >= NW / 2) __builtin_amdgcn_s_setprio(1);
+#endif
   // Q32 is deliberately not __restrict__: with it hipcc treats the query
   // fragments as invariant and re-loads them inside the tile loop instead of
   // keeping them in VGPRs (its waits would then also drain the LDS-DMA queue).
@@ -271,7 +279,9 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
         wait_barrier_x<0>(extra);
       }
       __builtin_amdgcn_sched_barrier(0);
-      if (it + PD < my_nt && !(abl & 1)) KNN_ISSUE(t + PD * S, nxt);
+      // (abl bit 3: the same pieces, always of the split's first tile -- DMA
+      // issue cost without the data stream; timing only)
+      if (it + PD < my_nt && !(abl & 1)) KNN_ISSUE((abl & 8) ? split : t + PD * S, nxt);
       if (gthr) {
         if (x_age == PD) {
 #pragma unroll

@@ -134,6 +134,13 @@ __device__ __forceinline__ void split_bf16(double x, unsigned short& hi, unsigne
   lo = __builtin_bit_cast(unsigned short, l);
 }
 
+// The fp16 candidate operand of an fp64 value: one rounding of v * 2^jx.
+// Shared by every fp16 image builder and by the merge, which rebuilds a
+// query's operands to measure their representation error.
+__device__ __forceinline__ _Float16 f16_operand(double v, int jx) {
+  return (_Float16)__builtin_ldexp(v, jx);
+}
+
 // ------------------------------------------------------- candidate kernel
 // Sorted insertion of v (< L[R-1]) into the ascending register list (L, I);
 // the previous last entry drops out.  Fully unrolled: no dynamic register

@@ -63,6 +63,20 @@ void launch_cand_s3(const unsigned short* XT, const float* XS, const unsigned sh
 void launch_prep_split_tiled(const double* X64, const double* mu, int64_t n, int d, int DP,
                              int64_t n_pad, double scale, unsigned short* out,
                              const float* seed_src, float* seed_out, hipStream_t s);
+// fp16 S3 kernel (DP > 256, DP % 32 == 0): XT/QT made by launch_prep_half_tiled
+void launch_cand_s3h(const unsigned short* XT, const float* XS, const unsigned short* QT, int DP,
+                     int64_t n_pad, int R, int S, int n_qt, float* out_v, int* out_i, int ablate,
+                     hipStream_t s);
+int s3h_blocks_per_cu(int R);
+int pad_dim_fp16_s3(int d);         // padded dim of the fp16 S3 image (multiple of 32, > 256)
+// fp64 rows -> fp16 S3 tile-chunk images of mult * 2^jx (x - mu) (knn_prep.hip);
+// train: seed_out[row] = seed_src[row] (+inf on pad rows) and the running max
+// of the rows' squared representation error in dx2max; queries: seed_out =
+// dx2max = null, valid[row] <= 0 -> zero operands
+void launch_prep_half_tiled(const double* X64, const double* mu, int64_t n, int d, int DP,
+                            int64_t n_pad, int jx, double mult, unsigned short* out,
+                            const float* seed_src, float* seed_out, const float* valid,
+                            unsigned long long* dx2max, hipStream_t s);
 bool cand_supported(int DP);
 int cand_tile_rows(int DP);         // train rows per tile of the kernel serving DP
 int cand_blocks_per_cu(int metric, int DP, int R, int nw);  // resident workgroups per CU
@@ -108,14 +122,13 @@ bool launch_cand(const CandLaunch& c, hipStream_t s);
 // query's operands left the format's range, its proxies are void (exact
 // rescan).  ue / up: absolute error per operand element / per product in
 // scaled units, for values outside the format's normal range.
-// qh (fp16 pass, else null): the query operands actually used, rows of
-// qh_stride halves of -2 * 2^jx (q - mu); the merge measures their
-// representation error instead of assuming the format's worst case.
+// f16: the candidate pass ran on fp16 operands; the merge measures each
+// query's representation error (rebuilding its operand's rounding) instead
+// of assuming the format's worst case.
 struct ProxyScale {
   const float* valid;
   double ue, up;
-  const unsigned short* qh = nullptr;
-  int qh_stride = 0;
+  bool f16 = false;
 };
 void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int R,
                          const TrainDev& t, const double* Q64, int64_t m, int W, int C,

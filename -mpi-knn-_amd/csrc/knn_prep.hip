@@ -278,7 +278,7 @@ prep_half_train_kernel(const double* __restrict__ X64, const double* __restrict_
       _Float16 h = (_Float16)0.0f;
       if (row < n && c < d) {
         const double x = X64[row * d + c] - mu[c];
-        h = (_Float16)__builtin_ldexp(x, jx);
+        h = f16_operand(x, jx);
         const double e = (double)h * sinv - x;
         e2 += e * e;
       }
@@ -329,7 +329,7 @@ prep_half_queries_kernel(const double* __restrict__ Q64, const double* __restric
     const int c = (int)(e - row * DP);
     _Float16 h = (_Float16)0.0f;
     if (row < m && c < d && valid[row] > 0.0f)
-      h = (_Float16)__builtin_ldexp(-2.0 * (Q64[row * d + c] - mu[c]), jx);
+      h = f16_operand(-2.0 * (Q64[row * d + c] - mu[c]), jx);
     out[e] = __builtin_bit_cast(unsigned short, h);
   }
 }
@@ -352,6 +352,73 @@ void launch_fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t s) {
   int64_t blocks = (n + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(fill_i32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p, n, v);
+}
+
+// ------------------------------- fp16 S3 images (DP > 256; cand_s3h_kernel)
+// Tile-chunk images: block (tile of kS3R rows, chunk of 32 dims) = kS3R rows
+// x 64 B, the four 16-B slots of row r (dims 0-7, 8-15, 16-23, 24-31 of the
+// chunk) at slot position s ^ ((r >> 2) & 3) -- the bf16x3 S3 layout with
+// one fp16 k-step of 16 dims in place of each hi/lo pair.  One wave per row,
+// lane g < DP/8 converting dims 8g .. 8g+7 of mult * (x - mu) at scale 2^jx.
+// Train (mult 1): the row's representation error ||h / 2^jx - (x - mu)||^2
+// is measured as in prep_half_train, seeds fl32(||x32||^2) (+inf on pad
+// rows) go to seed_out.  Queries (mult -2): zero operands for a query
+// launch_query_check marked invalid.
+__global__ void __launch_bounds__(256)
+prep_half_tiled_kernel(const double* __restrict__ X64, const double* __restrict__ mu, int64_t n,
+                       int d, int DP, int64_t n_pad, int jx, double mult,
+                       unsigned short* __restrict__ out, const float* __restrict__ seed_src,
+                       float* __restrict__ seed_out, const float* __restrict__ valid,
+                       unsigned long long* __restrict__ dx2max) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wstride = (int64_t)gridDim.x * 4;
+  const double sinv = __builtin_ldexp(1.0, -jx);
+  const int G = DP / 8, nch = DP / 32;
+  double m = 0.0;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n_pad; row += wstride) {
+    const bool live = row < n && (!valid || valid[row] > 0.0f);
+    const int64_t tile = row / kS3R;
+    const int r = (int)(row - tile * kS3R);
+    double e2 = 0.0;
+    for (int g = lane; g < G; g += 64) {
+      unsigned short hv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int col = 8 * g + u;
+        _Float16 h = (_Float16)0.0f;
+        if (live && col < d) {
+          const double x = X64[row * d + col] - mu[col];
+          h = f16_operand(mult * x, jx);
+          if (dx2max) {
+            const double e = (double)h * sinv - x;
+            e2 += e * e;
+          }
+        }
+        hv[u] = __builtin_bit_cast(unsigned short, h);
+      }
+      uint4 v;
+      v.x = hv[0] | (uint32_t)hv[1] << 16;
+      v.y = hv[2] | (uint32_t)hv[3] << 16;
+      v.z = hv[4] | (uint32_t)hv[5] << 16;
+      v.w = hv[6] | (uint32_t)hv[7] << 16;
+      unsigned char* blk = (unsigned char*)out + (((int64_t)tile * nch + (g >> 2)) * kS3R + r) * 64;
+      *(uint4*)(blk + s3_slot(r, g & 3) * 16) = v;
+    }
+    if (seed_out && lane == 0) seed_out[row] = row < n ? seed_src[row] : KNN_INF_F;
+    if (dx2max) m = fmax(m, wave_sum_d(e2));
+  }
+  if (dx2max && lane == 0)
+    atomicMax(dx2max, (unsigned long long)__double_as_longlong(m * (1.0 + 1e-12)));
+}
+
+void launch_prep_half_tiled(const double* X64, const double* mu, int64_t n, int d, int DP,
+                            int64_t n_pad, int jx, double mult, unsigned short* out,
+                            const float* seed_src, float* seed_out, const float* valid,
+                            unsigned long long* dx2max, hipStream_t s) {
+  int64_t blocks = (n_pad + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(prep_half_tiled_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X64, mu, n, d,
+                     DP, n_pad, jx, mult, out, seed_src, seed_out, valid, dx2max);
 }
 
 // ------------------------------- S3 images (bf16x3, DP > 256; knn_cand.hip)

@@ -188,17 +188,20 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
     double E =
         (METRIC == 0 ? f_err * (t.x2max + 2.1 * __builtin_sqrt(qa) * __builtin_sqrt(t.x2max))
                      : f_err * (qa + t.x1max)) + 1e-300;
-    if (METRIC == 0 && ps.qh) {
+    if (METRIC == 0 && ps.f16) {
       // fp16 operands: f_err covers the accumulation only; add the measured
       // representation error (q' = q - mu, x' = x - mu, dq / dx the operand
       // errors in unscaled units):  2 |q'.dx + dq.x' + dq.dx| <=
       // 2 (|q'| dxmax + |dq| (xmax + dxmax)), plus the fl32 seed's own
-      // rounding (3u ||x'||^2, u = 2^-24)
-      const unsigned short* qh = ps.qh + q * (int64_t)ps.qh_stride;
+      // rounding (3u ||x'||^2, u = 2^-24).  The query's operand is rebuilt
+      // here exactly as knn_prep.hip rounds it (one fp64 -> fp16 rounding
+      // of -2 * 2^jx (q - mu)), so its error is measured, not assumed.
       const double qs = -__builtin_ldexp(0.5, -t.jx);  // operand = -2 * 2^jx q'
       double dq2 = 0.0;
       for (int c = lane; c < d; c += 64) {
-        const double e = (double)__builtin_bit_cast(_Float16, qh[c]) * qs - (qv[c] - t.mu[c]);
+        const double x = qv[c] - t.mu[c];
+        const _Float16 h = f16_operand(-2.0 * x, t.jx);
+        const double e = (double)h * qs - x;
         dq2 += e * e;
       }
       const double qn = __builtin_sqrt(qa), xm = __builtin_sqrt(t.x2max);
@@ -831,7 +834,8 @@ void launch_rescan(int metric, const TrainDev& t, const double* Q64, const Resca
       hipLaunchKernelGGL((rescan_finish_fast_kernel<1, 256>), dim3(gf), dim3(256), lds, s, t, Q64,
                          rb.q, rb.tau, rb.cnt, cap, W, rb.fcnt, rb.buf, sink, rb.slow_q);
   }
-  const int gs = std::max(1, full_blocks);
+  if (full_blocks <= 0) return;  // (timing-only ablations)
+  const int gs = full_blocks;
   if (metric == 0)
     hipLaunchKernelGGL(rescan_full_kernel<0>, dim3(gs), dim3(kFullThreads), 0, s, t, Q64, rb.q,
                        rb.cnt, cap, rb.slow_q, W, sink, rb.counts, rb.totals);

@@ -12,7 +12,8 @@
 //     label per line (cpp:390-392), "Running time is <t> second" (cpp:398)
 // Extra flags: --gpus N (default 1), --mode query|train (multi-GPU layout),
 // --strict (exit 1 unless N_* divisible by --gpus, as MPI_Abort cpp:127-129),
-// --threads T (CSV parsing threads), --output path.
+// --threads T (CSV parsing threads), --output path, --timings (per-phase
+// seconds on stderr; stdout stays the reference's).
 // The timed region spans the same work as the reference (barrier to
 // barrier: CSV parsing, distribution, normalisation, both passes, output).
 #include <chrono>
@@ -44,6 +45,7 @@ struct Config {
   int mode = 0;
   bool strict = false;
   int threads = 0;
+  bool timings = false;
 };
 
 bool parse_bool(const std::string& v) { return v == "true" || v == "1" || v == "yes"; }
@@ -54,7 +56,7 @@ void usage() {
           "  [--class_cnt C] [--Euclidean_distance true|false] [--Normalize true|false]\n"
           "  [--Validation true|false] [--train_file F] [--validation_file F]\n"
           "  [--test_file F] [--output F] [--gpus G] [--mode query|train] [--strict]\n"
-          "  [--threads T]\n");
+          "  [--threads T] [--timings]\n");
 }
 
 int parse_args(int argc, char** argv, Config& c) {
@@ -67,6 +69,7 @@ int parse_args(int argc, char** argv, Config& c) {
     size_t eq = a.find('=');
     if (eq != std::string::npos) { v = a.substr(eq + 1); a = a.substr(0, eq); }
     else if (a == "strict") { c.strict = true; continue; }
+    else if (a == "timings") { c.timings = true; continue; }
     else if (i + 1 < argc) v = argv[++i];
     else { usage(); return 1; }
     if (a == "dim") c.dim = atoi(v.c_str());
@@ -126,12 +129,21 @@ int main(int argc, char** argv) {
 
   using clk = std::chrono::steady_clock;
   const auto start = clk::now();  // ≙ MPI_Barrier + MPI_Wtime, cpp:133-134
+  auto mark = start;
+  auto phase = [&](const char* name) {
+    const auto now = clk::now();
+    if (c.timings)
+      fprintf(stderr, "[knn_mpi_amd] %-10s %.3f s\n", name,
+              std::chrono::duration<double>(now - mark).count());
+    mark = now;
+  };
 
   std::vector<double> Xtr, Xte, Xva;
   std::vector<int32_t> Ltr, Lva;
   load(c.train_file, c.dim, true, c.N_train, Xtr, &Ltr, c.threads);
   load(c.test_file, c.dim, false, c.N_test, Xte, nullptr, c.threads);
   if (c.Validation) load(c.validation_file, c.dim, true, c.N_val, Xva, &Lva, c.threads);
+  phase("csv");
 
   if (c.Normalize) {  // cpp:229-306 on the GPUs: sharded min/max + RCCL all-reduce + apply
     std::vector<double*> sets{Xtr.data(), Xte.data()};
@@ -140,9 +152,11 @@ int main(int argc, char** argv) {
     if (knn_group_normalize(g, sets.data(), rows.data(), (int32_t)sets.size(), c.dim))
       die(knn_last_error());
   }
+  phase("normalize");
 
   if (knn_group_set_train(g, Xtr.data(), Ltr.data(), c.N_train, c.dim, c.class_cnt))
     die(knn_last_error());
+  phase("set_train");
   const int metric = c.Euclidean_distance ? KNN_METRIC_L2 : KNN_METRIC_L1;
 
   if (c.Validation) {  // cpp:308-349
@@ -155,16 +169,20 @@ int main(int argc, char** argv) {
       if (Lva[i] == pred[i]) acc++;
     acc /= c.N_val;
     std::cout << "accuracy = " << acc << std::endl;
+    phase("validation");
   }
 
   std::vector<int32_t> test_lab(c.N_test);  // cpp:352-393
   if (c.N_test > 0 &&
       knn_group_classify(g, Xte.data(), c.N_test, c.K, metric, test_lab.data(), nullptr, nullptr, nullptr))
     die(knn_last_error());
+  phase("test");
   {
+    // one label per line (cpp:390-392; '\n' without a flush per line)
     std::ofstream outfile(c.output);
-    for (long long i = 0; i < c.N_test; i++) outfile << test_lab[i] << std::endl;
+    for (long long i = 0; i < c.N_test; i++) outfile << test_lab[i] << '\n';
   }
+  phase("output");
 
   const auto finish = clk::now();  // cpp:395-396
   knn_group_destroy(g);

@@ -178,12 +178,21 @@ def test_cfg5_d960_k100(knn):
     clf = knn.Classifier(0)
     clf.set_train_device(X.data_ptr(), lab.data_ptr(), n, d, C, keep=(X, lab))
     got, idx, dist, flags = classify(knn, clf, Q, k)
-    assert clf.last_candidate_path() == 2, "cfg5 should run the bf16x3 candidate pass"
+    assert clf.last_candidate_path() == 4, "cfg5 should run the fp16 candidate pass (S3 kernel)"
+    assert clf.last_kernel_name().startswith("cand_s3_kernel<")
+    assert clf.last_kernel_name().endswith(",true>")
+    assert clf.last_rescan_count() * 16 <= m
     lab_all = lab.cpu().numpy()
     sample = np.arange(0, m, 4)
     check_properties(X, lab_all, Q, k, got, idx, dist, sample)
     check_oracle(X, lab_all, Q, k, got, idx, dist, np.arange(0, m, m // 8))
     check_optimal(X, Q, k, dist, np.arange(0, m, m // 128))
+    # the bf16x3 S3 kernel gives the same exact answer
+    clf.set_precision(knn.PRECISION_BF16X3)
+    gotb, _, distb, _ = classify(knn, clf, Q, k)
+    assert clf.last_candidate_path() == 2
+    np.testing.assert_array_equal(gotb, got)
+    assert (distb.view(np.int64) == dist.view(np.int64)).all()
     clf.close()
 
 
