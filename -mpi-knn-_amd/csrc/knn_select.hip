@@ -154,9 +154,9 @@ template <int METRIC, int NT, int EPL>
 __global__ void __launch_bounds__(NT)
 merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, int U, int R,
                     TrainDev t, const double* __restrict__ Q64, int W, int Cmax, int C2,
-                    double f_err, ProxyScale ps, const uint32_t* __restrict__ gthr, Sink sink,
-                    int* __restrict__ rescan_q, double* __restrict__ rescan_tau,
-                    int* __restrict__ rescan_cnt) {
+                    double f_err, ProxyScale ps, const uint32_t* __restrict__ gthr,
+                    int gstride, SegCands seg, Sink sink, int* __restrict__ rescan_q,
+                    double* __restrict__ rescan_tau, int* __restrict__ rescan_cnt) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int s_cn, s_cert;
   __shared__ double s_lb, s_qa, s_e;
@@ -224,23 +224,72 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
     const bool void_q = !(vq > 0.0f);
     const bool nonfinite = vq < 0.0f;
     // union in registers; min over full lists of their R-th (worst kept) entry
-    const float* lv = cv + q * U;
-    const int* li = ci + q * U;
     float v[EPL];
     int id[EPL];
     float mlr = KNN_INF_F;
     int nv = 0;
-#pragma unroll
-    for (int e = 0; e < EPL; ++e) {
-      const int x = lane + 64 * e;
-      v[e] = KNN_INF_F;
-      id[e] = -1;
-      if (x < U) {
-        v[e] = lv[x];
-        id[e] = li[x];
-        if (x % R == R - 1) mlr = fminf(mlr, v[e]);
+    int ne = EPL;  // register rows holding entries (the scan path: ceil(total / 64))
+    if (seg.buf) {
+      // scan-kernel segments, read compacted: lane s holds segment s's entry
+      // count; entry x of the union lies in the first segment whose inclusive
+      // prefix count exceeds x (binary search over the lanes).  A segment that
+      // overflowed dropped rows below the filter threshold, and a union
+      // larger than the registers leaves rows unread: nothing then bounds the
+      // rows left out (mlr = -inf: the query goes to the rescan with the W-th
+      // exact distance it has)
+      const int* sc = seg.cnt + q * seg.nseg;
+      int c = 0;
+      bool ov = false;
+      if (lane < seg.nseg) {
+        const int r = sc[lane];
+        c = min(r, seg.cap);
+        ov = r > seg.cap;
       }
-      nv += __popcll(__ballot(v[e] < KNN_INF_F));
+      int incl = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+      }
+      const int total = __shfl(incl, 63, 64);
+      if (__ballot(ov) || total > EPL * 64) mlr = -KNN_INF_F;
+      const int tot = min(total, EPL * 64);
+      ne = (tot + 63) >> 6;
+      const int2* sb = seg.buf + q * U;
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) {
+        const int x = lane + 64 * e;
+        v[e] = KNN_INF_F;
+        id[e] = -1;
+        if (e < ne) {
+          int sg = 0;
+#pragma unroll
+          for (int st = 32; st > 0; st >>= 1)
+            if (__shfl(incl, sg + st - 1, 64) <= x) sg += st;
+          const int j = x - (__shfl(incl, sg, 64) - __shfl(c, sg, 64));
+          if (x < tot) {
+            const int2 pr = sb[sg * seg.cap + j];
+            v[e] = __int_as_float(pr.x);
+            id[e] = pr.y;
+          }
+        }
+      }
+      nv = tot;
+    } else {
+      const float* lv = cv + q * U;
+      const int* li = ci + q * U;
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) {
+        const int x = lane + 64 * e;
+        v[e] = KNN_INF_F;
+        id[e] = -1;
+        if (x < U) {
+          v[e] = lv[x];
+          id[e] = li[x];
+          if (x % R == R - 1) mlr = fminf(mlr, v[e]);
+        }
+        nv += __popcll(__ballot(v[e] < KNN_INF_F));
+      }
     }
     mlr = wave_min(mlr);
     double tsel = KNN_INF_D;  // select proxies <= tsel
@@ -250,7 +299,8 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
         const uint32_t T = pre | ((1u << b) - 1u);
         int cnt = 0;
 #pragma unroll
-        for (int e = 0; e < EPL; ++e) cnt += __popcll(__ballot(f2key(v[e]) <= T));
+        for (int e = 0; e < EPL; ++e)
+          if (e < ne) cnt += __popcll(__ballot(f2key(v[e]) <= T));
         if (cnt < W) pre |= 1u << b;
       }
       const double vw = (double)key2f(pre) * pinv;
@@ -282,7 +332,8 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
         const uint32_t T = pre | ((1u << b) - 1u);
         int cnt = 0;
 #pragma unroll
-        for (int e = 0; e < EPL; ++e) cnt += __popcll(__ballot(v[e] < KNN_INF_F && f2key(v[e]) <= T));
+        for (int e = 0; e < EPL; ++e)
+          if (e < ne) cnt += __popcll(__ballot(v[e] < KNN_INF_F && f2key(v[e]) <= T));
         if (cnt < Cmax) pre |= 1u << b;
       }
       cn = 0;
@@ -305,9 +356,11 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
     // the candidate kernel also filtered with the query's global threshold
     // (cand_kernel): rows it dropped have proxy >= its final value
     float tq = KNN_INF_F;
-    if (gthr) {
+    if (gthr && gstride == 4) {
       const uint32_t* g = gthr + q * 4;
       tq = key2f(max(max(g[0], g[1]), max(g[2], g[3])));
+    } else if (gthr) {
+      tq = key2f(gthr[q * gstride]);
     }
     if (lane == 0) {
       // void proxies: exact rescan below; non-finite query: no neighbours
@@ -342,7 +395,8 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
     if (cn < W) {
       cert = false;  // fewer rows than the top W re-ranked (e.g. non-finite proxies)
     } else if (!(LB < KNN_INF_D)) {
-      cert = true;  // nothing was left out: every row was re-ranked exactly
+      // no bound on the rows left out (a candidate path without a filter
+      // threshold whose lists never filled): not certified
       cert = false;
     } else {
       const double dw = dk[W - 1], qa = s_qa, E = s_e;
@@ -380,27 +434,30 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
 template <int METRIC, int NT, int EPL>
 static void launch_mr(const float* cv, const int* ci, int U, int R, const TrainDev& t,
                       const double* Q64, int64_t m, int W, int Cmax, int C2, double f_err,
-                      ProxyScale ps, const uint32_t* gthr, const Sink& sink, int* rescan_q,
-                      double* rescan_tau, int* rescan_cnt, hipStream_t s) {
+                      ProxyScale ps, const uint32_t* gthr, int gstride, SegCands seg,
+                      const Sink& sink, int* rescan_q, double* rescan_tau, int* rescan_cnt,
+                      hipStream_t s) {
   const size_t lds = (size_t)(t.d <= kMergeLdsDim ? t.d : 0) * 8 + (size_t)C2 * 8 +
                      (size_t)NT * 17 * 8 + (size_t)C2 * 8;
   hipLaunchKernelGGL((merge_rerank_kernel<METRIC, NT, EPL>), dim3((unsigned)m), dim3(NT), lds, s,
-                     cv, ci, U, R, t, Q64, W, Cmax, C2, f_err, ps, gthr, sink, rescan_q, rescan_tau,
-                     rescan_cnt);
+                     cv, ci, U, R, t, Q64, W, Cmax, C2, f_err, ps, gthr, gstride, seg, sink, rescan_q,
+                     rescan_tau, rescan_cnt);
 }
 
 void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int R,
                          const TrainDev& t, const double* Q64, int64_t m, int W, int C,
-                         double f_err, ProxyScale ps, const uint32_t* gthr, const Sink& sink,
-                         int* rescan_q, double* rescan_tau, int* rescan_cnt, hipStream_t s) {
+                         double f_err, ProxyScale ps, const uint32_t* gthr, int gstride,
+                         SegCands seg, const Sink& sink, int* rescan_q, double* rescan_tau,
+                         int* rescan_cnt, hipStream_t s) {
   if (m <= 0) return;
-  const int U = NL * R;  // <= 2 * 64 * 16 (choose_geometry bounds S and R)
+  // <= 2 * 64 * 16 (choose_geometry bounds S and R; the scan path nseg * cap)
+  const int U = seg.buf ? seg.nseg * seg.cap : NL * R;
   int C2 = 1;
   while (C2 < C) C2 <<= 1;
   const bool big = C2 > 64, wide = U > 1024;
 #define KNN_MR(M_, NT_, EPL_) \
-  launch_mr<M_, NT_, EPL_>(cv, ci, U, R, t, Q64, m, W, C, C2, f_err, ps, gthr, sink, rescan_q, \
-                           rescan_tau, rescan_cnt, s)
+  launch_mr<M_, NT_, EPL_>(cv, ci, U, R, t, Q64, m, W, C, C2, f_err, ps, gthr, gstride, seg, sink, \
+                           rescan_q, rescan_tau, rescan_cnt, s)
   if (metric == 0) {
     if (big) { if (wide) KNN_MR(0, 256, 32); else KNN_MR(0, 256, 16); }
     else { if (wide) KNN_MR(0, 64, 32); else KNN_MR(0, 64, 16); }

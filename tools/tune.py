@@ -6,7 +6,9 @@ Variants: "prec:R:S[:ablate[:nw]]" e.g. auto:0:0 fp32:8:0 auto:8:0:1:8
 (prec: auto | fp32 | bf16x3 | m16 = bf16x3 on the 16x16x32 MFMA layout | fp16
  = fp16 on the 16x16x32 MFMA)
 (ablate bits: 1 = no staging loads, 2 = no selection epilogue; timing only;
-nw = waves per candidate workgroup, 0 auto / 4 / 8)"""
+nw = waves per candidate workgroup, 0 auto / 4 / 8)
+Extra tuning keys after a comma, e.g. "fp16:0:0,scan=1,scan_a=512" (keys not
+named by a variant are reset to automatic: scan -1, scan_a 0, scan_cap 0)."""
 import argparse
 import os
 import sys
@@ -43,9 +45,17 @@ def main():
     info = {}
     prec = {"auto": knn.PRECISION_AUTO, "fp32": knn.PRECISION_FP32, "bf16x3": knn.PRECISION_BF16X3,
             "m16": knn.PRECISION_BF16X3, "fp16": knn.PRECISION_FP16}
+    defaults = {"scan": -1, "scan_a": 0, "scan_cap": 0}
     for r in range(a.rounds + 1):
         for v in a.variants:
-            parts = v.split(":")
+            base, *extra = v.split(",")
+            kv = dict(defaults)
+            for e in extra:
+                key, val = e.split("=")
+                kv[key] = int(val)
+            for key, val in kv.items():
+                clf.set_tuning(key, val)
+            parts = base.split(":")
             p, R, S = parts[:3]
             abl = int(parts[3]) if len(parts) > 3 else 0
             nw = int(parts[4]) if len(parts) > 4 else 0
