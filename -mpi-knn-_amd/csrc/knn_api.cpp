@@ -380,7 +380,11 @@ static void choose_geometry(knn_ctx* ctx, int metric, bool streamed, int DP, int
     // top W expected per list: a list holding 5 of them (an overflow ->
     // the query fails certification) then has probability ~C(W,5)/(4S)^5
     int S_lo = std::max(1, (C + lps * R - 1) / (lps * R));
-    if (quad) S_lo = std::max(S_lo, W);
+    // quad lists: S >= 2W where every split still walks >= 32 tiles (a list
+    // then expects at most 1/8 of the query's top W; an overflow, 5 of them in
+    // one list, has probability ~C(W,5)/(8S)^5 -- 0.7 % of cfg3's queries
+    // failed at S = W, each an exact rescan), at least S >= W
+    if (quad) S_lo = std::max(S_lo, std::max<int>(W, (int)std::min<int64_t>(2 * W, n_tiles / 32)));
     S_lo = std::min(S_hi, S_lo);
     auto eff_of = [&](int S) {
       const int64_t wg = (int64_t)n_qt * S;
@@ -395,13 +399,21 @@ static void choose_geometry(knn_ctx* ctx, int metric, bool streamed, int DP, int
     int bS = S_lo;
     for (int S = S_lo; S <= S_hi; S++)
       if (eff_of(S) >= best - 0.02) { bS = S; break; }
+    // S3: prefer a split count that lets the XCD's concurrent workgroups
+    // share staged chunks (s3_map; gq 4 over 2 over none) within the same fill
+    if (streamed && DP > 256) {
+      int bq = s3_group(n_qt, bS);
+      for (int S = bS + 1; S <= S_hi && bq < 4; S++)
+        if (eff_of(S) >= best - 0.02 && s3_group(n_qt, S) > bq) { bS = S; bq = s3_group(n_qt, S); }
+    }
     if (ctx->tune_S) bS = std::min(ctx->tune_S, S_hi);
     bestS = bS;
     bestR = R;
     // R = 8 when the expected share of the top W per list (2S lists) is at
-    // most 2: a list overflow (-> certification fails) is then rare and the
-    // fast rescan absorbs it; else R = 16.
-    if (ctx->tune_R || quad || W <= 4 * bS) break;
+    // most 1/2: a list overflow (9 of the top W in one list -> certification
+    // fails) is then rare (at a share of 1.6 -- cfg5, W = 101, S = 32 -- 1.6 %
+    // of the queries failed); else R = 16.
+    if (ctx->tune_R || quad || W <= bS) break;
   }
   S_out = bestS;
   R_out = bestR;
@@ -471,71 +483,6 @@ static void auto_check(knn_ctx* ctx) {
   ctx->auto_pending = false;
 }
 
-// fp16 threshold scan (knn_scan.hip) in place of the list kernel: the
-// resident fp16 list kernel runs over a strided sample of ~W n / A rows
-// (A = target rows appended per query), the W-th smallest of its lists seeds
-// each query's threshold T, and the scan kernel streams every row against T.
-// AUTO: L2, 8-wave geometry (>= 4096 queries), n >= kScanMinRows, W <= 32.
-// Tuning keys "scan" (-1 auto, 0 off, 1 on), "scan_a" (A), "scan_cap".
-constexpr int kScanAppend = 256;
-constexpr int64_t kScanMinRows = 262144;
-constexpr int kScanMaxW = 32;
-constexpr int kScanTileRows = 128;  // rows per staged tile of cand_kernel<DP,4,4,8>
-struct ScanPlan {
-  bool on = false;
-  int S = 0, cap = 0;               // scan kernel: splits, segment capacity
-  int S_pre = 0, TS = 0, max_tiles = 0, NL_pre = 0;  // sample pre-pass (list kernel)
-};
-static void choose_geometry(knn_ctx* ctx, int metric, bool streamed, int DP, int nw, int n_qt,
-                            int64_t n_tiles, int W, int C, int& S_out, int& R_out);
-static ScanPlan plan_scan(knn_ctx* ctx, int DP, int n_qt, int W, int C) {
-  ScanPlan p;
-  const TrainDev& t = ctx->train;
-  if (ctx->tune_scan == 0) return p;
-  const int64_t n_tiles = t.n_pad / kScanTileRows;
-  const int A = ctx->tune_scan_a > 0 ? ctx->tune_scan_a : kScanAppend;
-  int64_t ST = ((int64_t)W * t.n / A + kScanTileRows - 1) / kScanTileRows;  // sample tiles
-  ST = std::max<int64_t>(ST, 1);
-  if (ctx->tune_scan < 0 && (t.n < kScanMinRows || W > kScanMaxW || 4 * ST > n_tiles)) return p;
-  ST = std::min(ST, n_tiles);
-  int R = 4;
-  const int keep_S = ctx->tune_S;  // the "S" override applies to the scan kernel
-  ctx->tune_S = 0;
-  choose_geometry(ctx, 4, false, DP, 8, n_qt, ST, W, C, p.S_pre, R);
-  ctx->tune_S = keep_S;
-  p.NL_pre = 4 * p.S_pre;
-  p.max_tiles = (int)((ST + p.S_pre - 1) / p.S_pre);
-  p.TS = (int)std::min<int64_t>(n_tiles / p.max_tiles, INT32_MAX);
-  if ((int64_t)p.max_tiles * p.S_pre > n_tiles || p.TS < p.S_pre) {
-    // the sample would cover (about) every tile: the pre-pass walks all rows
-    p.TS = p.S_pre;
-    p.max_tiles = 0;
-  }
-  // scan splits: the smallest S within 2 % of the best fill of the resident
-  // slots, and segments that hold ~3x their expected share of the A rows
-  const int64_t slots = (int64_t)scan_blocks_per_cu(DP) * ctx->cu_count;
-  auto eff_of = [&](int S) {
-    const int64_t wg = (int64_t)n_qt * S;
-    return (double)wg / (double)(((wg + slots - 1) / slots) * slots);
-  };
-  const int S_hi = (int)std::max<int64_t>(
-      1, std::min<int64_t>(64, t.n_pad / (16 * scan_rb(DP)) / scan_nw(DP)));  // >= 1 block per wave
-  double best = -1.0;
-  for (int S = 1; S <= S_hi; S++) best = std::max(best, eff_of(S));
-  p.S = 1;
-  for (int S = 1; S <= S_hi; S++)
-    if (eff_of(S) >= best - 0.02) { p.S = S; break; }
-  if (ctx->tune_S) p.S = std::min(ctx->tune_S, S_hi);
-  int cap = 16;
-  while (cap < 3 * A / p.S + 16) cap <<= 1;
-  if (ctx->tune_scan_cap) cap = ctx->tune_scan_cap;
-  while ((int64_t)p.S * cap > 2048 && cap > 8) cap >>= 1;  // the merge holds <= 2048 slots
-  if ((int64_t)p.S * cap > 2048) return p;
-  p.cap = cap;
-  p.on = true;
-  return p;
-}
-
 // Core search: candidate pass + merge/re-rank/certify + the device-driven
 // rescan.  Enqueue only: no host synchronisation on any path.
 int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric, const Sink& sink,
@@ -577,7 +524,6 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   if (DP <= 256 && kmetric != 1) nw = ctx->tune_nw ? std::min(ctx->tune_nw, 8) : (m >= 4096 ? 8 : 4);
   if (kmetric >= 3) nw = 8;
   if (kmetric == 4 && !s3 && ctx->tune_nw) nw = ctx->tune_nw;  // 4, 8 or 16
-  if (kmetric == 4 && !s3 && ctx->tune_scan > 0 && metric == KNN_METRIC_L2) nw = 8;  // scan: 256 queries
   if (s3) nw = 8;
   const int qpb = s3 ? kS3Rows : (DP <= 256 ? 32 * nw : kQPB);
   const int n_qt = (int)((m + qpb - 1) / qpb);
@@ -590,18 +536,8 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   choose_geometry(ctx, kmetric, s3, DP, nw, n_qt, n_tiles, W, C, S, R);
   const bool quad_lists = !s3 && (kmetric == 3 || kmetric == 4);  // 16x16: 4 lists per split
   if (quad_lists) R = 4;
-  int NL = (quad_lists ? 4 : 2) * S;
+  const int NL = (quad_lists ? 4 : 2) * S;
   C = std::min(C, NL * R);
-  ScanPlan sp;
-  if (kmetric == 4 && !s3 && qpb == kScanQ && metric == KNN_METRIC_L2) sp = plan_scan(ctx, DP, n_qt, W, C);
-  if (sp.on) {
-    // the list kernel runs only as the sample pre-pass (its lists seed T)
-    NL = sp.NL_pre;
-    C = std::min(C, sp.S * sp.cap);
-    if ((rc = ctx->seg_buf.ensure((size_t)m_pad * sp.S * sp.cap * sizeof(int2)))) return rc;
-    if ((rc = ctx->seg_cnt.ensure((size_t)m_pad * sp.S * sizeof(int)))) return rc;
-    if ((rc = ctx->tkey.ensure((size_t)m_pad * sizeof(uint32_t)))) return rc;
-  }
   // rescan workspace: the fast path serves the first `cap` failed queries
   const int cap = (int)std::min<int64_t>(m, kRescanFastQueries);
   if ((rc = ctx->Q32.ensure((size_t)m_pad * DP * sizeof(float)))) return rc;
@@ -622,15 +558,12 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   if ((rc = ctx->slow_q.ensure((size_t)m * sizeof(int) + 16))) return rc;
 
   ctx->last_kmetric = kmetric;
-  ctx->geom[0] = (int64_t)n_qt * (sp.on ? sp.S : S);
-  ctx->geom[1] = sp.on ? sp.S : S;
-  ctx->geom[2] = sp.on ? sp.cap : R;
+  ctx->geom[0] = (int64_t)n_qt * S;
+  ctx->geom[1] = S;
+  ctx->geom[2] = R;
   ctx->last_nw = nw;
   ctx->geom[3] = C;
-  if (sp.on)
-    snprintf(ctx->last_kernel, sizeof ctx->last_kernel, "scan_kernel<%d,%d,%d>", DP, scan_rb(DP),
-             scan_nw(DP));
-  else if (s3)
+  if (s3)
     snprintf(ctx->last_kernel, sizeof ctx->last_kernel, "cand_s3_kernel<%d,%s>", R,
              s3h ? "true" : "false");
   else if (DP <= 256)
@@ -679,19 +612,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   cl.nw = nw;
   cl.gthr = use_gthr ? (uint32_t*)ctx->gthr.p : nullptr;
   if (use_gthr) launch_fill_i32((int32_t*)ctx->gthr.p, m_pad * 4, (int32_t)kGthrInit, s);
-  if (sp.on) {
-    // sample pre-pass -> thresholds -> threshold scan of every row
-    cl.S = sp.S_pre;
-    cl.tile_stride = sp.TS;
-    cl.max_tiles = sp.max_tiles;
-    if (!launch_cand(cl, s))
-      return knn_fail(KNN_ERR_ARG, "no candidate kernel for the scan pre-pass geometry");
-    launch_seed_threshold(cl.out_v, sp.NL_pre * 4, m_pad, W, (uint32_t*)ctx->tkey.p, s);
-    if (!launch_scan(DP, Xk, (const unsigned short*)ctx->Q32.p, t.n_pad, sp.S, n_qt,
-                     (const uint32_t*)ctx->tkey.p, sp.cap, (int*)ctx->seg_cnt.p,
-                     (int2*)ctx->seg_buf.p, ctx->tune_ablate, s))
-      return knn_fail(KNN_ERR_ARG, "no scan kernel for this dimension");
-  } else if (s3h)
+  if (s3h)
     launch_cand_s3h((const unsigned short*)ctx->XT16.p, (const float*)ctx->XS16.p,
                     (const unsigned short*)ctx->Q32.p, DP, n_pad3, R, S, n_qt, cl.out_v, cl.out_i,
                     cl.ablate, s);
@@ -705,14 +626,10 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   if (tc) HIP_TRY(hipEventRecord(tc->ev[2], s));
   HIP_TRY(hipMemsetAsync(ctx->rescan_cnt.p, 0, 4 * sizeof(int), s));
   launch_merge_rerank(metric, (const float*)ctx->cand_v.p, (const int*)ctx->cand_i.p, NL, R, t, dQ,
-                      m, W, C, err_factor(kmetric, DP),
+                      m, W, C, err_factor(kmetric, DP), err_factor(0, t.DP),
                       kmetric == 4 ? ProxyScale{qvalid, 0x1p-14, 0x1p-28, true}
                                    : ProxyScale{qvalid, 0x1p-125, 0x1p-124},
-                      sp.on ? (const uint32_t*)ctx->tkey.p : cl.gthr, sp.on ? 1 : 4,
-                      sp.on ? SegCands{(const int2*)ctx->seg_buf.p, (const int*)ctx->seg_cnt.p,
-                                       sp.S, sp.cap}
-                            : SegCands{},
-                      sink, (int*)ctx->rescan_q.p,
+                      cl.gthr, sink, (int*)ctx->rescan_q.p,
                       (double*)ctx->rescan_tau.p, (int*)ctx->rescan_cnt.p, s);
   HIP_TRY(hipGetLastError());
   if (tc) HIP_TRY(hipEventRecord(tc->ev[3], s));
@@ -994,16 +911,6 @@ int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value) {
     ctx->tune_nw = (int)value;
   } else if (!strcmp(key, "ablate")) {
     ctx->tune_ablate = (int)value;  // timing experiments only: results become invalid
-  } else if (!strcmp(key, "scan")) {
-    if (value < -1 || value > 1) return knn_fail(KNN_ERR_ARG, "scan must be -1, 0 or 1");
-    ctx->tune_scan = (int)value;
-  } else if (!strcmp(key, "scan_a")) {
-    if (value < 0 || value > 65536) return knn_fail(KNN_ERR_ARG, "scan_a must be 0 .. 65536");
-    ctx->tune_scan_a = (int)value;
-  } else if (!strcmp(key, "scan_cap")) {
-    if (value != 0 && (value < 8 || value > 1024 || (value & (value - 1))))
-      return knn_fail(KNN_ERR_ARG, "scan_cap must be 0 or a power of two in [8, 1024]");
-    ctx->tune_scan_cap = (int)value;
   } else if (!strcmp(key, "S")) {
     if (value < 0 || value > 64) return knn_fail(KNN_ERR_ARG, "S must be 0 (auto) .. 64");
     ctx->tune_S = (int)value;

@@ -49,9 +49,6 @@ struct knn_ctx {
   int tune_nw = 0;             // resident kernel waves per workgroup (0 = auto)
   int tune_fp16 = -1;          // fp16 candidate pass: -1 auto, 0 off, 1 on
   int tune_m16 = -1;           // bf16x3 on the 16x16x32 MFMA layout: -1 auto, 0 off, 1 on
-  int tune_scan = -1;          // fp16 threshold-scan kernel (knn_scan.hip): -1 auto, 0 off, 1 on
-  int tune_scan_a = 0;         // scan: target rows appended per query (0 = default)
-  int tune_scan_cap = 0;       // scan: segment capacity (0 = automatic)
   int last_nw = 0;
   int last_kmetric = -1; // candidate kernel metric of the last search (knn_kernels.h)
   char last_kernel[96] = {0};  // name of the last candidate kernel launched
@@ -66,7 +63,7 @@ struct knn_ctx {
   DevBuf X64_own, lab_own, X32, xl2, xl1, stats, XB, XS, XH, XT16, XS16, mu, mu_part;
   // per-classify workspace
   DevBuf Q64, Q32, qvalid, cand_v, cand_i, gthr, rescan_q, rescan_tau, rescan_cnt, fr_cnt, fr_buf,
-      fr_q, fr_thr, slow_q, totals, seg_buf, seg_cnt, tkey;
+      fr_q, fr_thr, slow_q, totals;
   // host-API outputs
   DevBuf o_lab, o_idx, o_dist, o_flags;
   // normalisation: per-thread partial max/min, bounds, host-API staging
@@ -75,7 +72,7 @@ struct knn_ctx {
     return {&X64_own, &lab_own, &X32,   &xl2,   &xl1,    &stats,  &XB,       &XS,
             &XH,      &XT16,    &XS16,  &mu,      &mu_part, &Q64, &Q32,    &qvalid, &cand_v,   &cand_i,
             &gthr,    &rescan_q, &rescan_tau, &rescan_cnt, &fr_cnt, &fr_buf, &fr_q, &fr_thr,
-            &slow_q,  &totals,  &seg_buf, &seg_cnt, &tkey, &o_lab, &o_idx, &o_dist, &o_flags, &nrm_part, &nrm_mm, &nrm_X};
+            &slow_q,  &totals,  &o_lab, &o_idx, &o_dist, &o_flags, &nrm_part, &nrm_mm, &nrm_X};
   }
 };
 

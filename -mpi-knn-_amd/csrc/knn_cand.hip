@@ -233,11 +233,38 @@ __device__ __forceinline__ void s3_wait_barrier(int n) {
   }
 }
 
+// Workgroup -> (query tile, split) of the S3 kernel.  gq = 0: XCD-contiguous
+// ranges (xcd_remap), splits outer.  gq in {1, 2, 4} (n_qt % gq == 0 and
+// S % (32 / gq) == 0): the 32 workgroups an XCD runs at once (one per CU,
+// workgroup w on XCD w % 8) form one group of gq query tiles x 32/gq splits,
+// so each step's staged chunks are shared in the XCD's L2 -- a row chunk by
+// gq workgroups, a query chunk by 32/gq -- instead of each workgroup's query
+// images streaming through L2 on their own (32 query tiles per XCD with
+// gq = 0: the query images are re-fetched for every train tile).
+__device__ __forceinline__ void s3_map(int b, int nwg, int n_qt, int gq, int& qt, int& split) {
+  if (gq == 0) {
+    const int l = xcd_remap(b, nwg);
+    split = l / n_qt;
+    qt = l - split * n_qt;
+    return;
+  }
+  // group index g: rounds of 256 workgroups (32 per XCD), XCD-major inside
+  // a round; the tail of an incomplete round keeps its own order
+  const int full = nwg & ~255;
+  const int l = b < full ? (((b >> 3) >> 5) * 8 + (b & 7)) * 32 + ((b >> 3) & 31) : b;
+  const int gs = 32 / gq;
+  const int g = l >> 5, r = l & 31;
+  const int ngq = n_qt / gq;  // groups along the query tiles
+  const int sb = g / ngq, qb = g - sb * ngq;
+  qt = qb * gq + r % gq;
+  split = sb * gs + r / gq;
+}
+
 template <int R, bool F16>
 __global__ void __launch_bounds__(512)
 cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* QT, int nch,
                int n_tiles, int S, int n_qt, float* __restrict__ out_v, int* __restrict__ out_i,
-               int abl) {
+               int abl, int gq) {
   // abl: timing-only ablations as in cand_kernel (bit0 no staging after the
   // first steps, bit1 no selection epilogue); 0 in production.
   constexpr int BLK = kS3R * 64;        // bytes of one operand image
@@ -247,9 +274,8 @@ cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* 
   static_assert(4 * (PD - 1) + PD <= 15, "vmcnt wait range");
   __shared__ __attribute__((aligned(16))) unsigned char lds[NB * BUFB];
 
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int split = bid / n_qt;
-  const int qt = bid - split * n_qt;
+  int qt, split;
+  s3_map(blockIdx.x, gridDim.x, n_qt, gq, qt, split);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int j = lane & 31, h = lane >> 5;
@@ -408,30 +434,39 @@ int s3h_blocks_per_cu(int R) {
                 : occupancy_of(cand_s3_kernel<16, true>, 512);
 }
 
+// the S3 grouping (s3_map) that n_qt and S admit: 4, 2, 1, else 0
+int s3_group(int n_qt, int S) {
+  for (int gq : {4, 2, 1})
+    if (n_qt % gq == 0 && S % (32 / gq) == 0) return gq;
+  return 0;
+}
+
 void launch_cand_s3(const unsigned short* XT, const float* XS, const unsigned short* QT, int DP,
                     int64_t n_pad, int R, int S, int n_qt, float* out_v, int* out_i, int ablate,
                     hipStream_t s) {
+  const int gq = s3_group(n_qt, S);
   const int nch = DP / kS3DC;
   const int n_tiles = (int)(n_pad / kS3R);
   if (R == 8)
     hipLaunchKernelGGL((cand_s3_kernel<8, false>), dim3((unsigned)(n_qt * S)), dim3(512), 0, s, XT,
-                       XS, QT, nch, n_tiles, S, n_qt, out_v, out_i, ablate);
+                       XS, QT, nch, n_tiles, S, n_qt, out_v, out_i, ablate, gq);
   else
     hipLaunchKernelGGL((cand_s3_kernel<16, false>), dim3((unsigned)(n_qt * S)), dim3(512), 0, s, XT,
-                       XS, QT, nch, n_tiles, S, n_qt, out_v, out_i, ablate);
+                       XS, QT, nch, n_tiles, S, n_qt, out_v, out_i, ablate, gq);
 }
 
 void launch_cand_s3h(const unsigned short* XT, const float* XS, const unsigned short* QT, int DP,
                      int64_t n_pad, int R, int S, int n_qt, float* out_v, int* out_i, int ablate,
                      hipStream_t s) {
+  const int gq = s3_group(n_qt, S);
   const int nch = DP / 32;
   const int n_tiles = (int)(n_pad / kS3R);
   if (R == 8)
     hipLaunchKernelGGL((cand_s3_kernel<8, true>), dim3((unsigned)(n_qt * S)), dim3(512), 0, s, XT,
-                       XS, QT, nch, n_tiles, S, n_qt, out_v, out_i, ablate);
+                       XS, QT, nch, n_tiles, S, n_qt, out_v, out_i, ablate, gq);
   else
     hipLaunchKernelGGL((cand_s3_kernel<16, true>), dim3((unsigned)(n_qt * S)), dim3(512), 0, s, XT,
-                       XS, QT, nch, n_tiles, S, n_qt, out_v, out_i, ablate);
+                       XS, QT, nch, n_tiles, S, n_qt, out_v, out_i, ablate, gq);
 }
 
 template <int R, int METRIC>

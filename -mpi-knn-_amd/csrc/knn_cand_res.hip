@@ -99,10 +99,7 @@ __global__ void __launch_bounds__(NW * 64)
 __attribute__((amdgpu_waves_per_eu((METRIC == 4 ? DP / 2 : DP) <= 160 && R <= 8 ? 4 : 1)))
 cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
             int n_qt, float* __restrict__ out_v, int* __restrict__ out_i, int abl,
-            uint32_t* gthr, int TS, int max_tiles) {
-  // TS: tile stride of a split's walk (S in the search; the scan path's
-  // threshold pre-pass walks a strided sample), max_tiles: cap on the tiles
-  // a split visits (0 = all)
+            uint32_t* gthr) {
 #if KNN_SETPRIO
   // the second-dispatched half of the workgroup at priority 1 (MI355X_MICROARCH
   // "Two waves per SIMD", item 4)
@@ -234,8 +231,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   uint32_t last_pub = kKeyInf;
   int x_ops = 0, x_age = -1;  // ops of the pending exchange, tiles since it
 
-  int my_nt = split < n_tiles ? (n_tiles - split + TS - 1) / TS : 0;
-  if (max_tiles > 0) my_nt = min(my_nt, max_tiles);
+  const int my_nt = split < n_tiles ? (n_tiles - split + S - 1) / S : 0;
 
   // ---- staging: this wave's LDS-DMA pieces i = wv, wv+NW, ... of tile t ->
   // buffer b.  The last piece may read past the tile (and past the last row:
@@ -254,12 +250,12 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
 
 #pragma unroll
   for (int p = 0; p < PD; ++p)
-    if (my_nt > p) KNN_ISSUE(split + p * TS, p);
+    if (my_nt > p) KNN_ISSUE(split + p * S, p);
 
   const bool g_hi = wv < NG % NW || NG % NW == 0;
   int cur = 0, nxt = PD;  // buffer of tile it, buffer that tile it+PD goes to
   for (int it = 0; it < my_nt; ++it) {
-    const int t = split + it * TS;
+    const int t = split + it * S;
     if constexpr (TEC) {
 #pragma unroll
       for (int b = 0; b < NQL; ++b) thr[b] = L[b][R - 1];  // for the exchange below
@@ -285,7 +281,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       __builtin_amdgcn_sched_barrier(0);
       // (abl bit 3: the same pieces, always of the split's first tile -- DMA
       // issue cost without the data stream; timing only)
-      if (it + PD < my_nt && !(abl & 1)) KNN_ISSUE((abl & 8) ? split : t + PD * TS, nxt);
+      if (it + PD < my_nt && !(abl & 1)) KNN_ISSUE((abl & 8) ? split : t + PD * S, nxt);
       if (gthr) {
         if (x_age == PD) {
 #pragma unroll
@@ -501,8 +497,8 @@ template <int DP, int R, int METRIC, int NW>
 static void launch_res(const CandLaunch& c, hipStream_t s) {
   hipLaunchKernelGGL((cand_kernel<DP, R, METRIC, NW>), dim3((unsigned)(c.n_qt * c.S)),
                      dim3(NW * 64), 0, s, c.X32, c.Q32, (int)(c.n_pad / (kTR * res_tpb<METRIC>())), c.S,
-                     c.n_qt, c.out_v, c.out_i, c.ablate, c.gthr, c.tile_stride ? c.tile_stride : c.S,
-                     c.max_tiles);
+                     c.n_qt,
+                     c.out_v, c.out_i, c.ablate, c.gthr);
 }
 
 // Instantiated variants: R in {4, 8, 16}; METRIC 0/2 with NW in {4, 8};

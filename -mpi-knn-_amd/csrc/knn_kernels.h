@@ -68,6 +68,8 @@ void launch_cand_s3h(const unsigned short* XT, const float* XS, const unsigned s
                      int64_t n_pad, int R, int S, int n_qt, float* out_v, int* out_i, int ablate,
                      hipStream_t s);
 int s3h_blocks_per_cu(int R);
+// S3 workgroup grouping for n_qt query tiles and S splits (knn_cand.hip, s3_map)
+int s3_group(int n_qt, int S);
 int pad_dim_fp16_s3(int d);         // padded dim of the fp16 S3 image (multiple of 32, > 256)
 // fp64 rows -> fp16 S3 tile-chunk images of mult * 2^jx (x - mu) (knn_prep.hip);
 // train: seed_out[row] = seed_src[row] (+inf on pad rows) and the running max
@@ -94,29 +96,7 @@ struct CandLaunch {
   int ablate;   // timing-only ablation bits (0 in production)
   int nw;       // resident kernel: waves (x32 queries) per workgroup, 4 or 8
   uint32_t* gthr;  // resident kernel: per-query global thresholds [m_pad][4] (keys)
-  int tile_stride;  // resident kernel: tile stride of a split's walk (0 = S)
-  int max_tiles;    // resident kernel: tiles per split at most (0 = all)
 };
-
-// fp16 threshold-scan kernel (knn_scan.hip), DP in {32, 64, ..., 256}:
-// XH the fp16 train rows (ensure_fp16 layout), Qh the queries' fp16 rows
-// (m_pad x DP halves), tkey[m_pad] the per-query threshold keys; appends
-// (proxy bits, row) of every row with proxy < T to buf[q][split][cap] and
-// writes cnt[q][split] (> cap: overflowed).  false: DP not instantiated.
-constexpr int kScanQ = 256;  // queries per workgroup of the scan kernel
-// scan kernel shape by DP: waves per workgroup (two waves per SIMD: two
-// 4-wave workgroups per CU while 256 query rows fit twice in LDS, else one
-// 8-wave workgroup) and 16-row blocks per wave step RB (each LDS query
-// fragment feeds RB MFMAs; RB x DP/32 A fragments stay in VGPRs)
-constexpr int scan_nw(int DP) { return DP <= 128 ? 4 : 8; }
-constexpr int scan_rb(int DP) { return DP <= 192 ? 4 : 2; }
-bool launch_scan(int DP, const float* XH, const unsigned short* Qh, int64_t n_pad, int S, int n_qt,
-                 const uint32_t* tkey, int cap, int* cnt, int2* buf, int abl, hipStream_t s);
-int scan_blocks_per_cu(int DP);
-// tkey[q] <- key of the next float above the W-th smallest of the U values
-// pv[q][0..U) (the pre-pass's list entries; W <= U, U % 4 == 0)
-void launch_seed_threshold(const float* pv, int U, int64_t m_pad, int W, uint32_t* tkey,
-                           hipStream_t s);
 constexpr uint32_t kGthrInit = 0xFF800000u;  // order-preserving key of +inf
 
 // Candidate-pass operands are centred on the train column means mu (see knn_prep.hip).
@@ -152,21 +132,11 @@ struct ProxyScale {
   double ue, up;
   bool f16 = false;
 };
-// Candidates come either as lists (cv/ci: [m][NL][R]) or, for the scan
-// kernel, as segments (seg != null: seg_buf[m][nseg][cap] (proxy bits, row)
-// with seg_cnt[m][nseg] valid entries each); gthr: the filter thresholds the
-// candidate kernel applied, gstride keys per query (4 for the list kernels'
-// slots -- the max applies -- 1 for the scan kernel's T)
-struct SegCands {
-  const int2* buf = nullptr;
-  const int* cnt = nullptr;
-  int nseg = 0, cap = 0;
-};
 void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int R,
                          const TrainDev& t, const double* Q64, int64_t m, int W, int C,
-                         double f_err, ProxyScale ps, const uint32_t* gthr, int gstride,
-                         SegCands seg, const Sink& sink, int* rescan_q, double* rescan_tau,
-                         int* rescan_cnt, hipStream_t s);
+                         double f_err, double f32_err, ProxyScale ps, const uint32_t* gthr,
+                         const Sink& sink, int* rescan_q, double* rescan_tau, int* rescan_cnt,
+                         hipStream_t s);
 constexpr int kRescanCap = 1024;        // rows a fast rescan may append per query
 constexpr int kRescanStageMaxDP = 256;  // fast rescan stages rows in LDS up to this DP
 constexpr int kRescanFastQueries = 65536;  // failed queries per call the fast path serves

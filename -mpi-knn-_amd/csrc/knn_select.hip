@@ -150,16 +150,63 @@ __device__ void exact_sorted(const TrainDev& t, const double* qv, int* di, doubl
   bitonic_sort_lds(dk, di, C2, tid, NT);
 }
 
+// Large d (> kPrefilterMinD, L2): the selected rows' fp64 rows are the
+// merge's main HBM stream (cfg5: ~200 rows x 7.7 KB per query).  A first
+// pass computes each selected row's fp32 proxy from the fp32 copy X32 (half
+// the bytes; an fmaf chain, rigorous bound e32 in unscaled units) and sorts
+// the rows by it; a row whose fp32 proxy exceeds the W-th smallest by more
+// than 2 e32 cannot be in the top W -- the W rows below it all have exact
+// distances below its own -- so only the prefix within reach goes on to the
+// exact fp64 re-rank.  Returns that prefix length (di[0..) reordered).
+constexpr int kPrefilterMinD = 256;
+template <int NT>
+__device__ int fp32_prefilter(const TrainDev& t, const double* qv, float* qf, int* di, double* dk,
+                              int cn, int C2, int W, double e32, int tid) {
+  __shared__ int s_cut;
+  const int DP = t.DP, RSF = DP + 4;
+  for (int i = tid; i < DP; i += NT)
+    qf[i] = i < t.d ? (float)__builtin_ldexp(-2.0 * (qv[i] - t.mu[i]), t.jx) : 0.0f;
+  if (tid == 0) s_cut = cn;
+  __syncthreads();
+  const double pinv = __builtin_ldexp(1.0, -2 * t.jx);
+  for (int c = tid; c < C2; c += NT) {
+    double p = KNN_INF_D;
+    if (c < cn) {
+      const float* xr = t.X32 + (int64_t)di[c] * RSF;
+      float a = xr[DP];  // fl32(||x32||^2)
+#pragma unroll 8
+      for (int i = 0; i < DP; i += 4) {
+        const float4 x4 = *(const float4*)(xr + i);
+        const float4 q4 = *(const float4*)(qf + i);
+        a = __builtin_fmaf(q4.x, x4.x, a);
+        a = __builtin_fmaf(q4.y, x4.y, a);
+        a = __builtin_fmaf(q4.z, x4.z, a);
+        a = __builtin_fmaf(q4.w, x4.w, a);
+      }
+      p = (double)a * pinv;
+    } else {
+      di[c] = INT_MAX;
+    }
+    dk[c] = p;
+  }
+  bitonic_sort_lds(dk, di, C2, tid, NT);
+  const double cut = dk[W - 1] + 2.0 * e32 + 1e-9 * (__builtin_fabs(dk[W - 1]) + e32) + 1e-300;
+  for (int c = tid; c < cn; c += NT)
+    if (dk[c] > cut && (c == 0 || !(dk[c - 1] > cut))) s_cut = c;  // first row past the cut
+  __syncthreads();
+  return s_cut;
+}
+
 template <int METRIC, int NT, int EPL>
 __global__ void __launch_bounds__(NT)
 merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, int U, int R,
                     TrainDev t, const double* __restrict__ Q64, int W, int Cmax, int C2,
-                    double f_err, ProxyScale ps, const uint32_t* __restrict__ gthr,
-                    int gstride, SegCands seg, Sink sink, int* __restrict__ rescan_q,
+                    double f_err, double f32_err, ProxyScale ps,
+                    const uint32_t* __restrict__ gthr, Sink sink, int* __restrict__ rescan_q,
                     double* __restrict__ rescan_tau, int* __restrict__ rescan_cnt) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int s_cn, s_cert;
-  __shared__ double s_lb, s_qa, s_e;
+  __shared__ double s_lb, s_qa, s_e, s_e32;
   const int d = t.d;
   // the query row is staged in LDS up to kMergeLdsDim dims, else read in place
   const bool q_in_lds = d <= kMergeLdsDim;
@@ -167,6 +214,8 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
   double* tb = dk + C2;
   int* di = (int*)(tb + NT * 17);
   int* ls = di + C2;
+  // fp32 query operand of the large-d prefilter [DP] (16-B aligned: float4 reads)
+  float* qf = (float*)(((uintptr_t)(ls + C2) + 15) & ~(uintptr_t)15);
   const int64_t q = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63;
 
@@ -224,72 +273,23 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
     const bool void_q = !(vq > 0.0f);
     const bool nonfinite = vq < 0.0f;
     // union in registers; min over full lists of their R-th (worst kept) entry
+    const float* lv = cv + q * U;
+    const int* li = ci + q * U;
     float v[EPL];
     int id[EPL];
     float mlr = KNN_INF_F;
     int nv = 0;
-    int ne = EPL;  // register rows holding entries (the scan path: ceil(total / 64))
-    if (seg.buf) {
-      // scan-kernel segments, read compacted: lane s holds segment s's entry
-      // count; entry x of the union lies in the first segment whose inclusive
-      // prefix count exceeds x (binary search over the lanes).  A segment that
-      // overflowed dropped rows below the filter threshold, and a union
-      // larger than the registers leaves rows unread: nothing then bounds the
-      // rows left out (mlr = -inf: the query goes to the rescan with the W-th
-      // exact distance it has)
-      const int* sc = seg.cnt + q * seg.nseg;
-      int c = 0;
-      bool ov = false;
-      if (lane < seg.nseg) {
-        const int r = sc[lane];
-        c = min(r, seg.cap);
-        ov = r > seg.cap;
-      }
-      int incl = c;
 #pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += y;
+    for (int e = 0; e < EPL; ++e) {
+      const int x = lane + 64 * e;
+      v[e] = KNN_INF_F;
+      id[e] = -1;
+      if (x < U) {
+        v[e] = lv[x];
+        id[e] = li[x];
+        if (x % R == R - 1) mlr = fminf(mlr, v[e]);
       }
-      const int total = __shfl(incl, 63, 64);
-      if (__ballot(ov) || total > EPL * 64) mlr = -KNN_INF_F;
-      const int tot = min(total, EPL * 64);
-      ne = (tot + 63) >> 6;
-      const int2* sb = seg.buf + q * U;
-#pragma unroll
-      for (int e = 0; e < EPL; ++e) {
-        const int x = lane + 64 * e;
-        v[e] = KNN_INF_F;
-        id[e] = -1;
-        if (e < ne) {
-          int sg = 0;
-#pragma unroll
-          for (int st = 32; st > 0; st >>= 1)
-            if (__shfl(incl, sg + st - 1, 64) <= x) sg += st;
-          const int j = x - (__shfl(incl, sg, 64) - __shfl(c, sg, 64));
-          if (x < tot) {
-            const int2 pr = sb[sg * seg.cap + j];
-            v[e] = __int_as_float(pr.x);
-            id[e] = pr.y;
-          }
-        }
-      }
-      nv = tot;
-    } else {
-      const float* lv = cv + q * U;
-      const int* li = ci + q * U;
-#pragma unroll
-      for (int e = 0; e < EPL; ++e) {
-        const int x = lane + 64 * e;
-        v[e] = KNN_INF_F;
-        id[e] = -1;
-        if (x < U) {
-          v[e] = lv[x];
-          id[e] = li[x];
-          if (x % R == R - 1) mlr = fminf(mlr, v[e]);
-        }
-        nv += __popcll(__ballot(v[e] < KNN_INF_F));
-      }
+      nv += __popcll(__ballot(v[e] < KNN_INF_F));
     }
     mlr = wave_min(mlr);
     double tsel = KNN_INF_D;  // select proxies <= tsel
@@ -299,8 +299,7 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
         const uint32_t T = pre | ((1u << b) - 1u);
         int cnt = 0;
 #pragma unroll
-        for (int e = 0; e < EPL; ++e)
-          if (e < ne) cnt += __popcll(__ballot(f2key(v[e]) <= T));
+        for (int e = 0; e < EPL; ++e) cnt += __popcll(__ballot(f2key(v[e]) <= T));
         if (cnt < W) pre |= 1u << b;
       }
       const double vw = (double)key2f(pre) * pinv;
@@ -332,8 +331,7 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
         const uint32_t T = pre | ((1u << b) - 1u);
         int cnt = 0;
 #pragma unroll
-        for (int e = 0; e < EPL; ++e)
-          if (e < ne) cnt += __popcll(__ballot(v[e] < KNN_INF_F && f2key(v[e]) <= T));
+        for (int e = 0; e < EPL; ++e) cnt += __popcll(__ballot(v[e] < KNN_INF_F && f2key(v[e]) <= T));
         if (cnt < Cmax) pre |= 1u << b;
       }
       cn = 0;
@@ -356,13 +354,16 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
     // the candidate kernel also filtered with the query's global threshold
     // (cand_kernel): rows it dropped have proxy >= its final value
     float tq = KNN_INF_F;
-    if (gthr && gstride == 4) {
+    if (gthr) {
       const uint32_t* g = gthr + q * 4;
       tq = key2f(max(max(g[0], g[1]), max(g[2], g[3])));
-    } else if (gthr) {
-      tq = key2f(gthr[q * gstride]);
     }
     if (lane == 0) {
+      // fp32 prefilter bound (the fp32 candidate path's fmaf-chain model and
+      // absolute terms, unscaled; fp32_prefilter)
+      s_e32 = f32_err * (t.x2max + 2.1 * __builtin_sqrt(qa) * __builtin_sqrt(t.x2max)) +
+              0x1p-125 * 1.001 * (2.0 * q1 + t.x1max) * sinv + t.DP * 0x1p-124 * sinv * sinv +
+              1e-300;
       // void proxies: exact rescan below; non-finite query: no neighbours
       s_cn = nonfinite ? -1 : (void_q ? Cmax + 1 : cn);
       s_lb = (double)fminf(fminf(lbx, mlr), tq) * pinv;
@@ -385,7 +386,12 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
     return;
   }
 
-  exact_sorted<METRIC, NT>(t, qv, di, dk, tb, cn, C2, tid);
+  // large d: rows the fp32 proxies rule out skip the fp64 re-rank; they are
+  // not counted below (cn2 <= cn), the W-th exact distance is unchanged
+  const int cn2 = (METRIC == 0 && d > kPrefilterMinD && cn > W)
+                      ? fp32_prefilter<NT>(t, qv, qf, di, dk, cn, C2, W, s_e32, tid)
+                      : cn;
+  exact_sorted<METRIC, NT>(t, qv, di, dk, tb, cn2, C2, tid);
 
   // certification: every row not re-ranked has proxy >= LB, hence exact
   // distance >= the bound below (rigorous error bound E)
@@ -395,8 +401,8 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
     if (cn < W) {
       cert = false;  // fewer rows than the top W re-ranked (e.g. non-finite proxies)
     } else if (!(LB < KNN_INF_D)) {
-      // no bound on the rows left out (a candidate path without a filter
-      // threshold whose lists never filled): not certified
+      // no bound on the rows left out (lists that never filled and no filter
+      // threshold): not certified, the rescan decides
       cert = false;
     } else {
       const double dw = dk[W - 1], qa = s_qa, E = s_e;
@@ -421,42 +427,41 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
   if (!s_cert) return;
 
   const int need = sink.mode == MODE_SINGLE ? sink.k : sink.w;
-  for (int c = tid; c < need && c < cn; c += NT) ls[c] = t.lab[di[c]];
+  for (int c = tid; c < need && c < cn2; c += NT) ls[c] = t.lab[di[c]];
   __syncthreads();
   if (tid < 64) {
     if (sink.mode == MODE_SINGLE)
-      finish_single(q, dk, di, ls, cn, sink.k, sink.idx_off, 0, sink);
+      finish_single(q, dk, di, ls, cn2, sink.k, sink.idx_off, 0, sink);
     else
-      finish_partial(q, dk, di, ls, cn, sink.w, sink.idx_off, sink);
+      finish_partial(q, dk, di, ls, cn2, sink.w, sink.idx_off, sink);
   }
 }
 
 template <int METRIC, int NT, int EPL>
 static void launch_mr(const float* cv, const int* ci, int U, int R, const TrainDev& t,
                       const double* Q64, int64_t m, int W, int Cmax, int C2, double f_err,
-                      ProxyScale ps, const uint32_t* gthr, int gstride, SegCands seg,
-                      const Sink& sink, int* rescan_q, double* rescan_tau, int* rescan_cnt,
-                      hipStream_t s) {
+                      double f32_err, ProxyScale ps, const uint32_t* gthr, const Sink& sink,
+                      int* rescan_q, double* rescan_tau, int* rescan_cnt, hipStream_t s) {
   const size_t lds = (size_t)(t.d <= kMergeLdsDim ? t.d : 0) * 8 + (size_t)C2 * 8 +
-                     (size_t)NT * 17 * 8 + (size_t)C2 * 8;
+                     (size_t)NT * 17 * 8 + (size_t)C2 * 8 +
+                     (METRIC == 0 && t.d > kPrefilterMinD ? (size_t)t.DP * 4 + 16 : 0);
   hipLaunchKernelGGL((merge_rerank_kernel<METRIC, NT, EPL>), dim3((unsigned)m), dim3(NT), lds, s,
-                     cv, ci, U, R, t, Q64, W, Cmax, C2, f_err, ps, gthr, gstride, seg, sink, rescan_q,
+                     cv, ci, U, R, t, Q64, W, Cmax, C2, f_err, f32_err, ps, gthr, sink, rescan_q,
                      rescan_tau, rescan_cnt);
 }
 
 void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int R,
                          const TrainDev& t, const double* Q64, int64_t m, int W, int C,
-                         double f_err, ProxyScale ps, const uint32_t* gthr, int gstride,
-                         SegCands seg, const Sink& sink, int* rescan_q, double* rescan_tau,
-                         int* rescan_cnt, hipStream_t s) {
+                         double f_err, double f32_err, ProxyScale ps, const uint32_t* gthr,
+                         const Sink& sink, int* rescan_q, double* rescan_tau, int* rescan_cnt,
+                         hipStream_t s) {
   if (m <= 0) return;
-  // <= 2 * 64 * 16 (choose_geometry bounds S and R; the scan path nseg * cap)
-  const int U = seg.buf ? seg.nseg * seg.cap : NL * R;
+  const int U = NL * R;  // <= 2 * 64 * 16 (choose_geometry bounds S and R)
   int C2 = 1;
   while (C2 < C) C2 <<= 1;
   const bool big = C2 > 64, wide = U > 1024;
 #define KNN_MR(M_, NT_, EPL_) \
-  launch_mr<M_, NT_, EPL_>(cv, ci, U, R, t, Q64, m, W, C, C2, f_err, ps, gthr, gstride, seg, sink, \
+  launch_mr<M_, NT_, EPL_>(cv, ci, U, R, t, Q64, m, W, C, C2, f_err, f32_err, ps, gthr, sink, \
                            rescan_q, rescan_tau, rescan_cnt, s)
   if (metric == 0) {
     if (big) { if (wide) KNN_MR(0, 256, 32); else KNN_MR(0, 256, 16); }
@@ -621,9 +626,12 @@ rescan_filter_kernel(TrainDev t, const float* __restrict__ qf, const float* __re
   }
 }
 
-// DP > 256 (rows too long to stage 64 per wave): lane = train row, read in
-// place from X32 (each lane walks its own row in 16-B steps; the lines it
-// touches are reused from L1/L2 by its next loads), queries from LDS.
+// DP > 256 (rows too long to stage 64 per wave): 4 lanes per train row, 16
+// rows per wave step; lane part p of row r reads float4 p, p+4, p+8, ... of
+// the row (a wave-instruction covers 64 contiguous bytes of each of its 16
+// rows, read in place from X32) against the queries in LDS, and the 4
+// partial sums of each query are added by two xor-shuffles.  The fp32 error
+// bound of the fmaf chain holds for any summation order (Higham 3.1).
 template <int METRIC, int FQ>
 __global__ void __launch_bounds__(256)
 rescan_filter_wide_kernel(TrainDev t, const float* __restrict__ qf, const float* __restrict__ thr,
@@ -635,8 +643,8 @@ rescan_filter_wide_kernel(TrainDev t, const float* __restrict__ qf, const float*
   const int DP = t.DP, RSF = DP + 4;
   float* qs = fsm;             // [FQ][DP]
   float* thr_s = qs + FQ * DP; // [FQ]
-  const int tid = threadIdx.x;
-  const int64_t row = (int64_t)blockIdx.x * blockDim.x + tid;
+  const int tid = threadIdx.x, lane = tid & 63, part = lane & 3;
+  const int64_t row = ((int64_t)blockIdx.x * 4 + (tid >> 6)) * 16 + (lane >> 2);
   const bool active = row < t.n_pad;
   const float* xr = t.X32 + (active ? row : 0) * RSF;
   for (int g0 = 0; g0 < nf; g0 += FQ) {
@@ -648,31 +656,39 @@ rescan_filter_wide_kernel(TrainDev t, const float* __restrict__ qf, const float*
     }
     if (tid < FQ) thr_s[tid] = tid < nfg ? thr[g0 + tid] : -KNN_INF_F;
     __syncthreads();
-    if (active) {
-      const float seed = xr[METRIC == 0 ? DP : DP + 1];
-      float acc[FQ];
+    float acc[FQ];
 #pragma unroll
-      for (int qi = 0; qi < FQ; ++qi) acc[qi] = seed;
-      for (int c = 0; c < DP / 4; ++c) {
-        const float4 x4 = *(const float4*)(xr + 4 * c);
+    for (int qi = 0; qi < FQ; ++qi) acc[qi] = 0.0f;
+#pragma unroll 4
+    for (int c = 4 * part; c < DP; c += 16) {
+      const float4 x4 = *(const float4*)(xr + c);
 #pragma unroll
-        for (int qi = 0; qi < FQ; ++qi) {
-          const float4 q4 = *(const float4*)(qs + qi * DP + 4 * c);
-          float a = acc[qi];
-          if (METRIC == 0) {
-            a = __builtin_fmaf(q4.x, x4.x, a);
-            a = __builtin_fmaf(q4.y, x4.y, a);
-            a = __builtin_fmaf(q4.z, x4.z, a);
-            a = __builtin_fmaf(q4.w, x4.w, a);
-          } else {
-            a = a + __builtin_fabsf(q4.x - x4.x);
-            a = a + __builtin_fabsf(q4.y - x4.y);
-            a = a + __builtin_fabsf(q4.z - x4.z);
-            a = a + __builtin_fabsf(q4.w - x4.w);
-          }
-          acc[qi] = a;
+      for (int qi = 0; qi < FQ; ++qi) {
+        const float4 q4 = *(const float4*)(qs + qi * DP + c);
+        float a = acc[qi];
+        if (METRIC == 0) {
+          a = __builtin_fmaf(q4.x, x4.x, a);
+          a = __builtin_fmaf(q4.y, x4.y, a);
+          a = __builtin_fmaf(q4.z, x4.z, a);
+          a = __builtin_fmaf(q4.w, x4.w, a);
+        } else {
+          a = a + __builtin_fabsf(q4.x - x4.x);
+          a = a + __builtin_fabsf(q4.y - x4.y);
+          a = a + __builtin_fabsf(q4.z - x4.z);
+          a = a + __builtin_fabsf(q4.w - x4.w);
         }
+        acc[qi] = a;
       }
+    }
+    const float seed = xr[METRIC == 0 ? DP : DP + 1];  // +inf on pad rows: never passes
+#pragma unroll
+    for (int qi = 0; qi < FQ; ++qi) {
+      float a = acc[qi];
+      a += __shfl_xor(a, 1, 64);
+      a += __shfl_xor(a, 2, 64);
+      acc[qi] = a + seed;
+    }
+    if (active && part == 0) {
 #pragma unroll
       for (int qi = 0; qi < FQ; ++qi)
         if (qi < nfg) rescan_append(acc[qi], thr_s[qi], g0 + qi, row, fcnt, buf);
@@ -873,7 +889,7 @@ void launch_rescan(int metric, const TrainDev& t, const double* Q64, const Resca
         hipLaunchKernelGGL((rescan_filter_kernel<1, FQ>), fg, dim3(64 * nwb), flds, s, t, rb.qf,
                            rb.thr, rb.cnt, cap, rb.fcnt, rb.buf);
     } else {
-      const dim3 fg((unsigned)((t.n_pad + 255) / 256));
+      const dim3 fg((unsigned)((t.n_pad + 63) / 64));  // 64 rows per 4-wave block
       if (metric == 0)
         hipLaunchKernelGGL((rescan_filter_wide_kernel<0, FQ>), fg, dim3(256), qbytes, s, t, rb.qf,
                            rb.thr, rb.cnt, cap, rb.fcnt, rb.buf);

@@ -34,20 +34,16 @@ def knn():
     return mod
 
 
-@pytest.fixture(scope="module", params=["auto", "fp32", "m16", "fp16", "scan"])
+@pytest.fixture(scope="module", params=["auto", "fp32", "m16", "fp16"])
 def clf(knn, request):
     """Every parity test runs with the default candidate path (AUTO: fp16 for
     batches of >= 4096 queries at d <= 256, else bf16x3 on 32x32x16 for L2),
     with the fp32 path forced, with bf16x3 on the 16x16x32 MFMA layout forced,
-    with the fp16 list path forced (every batch size, threshold scan off) and
-    with the fp16 threshold scan forced (sample pre-pass + scan kernel, every
-    batch and train size; L2 at d <= 256)."""
+    and with the fp16 path forced (every batch size)."""
     c = knn.Classifier(0)
     c.set_precision({"auto": knn.PRECISION_AUTO, "fp32": knn.PRECISION_FP32,
-                     "m16": knn.PRECISION_BF16X3, "fp16": knn.PRECISION_FP16,
-                     "scan": knn.PRECISION_FP16}[request.param])
+                     "m16": knn.PRECISION_BF16X3, "fp16": knn.PRECISION_FP16}[request.param])
     c.set_tuning("mfma16", 1 if request.param == "m16" else -1)
-    c.set_tuning("scan", {"fp16": 0, "scan": 1}.get(request.param, -1))
     yield c
     c.close()
 

@@ -7,8 +7,8 @@ Variants: "prec:R:S[:ablate[:nw]]" e.g. auto:0:0 fp32:8:0 auto:8:0:1:8
  = fp16 on the 16x16x32 MFMA)
 (ablate bits: 1 = no staging loads, 2 = no selection epilogue; timing only;
 nw = waves per candidate workgroup, 0 auto / 4 / 8)
-Extra tuning keys after a comma, e.g. "fp16:0:0,scan=1,scan_a=512" (keys not
-named by a variant are reset to automatic: scan -1, scan_a 0, scan_cap 0)."""
+Extra tuning keys after a comma, e.g. "fp16:0:0,mfma16=1" (keys listed in
+`defaults` and not named by a variant are reset to automatic)."""
 import argparse
 import os
 import sys
@@ -45,7 +45,7 @@ def main():
     info = {}
     prec = {"auto": knn.PRECISION_AUTO, "fp32": knn.PRECISION_FP32, "bf16x3": knn.PRECISION_BF16X3,
             "m16": knn.PRECISION_BF16X3, "fp16": knn.PRECISION_FP16}
-    defaults = {"scan": -1, "scan_a": 0, "scan_cap": 0}
+    defaults = {}
     for r in range(a.rounds + 1):
         for v in a.variants:
             base, *extra = v.split(",")
