@@ -385,6 +385,16 @@ static void choose_geometry(knn_ctx* ctx, int metric, bool streamed, int DP, int
     // one list, has probability ~C(W,5)/(8S)^5 -- 0.7 % of cfg3's queries
     // failed at S = W, each an exact rescan), at least S >= W
     if (quad) S_lo = std::max(S_lo, std::max<int>(W, (int)std::min<int64_t>(2 * W, n_tiles / 32)));
+    // R = 8 needs an expected share of the top W per list (2S lists) of at
+    // most 0.8 (S >= W / 1.6): a list overflow (9 of them in one list -> the
+    // query fails certification) then has probability < 1e-6 per list; at a
+    // share of 1.6 (cfg5, W = 101, S = 32) 1.6 % of the queries failed.
+    // Where no such S exists R = 16 runs instead.
+    if (R == 8 && !ctx->tune_R) {
+      const int s8 = (W * 5 + 7) / 8;
+      if (s8 > S_hi) continue;
+      S_lo = std::max(S_lo, s8);
+    }
     S_lo = std::min(S_hi, S_lo);
     auto eff_of = [&](int S) {
       const int64_t wg = (int64_t)n_qt * S;
@@ -409,11 +419,7 @@ static void choose_geometry(knn_ctx* ctx, int metric, bool streamed, int DP, int
     if (ctx->tune_S) bS = std::min(ctx->tune_S, S_hi);
     bestS = bS;
     bestR = R;
-    // R = 8 when the expected share of the top W per list (2S lists) is at
-    // most 1/2: a list overflow (9 of the top W in one list -> certification
-    // fails) is then rare (at a share of 1.6 -- cfg5, W = 101, S = 32 -- 1.6 %
-    // of the queries failed); else R = 16.
-    if (ctx->tune_R || quad || W <= bS) break;
+    break;
   }
   S_out = bestS;
   R_out = bestR;
@@ -626,7 +632,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   if (tc) HIP_TRY(hipEventRecord(tc->ev[2], s));
   HIP_TRY(hipMemsetAsync(ctx->rescan_cnt.p, 0, 4 * sizeof(int), s));
   launch_merge_rerank(metric, (const float*)ctx->cand_v.p, (const int*)ctx->cand_i.p, NL, R, t, dQ,
-                      m, W, C, err_factor(kmetric, DP), err_factor(0, t.DP),
+                      m, W, C, err_factor(kmetric, DP),
                       kmetric == 4 ? ProxyScale{qvalid, 0x1p-14, 0x1p-28, true}
                                    : ProxyScale{qvalid, 0x1p-125, 0x1p-124},
                       cl.gthr, sink, (int*)ctx->rescan_q.p,

@@ -134,9 +134,8 @@ struct ProxyScale {
 };
 void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int R,
                          const TrainDev& t, const double* Q64, int64_t m, int W, int C,
-                         double f_err, double f32_err, ProxyScale ps, const uint32_t* gthr,
-                         const Sink& sink, int* rescan_q, double* rescan_tau, int* rescan_cnt,
-                         hipStream_t s);
+                         double f_err, ProxyScale ps, const uint32_t* gthr, const Sink& sink,
+                         int* rescan_q, double* rescan_tau, int* rescan_cnt, hipStream_t s);
 constexpr int kRescanCap = 1024;        // rows a fast rescan may append per query
 constexpr int kRescanStageMaxDP = 256;  // fast rescan stages rows in LDS up to this DP
 constexpr int kRescanFastQueries = 65536;  // failed queries per call the fast path serves

@@ -106,28 +106,48 @@ __device__ __forceinline__ int lanes_below(unsigned long long mask) {
 // row piece) into an LDS tile of squared (L1: absolute) differences, then
 // thread c adds its candidate's terms in dimension order -- bit-exact with
 // cpp:33-50 / cpp:51-67 (sequential, no FMA; sqrt correctly rounded).
+// (The squared difference is formed from the same fp64 operands in the
+// same operation as before the prefetch: the result bits are unchanged.)
 // Pads [cn, C2) with (+inf, INT_MAX) and sorts (dist, idx) ascending.
 // All NT threads; tb holds NT x 17 doubles.
 template <int METRIC, int NT>
 __device__ void exact_sorted(const TrainDev& t, const double* qv, int* di, double* dk, double* tb,
                              int cn, int C2, int tid) {
   const int d = t.d;
+  // the raw fp64 values of a 16-dim chunk, EPT per thread (nb * 16 <= NT * 16);
+  // two register sets in flight: chunk c+1's and c+2's loads overlap chunk c's
+  // sums and barriers (rows of 7.7 KB at d = 960 make this an HBM stream)
+  constexpr int EPT = 16;
   for (int b0 = 0; b0 < cn; b0 += NT) {
     const int nb = min(NT, cn - b0);
-    double r = 0.0;
-    for (int c0 = 0; c0 < d; c0 += 16) {
-      const int nd = min(16, d - c0);
-      for (int e = tid; e < nb * 16; e += NT) {
+    const int ne = nb * 16;
+    auto fetch = [&](int c0, double (&o)[EPT]) {
+#pragma unroll
+      for (int k = 0; k < EPT; ++k) {
+        const int e = tid + k * NT;
         const int c = e >> 4, j = e & 15;
-        double val = 0.0;
-        if (j < nd) {
-          const double x = t.X64[(int64_t)di[b0 + c] * d + c0 + j];
-          const double tq = qv[c0 + j] - x;
-          val = METRIC == 0 ? tq * tq : __builtin_fabs(tq);
+        o[k] = (e < ne && c0 + j < d) ? t.X64[(int64_t)di[b0 + c] * d + c0 + j] : 0.0;
+      }
+    };
+    double r = 0.0;
+    // stage chunk c0 (values in x) into tb, refill x with chunk c0 + 32, add
+    auto step = [&](int c0, double (&x)[EPT]) {
+      const int nd = min(16, d - c0);
+#pragma unroll
+      for (int k = 0; k < EPT; ++k) {
+        const int e = tid + k * NT;
+        const int c = e >> 4, j = e & 15;
+        if (e < ne) {
+          double val = 0.0;
+          if (j < nd) {
+            const double tq = qv[c0 + j] - x[k];
+            val = METRIC == 0 ? tq * tq : __builtin_fabs(tq);
+          }
+          tb[c * 17 + j] = val;
         }
-        tb[c * 17 + j] = val;
       }
       __syncthreads();
+      if (c0 + 32 < d) fetch(c0 + 32, x);
       if (tid < nb) {
         const double* row = tb + tid * 17;
         if (nd == 16) {
@@ -138,6 +158,13 @@ __device__ void exact_sorted(const TrainDev& t, const double* qv, int* di, doubl
         }
       }
       __syncthreads();
+    };
+    double xa[EPT], xb[EPT];
+    fetch(0, xa);
+    if (16 < d) fetch(16, xb);
+    for (int c0 = 0; c0 < d; c0 += 32) {
+      step(c0, xa);
+      if (c0 + 16 < d) step(c0 + 16, xb);
     }
     if (tid < nb) dk[b0 + tid] = METRIC == 0 ? __builtin_sqrt(r) : r;  // correctly rounded
   }
@@ -150,63 +177,16 @@ __device__ void exact_sorted(const TrainDev& t, const double* qv, int* di, doubl
   bitonic_sort_lds(dk, di, C2, tid, NT);
 }
 
-// Large d (> kPrefilterMinD, L2): the selected rows' fp64 rows are the
-// merge's main HBM stream (cfg5: ~200 rows x 7.7 KB per query).  A first
-// pass computes each selected row's fp32 proxy from the fp32 copy X32 (half
-// the bytes; an fmaf chain, rigorous bound e32 in unscaled units) and sorts
-// the rows by it; a row whose fp32 proxy exceeds the W-th smallest by more
-// than 2 e32 cannot be in the top W -- the W rows below it all have exact
-// distances below its own -- so only the prefix within reach goes on to the
-// exact fp64 re-rank.  Returns that prefix length (di[0..) reordered).
-constexpr int kPrefilterMinD = 256;
-template <int NT>
-__device__ int fp32_prefilter(const TrainDev& t, const double* qv, float* qf, int* di, double* dk,
-                              int cn, int C2, int W, double e32, int tid) {
-  __shared__ int s_cut;
-  const int DP = t.DP, RSF = DP + 4;
-  for (int i = tid; i < DP; i += NT)
-    qf[i] = i < t.d ? (float)__builtin_ldexp(-2.0 * (qv[i] - t.mu[i]), t.jx) : 0.0f;
-  if (tid == 0) s_cut = cn;
-  __syncthreads();
-  const double pinv = __builtin_ldexp(1.0, -2 * t.jx);
-  for (int c = tid; c < C2; c += NT) {
-    double p = KNN_INF_D;
-    if (c < cn) {
-      const float* xr = t.X32 + (int64_t)di[c] * RSF;
-      float a = xr[DP];  // fl32(||x32||^2)
-#pragma unroll 8
-      for (int i = 0; i < DP; i += 4) {
-        const float4 x4 = *(const float4*)(xr + i);
-        const float4 q4 = *(const float4*)(qf + i);
-        a = __builtin_fmaf(q4.x, x4.x, a);
-        a = __builtin_fmaf(q4.y, x4.y, a);
-        a = __builtin_fmaf(q4.z, x4.z, a);
-        a = __builtin_fmaf(q4.w, x4.w, a);
-      }
-      p = (double)a * pinv;
-    } else {
-      di[c] = INT_MAX;
-    }
-    dk[c] = p;
-  }
-  bitonic_sort_lds(dk, di, C2, tid, NT);
-  const double cut = dk[W - 1] + 2.0 * e32 + 1e-9 * (__builtin_fabs(dk[W - 1]) + e32) + 1e-300;
-  for (int c = tid; c < cn; c += NT)
-    if (dk[c] > cut && (c == 0 || !(dk[c - 1] > cut))) s_cut = c;  // first row past the cut
-  __syncthreads();
-  return s_cut;
-}
-
 template <int METRIC, int NT, int EPL>
 __global__ void __launch_bounds__(NT)
 merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, int U, int R,
                     TrainDev t, const double* __restrict__ Q64, int W, int Cmax, int C2,
-                    double f_err, double f32_err, ProxyScale ps,
-                    const uint32_t* __restrict__ gthr, Sink sink, int* __restrict__ rescan_q,
-                    double* __restrict__ rescan_tau, int* __restrict__ rescan_cnt) {
+                    double f_err, ProxyScale ps, const uint32_t* __restrict__ gthr, Sink sink,
+                    int* __restrict__ rescan_q, double* __restrict__ rescan_tau,
+                    int* __restrict__ rescan_cnt) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int s_cn, s_cert;
-  __shared__ double s_lb, s_qa, s_e, s_e32;
+  __shared__ double s_lb, s_qa, s_e;
   const int d = t.d;
   // the query row is staged in LDS up to kMergeLdsDim dims, else read in place
   const bool q_in_lds = d <= kMergeLdsDim;
@@ -214,8 +194,6 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
   double* tb = dk + C2;
   int* di = (int*)(tb + NT * 17);
   int* ls = di + C2;
-  // fp32 query operand of the large-d prefilter [DP] (16-B aligned: float4 reads)
-  float* qf = (float*)(((uintptr_t)(ls + C2) + 15) & ~(uintptr_t)15);
   const int64_t q = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63;
 
@@ -359,11 +337,6 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
       tq = key2f(max(max(g[0], g[1]), max(g[2], g[3])));
     }
     if (lane == 0) {
-      // fp32 prefilter bound (the fp32 candidate path's fmaf-chain model and
-      // absolute terms, unscaled; fp32_prefilter)
-      s_e32 = f32_err * (t.x2max + 2.1 * __builtin_sqrt(qa) * __builtin_sqrt(t.x2max)) +
-              0x1p-125 * 1.001 * (2.0 * q1 + t.x1max) * sinv + t.DP * 0x1p-124 * sinv * sinv +
-              1e-300;
       // void proxies: exact rescan below; non-finite query: no neighbours
       s_cn = nonfinite ? -1 : (void_q ? Cmax + 1 : cn);
       s_lb = (double)fminf(fminf(lbx, mlr), tq) * pinv;
@@ -386,12 +359,7 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
     return;
   }
 
-  // large d: rows the fp32 proxies rule out skip the fp64 re-rank; they are
-  // not counted below (cn2 <= cn), the W-th exact distance is unchanged
-  const int cn2 = (METRIC == 0 && d > kPrefilterMinD && cn > W)
-                      ? fp32_prefilter<NT>(t, qv, qf, di, dk, cn, C2, W, s_e32, tid)
-                      : cn;
-  exact_sorted<METRIC, NT>(t, qv, di, dk, tb, cn2, C2, tid);
+  exact_sorted<METRIC, NT>(t, qv, di, dk, tb, cn, C2, tid);
 
   // certification: every row not re-ranked has proxy >= LB, hence exact
   // distance >= the bound below (rigorous error bound E)
@@ -427,42 +395,40 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
   if (!s_cert) return;
 
   const int need = sink.mode == MODE_SINGLE ? sink.k : sink.w;
-  for (int c = tid; c < need && c < cn2; c += NT) ls[c] = t.lab[di[c]];
+  for (int c = tid; c < need && c < cn; c += NT) ls[c] = t.lab[di[c]];
   __syncthreads();
   if (tid < 64) {
     if (sink.mode == MODE_SINGLE)
-      finish_single(q, dk, di, ls, cn2, sink.k, sink.idx_off, 0, sink);
+      finish_single(q, dk, di, ls, cn, sink.k, sink.idx_off, 0, sink);
     else
-      finish_partial(q, dk, di, ls, cn2, sink.w, sink.idx_off, sink);
+      finish_partial(q, dk, di, ls, cn, sink.w, sink.idx_off, sink);
   }
 }
 
 template <int METRIC, int NT, int EPL>
 static void launch_mr(const float* cv, const int* ci, int U, int R, const TrainDev& t,
                       const double* Q64, int64_t m, int W, int Cmax, int C2, double f_err,
-                      double f32_err, ProxyScale ps, const uint32_t* gthr, const Sink& sink,
-                      int* rescan_q, double* rescan_tau, int* rescan_cnt, hipStream_t s) {
+                      ProxyScale ps, const uint32_t* gthr, const Sink& sink, int* rescan_q,
+                      double* rescan_tau, int* rescan_cnt, hipStream_t s) {
   const size_t lds = (size_t)(t.d <= kMergeLdsDim ? t.d : 0) * 8 + (size_t)C2 * 8 +
-                     (size_t)NT * 17 * 8 + (size_t)C2 * 8 +
-                     (METRIC == 0 && t.d > kPrefilterMinD ? (size_t)t.DP * 4 + 16 : 0);
+                     (size_t)NT * 17 * 8 + (size_t)C2 * 8;
   hipLaunchKernelGGL((merge_rerank_kernel<METRIC, NT, EPL>), dim3((unsigned)m), dim3(NT), lds, s,
-                     cv, ci, U, R, t, Q64, W, Cmax, C2, f_err, f32_err, ps, gthr, sink, rescan_q,
-                     rescan_tau, rescan_cnt);
+                     cv, ci, U, R, t, Q64, W, Cmax, C2, f_err, ps, gthr, sink, rescan_q, rescan_tau,
+                     rescan_cnt);
 }
 
 void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int R,
                          const TrainDev& t, const double* Q64, int64_t m, int W, int C,
-                         double f_err, double f32_err, ProxyScale ps, const uint32_t* gthr,
-                         const Sink& sink, int* rescan_q, double* rescan_tau, int* rescan_cnt,
-                         hipStream_t s) {
+                         double f_err, ProxyScale ps, const uint32_t* gthr, const Sink& sink,
+                         int* rescan_q, double* rescan_tau, int* rescan_cnt, hipStream_t s) {
   if (m <= 0) return;
   const int U = NL * R;  // <= 2 * 64 * 16 (choose_geometry bounds S and R)
   int C2 = 1;
   while (C2 < C) C2 <<= 1;
   const bool big = C2 > 64, wide = U > 1024;
 #define KNN_MR(M_, NT_, EPL_) \
-  launch_mr<M_, NT_, EPL_>(cv, ci, U, R, t, Q64, m, W, C, C2, f_err, f32_err, ps, gthr, sink, \
-                           rescan_q, rescan_tau, rescan_cnt, s)
+  launch_mr<M_, NT_, EPL_>(cv, ci, U, R, t, Q64, m, W, C, C2, f_err, ps, gthr, sink, rescan_q, \
+                           rescan_tau, rescan_cnt, s)
   if (metric == 0) {
     if (big) { if (wide) KNN_MR(0, 256, 32); else KNN_MR(0, 256, 16); }
     else { if (wide) KNN_MR(0, 64, 32); else KNN_MR(0, 64, 16); }
@@ -603,6 +569,7 @@ rescan_filter_kernel(TrainDev t, const float* __restrict__ qf, const float* __re
         const float4 x4 = *(const float4*)(xr + 4 * c);
 #pragma unroll
         for (int qi = 0; qi < FQ; ++qi) {
+          if (qi >= nfg) break;  // group-uniform: no LDS reads for empty query slots
           const float4 q4 = *(const float4*)(qs + qi * DP + 4 * c);
           float a = acc[qi];
           if (METRIC == 0) {  // the candidate pass's fp32 model: an fmaf chain
@@ -664,6 +631,7 @@ rescan_filter_wide_kernel(TrainDev t, const float* __restrict__ qf, const float*
       const float4 x4 = *(const float4*)(xr + c);
 #pragma unroll
       for (int qi = 0; qi < FQ; ++qi) {
+        if (qi >= nfg) break;  // group-uniform: no LDS reads for empty query slots
         const float4 q4 = *(const float4*)(qs + qi * DP + c);
         float a = acc[qi];
         if (METRIC == 0) {
@@ -889,12 +857,17 @@ void launch_rescan(int metric, const TrainDev& t, const double* Q64, const Resca
         hipLaunchKernelGGL((rescan_filter_kernel<1, FQ>), fg, dim3(64 * nwb), flds, s, t, rb.qf,
                            rb.thr, rb.cnt, cap, rb.fcnt, rb.buf);
     } else {
-      const dim3 fg((unsigned)((t.n_pad + 63) / 64));  // 64 rows per 4-wave block
+      // 64 rows per 4-wave block; 8 queries per pass (a failed query is rare
+      // at d > 256: the LDS of 8 query rows leaves room for 5 blocks per CU,
+      // i.e. more row loads in flight than 2 blocks with 16 queries)
+      constexpr int FQW = 8;
+      const size_t qbw = (size_t)FQW * (t.DP + 1) * 4;
+      const dim3 fg((unsigned)((t.n_pad + 63) / 64));
       if (metric == 0)
-        hipLaunchKernelGGL((rescan_filter_wide_kernel<0, FQ>), fg, dim3(256), qbytes, s, t, rb.qf,
+        hipLaunchKernelGGL((rescan_filter_wide_kernel<0, FQW>), fg, dim3(256), qbw, s, t, rb.qf,
                            rb.thr, rb.cnt, cap, rb.fcnt, rb.buf);
       else
-        hipLaunchKernelGGL((rescan_filter_wide_kernel<1, FQ>), fg, dim3(256), qbytes, s, t, rb.qf,
+        hipLaunchKernelGGL((rescan_filter_wide_kernel<1, FQW>), fg, dim3(256), qbw, s, t, rb.qf,
                            rb.thr, rb.cnt, cap, rb.fcnt, rb.buf);
     }
     const size_t lds = (size_t)(t.d <= 1024 ? t.d : 0) * 8 + (size_t)kRescanCap * 8 +
