@@ -32,7 +32,7 @@ struct knn_group {
   std::vector<ncclComm_t> comms;
   std::vector<DevBuf> X, lab;                  // per-device train rows (full or shard)
   std::vector<DevBuf> Q, olab, oidx, odist, oflags;
-  std::vector<DevBuf> pd, pi, pl, gd, gi, gl;  // train-sharded partial / gathered lists
+  std::vector<DevBuf> pk, gk;                  // train-sharded packed partial / gathered lists
   std::vector<DevBuf> nX, nmm;                 // normalisation shards / per-dim bounds
   int64_t n = 0;
   int d = 0;
@@ -99,8 +99,8 @@ int knn_group_create(knn_group** out, int ndev, const int* devs, int mode) {
       return knn_fail(KNN_ERR_COMM, std::string("ncclCommInitAll failed: ") + ncclGetErrorString(r));
     }
   }
-  for (auto* v : {&g->X, &g->lab, &g->Q, &g->olab, &g->oidx, &g->odist, &g->oflags, &g->pd,
-                  &g->pi, &g->pl, &g->gd, &g->gi, &g->gl, &g->nX, &g->nmm})
+  for (auto* v : {&g->X, &g->lab, &g->Q, &g->olab, &g->oidx, &g->odist, &g->oflags, &g->pk,
+                  &g->gk, &g->nX, &g->nmm})
     v->resize(ndev);
   *out = g;
   return KNN_OK;
@@ -113,8 +113,8 @@ int knn_group_destroy(knn_group* g) {
       (void)hipSetDevice(g->devs[i]);
       (void)hipDeviceSynchronize();
     }
-    for (auto* v : {&g->X, &g->lab, &g->Q, &g->olab, &g->oidx, &g->odist, &g->oflags, &g->pd,
-                    &g->pi, &g->pl, &g->gd, &g->gi, &g->gl, &g->nX, &g->nmm})
+    for (auto* v : {&g->X, &g->lab, &g->Q, &g->olab, &g->oidx, &g->odist, &g->oflags, &g->pk,
+                    &g->gk, &g->nX, &g->nmm})
       if (i < (int)v->size()) (*v)[i].release();
   }
   for (auto c : g->comms)
@@ -260,15 +260,13 @@ int knn_group_classify(knn_group* g, const double* Q, int64_t m, int32_t k, int3
   const int w = (int)std::min<int64_t>((int64_t)k + 1, g->n);
   if ((int64_t)G * w > 4096)  // merge_vote_partials holds the G*w entries of a query in LDS
     return knn_fail(KNN_ERR_ARG, "train-sharded merge needs ngpus * (k+1) <= 4096");
+  const int64_t PB = knnk::packed_part_bytes(m, w);
   int rc = for_each_dev(g, [&](int i) {
     int e;
     if ((e = g->Q[i].ensure((size_t)m * d * sizeof(double)))) return e;
-    if ((e = g->pd[i].ensure((size_t)m * w * sizeof(double)))) return e;
-    if ((e = g->pi[i].ensure((size_t)m * w * sizeof(int64_t)))) return e;
-    if ((e = g->pl[i].ensure((size_t)m * w * sizeof(int32_t)))) return e;
-    if ((e = g->gd[i].ensure((size_t)G * m * w * sizeof(double)))) return e;
-    if ((e = g->gi[i].ensure((size_t)G * m * w * sizeof(int64_t)))) return e;
-    if ((e = g->gl[i].ensure((size_t)G * m * w * sizeof(int32_t)))) return e;
+    // this GPU's lists packed [dist | idx | label] (one all-gather per step)
+    if ((e = g->pk[i].ensure((size_t)PB))) return e;
+    if (G > 1 && (e = g->gk[i].ensure((size_t)G * PB))) return e;
     if ((e = g->olab[i].ensure((size_t)m * sizeof(int32_t)))) return e;
     if ((e = g->oflags[i].ensure((size_t)m * sizeof(int32_t)))) return e;
     if ((e = g->oidx[i].ensure((size_t)m * k * sizeof(int64_t)))) return e;
@@ -290,31 +288,27 @@ int knn_group_classify(knn_group* g, const double* Q, int64_t m, int32_t k, int3
     NCCL_G(ncclGroupEnd());
   }
   rc = for_each_dev(g, [&](int i) {
+    unsigned char* pb = (unsigned char*)g->pk[i].p;
     return knn_search_partial_device(g->ctx[i], (const double*)g->Q[i].p, m, w, metric,
-                                     (double*)g->pd[i].p, (int64_t*)g->pi[i].p,
-                                     (int32_t*)g->pl[i].p, nullptr);
+                                     (double*)pb, (int64_t*)(pb + 8 * m * w),
+                                     (int32_t*)(pb + 16 * m * w), nullptr);
   });
   if (rc) return rc;
-  if (G > 1) {
+  if (G > 1) {  // one all-gather of the packed lists (≙ the reference's MPI_Gather, cpp:340)
     NCCL_G(ncclGroupStart());
-    for (int i = 0; i < G; i++) {
-      hipStream_t s = g->ctx[i]->stream;
-      NCCL_G(ncclAllGather(g->pd[i].p, g->gd[i].p, (size_t)m * w, ncclFloat64, g->comms[i], s));
-      NCCL_G(ncclAllGather(g->pi[i].p, g->gi[i].p, (size_t)m * w, ncclInt64, g->comms[i], s));
-      NCCL_G(ncclAllGather(g->pl[i].p, g->gl[i].p, (size_t)m * w, ncclInt32, g->comms[i], s));
-    }
+    for (int i = 0; i < G; i++)
+      NCCL_G(ncclAllGather(g->pk[i].p, g->gk[i].p, (size_t)PB, ncclUint8, g->comms[i],
+                           g->ctx[i]->stream));
     NCCL_G(ncclGroupEnd());
   }
   rc = for_each_dev(g, [&](int i) {
     const int64_t q0 = m * i / G, q1 = m * (i + 1) / G, mi = q1 - q0;
     if (mi <= 0) return KNN_OK;
     hipStream_t s = g->ctx[i]->stream;
-    const double* sd = (const double*)(G > 1 ? g->gd[i].p : g->pd[i].p);
-    const int64_t* si = (const int64_t*)(G > 1 ? g->gi[i].p : g->pi[i].p);
-    const int32_t* sl = (const int32_t*)(G > 1 ? g->gl[i].p : g->pl[i].p);
-    knnk::launch_merge_vote_partials(sd, si, sl, G, m, w, k, (int32_t*)g->olab[i].p,
+    const double* sk = (const double*)(G > 1 ? g->gk[i].p : g->pk[i].p);
+    knnk::launch_merge_vote_partials(sk, nullptr, nullptr, G, m, w, k, (int32_t*)g->olab[i].p,
                                      (int64_t*)g->oidx[i].p, (double*)g->odist[i].p,
-                                     (int32_t*)g->oflags[i].p, s, q0, mi);
+                                     (int32_t*)g->oflags[i].p, s, q0, mi, PB);
     if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
       return knn_fail(KNN_ERR_DEVICE, "merge/vote failed");
     return KNN_OK;

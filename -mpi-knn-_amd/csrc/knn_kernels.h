@@ -161,7 +161,10 @@ void launch_rescan(int metric, const TrainDev& t, const double* Q64, const Resca
 void launch_merge_vote_partials(const double* dist, const int64_t* idx, const int32_t* lab,
                                 int parts, int64_t m, int w, int k, int32_t* out_lab,
                                 int64_t* out_idx, double* out_dist, int32_t* out_flags,
-                                hipStream_t s, int64_t q0 = 0, int64_t mq = -1);
+                                hipStream_t s, int64_t q0 = 0, int64_t mq = -1,
+                                int64_t pstride = 0);
+// byte stride of one part's packed [dist | idx | label] lists of m x w entries
+inline int64_t packed_part_bytes(int64_t m, int w) { return (m * w * 20 + 15) / 16 * 16; }
 void launch_fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t s);
 // fp64 rows -> [hi(DP) | lo(DP)] bf16 rows of scale*x (candidate metric 2 = L2 via bf16x3)
 // rows of `out` are row_shorts 16-bit words; xl2/xl1 (train only, else null)

@@ -896,7 +896,10 @@ void launch_rescan(int metric, const TrainDev& t, const double* Q64, const Resca
 __global__ void __launch_bounds__(64)
 merge_vote_partials_kernel(const double* __restrict__ dist, const int64_t* __restrict__ idx,
                            const int32_t* __restrict__ lab, int parts, int64_t m, int w, int k,
-                           int P2, int64_t q0, Sink sink) {
+                           int P2, int64_t q0, int64_t pstride, Sink sink) {
+  // pstride = 0: three arrays [parts][m][w]; pstride > 0: one packed buffer
+  // per part at byte offset p * pstride from dist, holding that part's
+  // [m][w] dists | [m][w] idx | [m][w] labels (knn_group's single all-gather)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* dk = (double*)smem;
   int64_t* gi = (int64_t*)(dk + P2);
@@ -905,13 +908,30 @@ merge_vote_partials_kernel(const double* __restrict__ dist, const int64_t* __res
   const int64_t qo = blockIdx.x;      // row in the outputs
   const int lane = threadIdx.x;
   const int ne = parts * w;
+  auto entry = [&](int e, double& v, int64_t& id, int32_t& lb) {
+    const int p = e / w, c = e - p * w;
+    if (pstride > 0) {
+      const unsigned char* pb = (const unsigned char*)dist + p * pstride;
+      const int64_t o = q * w + c, mw = m * w;
+      v = ((const double*)pb)[o];
+      id = ((const int64_t*)(pb + 8 * mw))[o];
+      lb = ((const int32_t*)(pb + 16 * mw))[o];
+    } else {
+      const int64_t src = ((int64_t)p * m + q) * w + c;
+      v = dist[src];
+      id = idx[src];
+      lb = lab[src];
+    }
+  };
   for (int e = lane; e < P2; e += 64) {
     double v = KNN_INF_D;
     int64_t id = LLONG_MAX;
     if (e < ne) {
-      const int p = e / w, c = e - p * w;
-      const int64_t src = ((int64_t)p * m + q) * w + c;
-      if (idx[src] >= 0) { v = dist[src]; id = idx[src]; }
+      double ev;
+      int64_t eid;
+      int32_t elb;
+      entry(e, ev, eid, elb);
+      if (eid >= 0) { v = ev; id = eid; }
     }
     dk[e] = v;
     gi[e] = id;
@@ -920,18 +940,18 @@ merge_vote_partials_kernel(const double* __restrict__ dist, const int64_t* __res
   bitonic_sort_lds(dk, gi, P2, lane, 64);
   // labels travel with the lists: place each one at its entry's sorted slot
   for (int e = lane; e < ne; e += 64) {
-    const int p = e / w, c = e - p * w;
-    const int64_t src = ((int64_t)p * m + q) * w + c;
-    if (idx[src] < 0) continue;
+    double v;
+    int64_t id;
+    int32_t lb;
+    entry(e, v, id, lb);
+    if (id < 0) continue;
     // position of (dist, idx) in the sorted array: binary search
-    const double v = dist[src];
-    const int64_t id = idx[src];
     int lo = 0, hi = P2;
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
       if (pair_less(dk[mid], gi[mid], v, id)) lo = mid + 1; else hi = mid;
     }
-    if (lo < k + 1) ls[lo] = lab[src];
+    if (lo < k + 1) ls[lo] = lb;
   }
   __syncthreads();
   int cnt = 0;
@@ -967,7 +987,7 @@ merge_vote_partials_kernel(const double* __restrict__ dist, const int64_t* __res
 void launch_merge_vote_partials(const double* dist, const int64_t* idx, const int32_t* lab,
                                 int parts, int64_t m, int w, int k, int32_t* out_lab,
                                 int64_t* out_idx, double* out_dist, int32_t* out_flags,
-                                hipStream_t s, int64_t q0, int64_t mq) {
+                                hipStream_t s, int64_t q0, int64_t mq, int64_t pstride) {
   if (mq < 0) mq = m - q0;
   if (mq <= 0) return;
   int P2 = 1;
@@ -981,7 +1001,7 @@ void launch_merge_vote_partials(const double* dist, const int64_t* idx, const in
   sink.flags = out_flags;
   const size_t lds = (size_t)P2 * (8 + 8 + 4);
   hipLaunchKernelGGL(merge_vote_partials_kernel, dim3((unsigned)mq), dim3(64), lds, s, dist, idx,
-                     lab, parts, m, w, k, P2, q0, sink);
+                     lab, parts, m, w, k, P2, q0, pstride, sink);
 }
 
 }  // namespace knnk

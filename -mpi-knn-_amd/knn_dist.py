@@ -89,6 +89,21 @@ def _all_gather_stack(t):
     return torch.stack(out, 0)
 
 
+def _all_gather_packed(d, i, l):
+    """The three partial-list tensors of this rank as one byte buffer
+    [dist | idx | label] and a single all-gather (one collective per step,
+    like knn_group_classify's ncclAllGather); unpacked into [W][m][w] each."""
+    parts = [t.contiguous().reshape(-1).view(torch.uint8) for t in (d, i, l)]
+    sizes = [p.numel() for p in parts]
+    packed = torch.cat(parts)
+    out = _all_gather_stack(packed)
+    res, o = [], 0
+    for t, nb in zip((d, i, l), sizes):
+        res.append(out[:, o:o + nb].contiguous().view(t.dtype).reshape((-1,) + tuple(t.shape)))
+        o += nb
+    return tuple(res)
+
+
 def normalize_sharded(local_sets, minmax, apply, d, device=None):
     """Transductive min-max normalisation with the reference's decomposition
     (cpp:229-306): minmax(set, mx, mn, init) folds this rank's rows of each
@@ -115,8 +130,8 @@ def train_sharded(search_partial, merge_vote, Q, m, w, k, device=None):
     lists.  Returns this rank's label slice and its [q0, q1)."""
     world, rank = world_info()
     d, i, l = search_partial(Q)
-    if world > 1:  # ncclAllGather of the partial lists -> [W][m][w]
-        gd, gi, gl = (_all_gather_stack(t.contiguous()) for t in (d, i, l))
+    if world > 1:  # one all-gather of the packed partial lists -> [W][m][w] each
+        gd, gi, gl = _all_gather_packed(d, i, l)
     else:
         gd, gi, gl = d[None], i[None], l[None]
     q0, q1 = shard_range(m, world, rank)
