@@ -665,6 +665,25 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   return KNN_OK;
 }
 
+// k > kMaxK: the exact large-k path (knn_select.hip, large_k_kernel); the
+// scratch (every row's distance per workgroup) is capped at ~8 GB.
+static int run_large_k(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
+                       const Sink& sink, hipStream_t s) {
+  const TrainDev& t = ctx->train;
+  const int64_t per = large_k_scratch_bytes(t.n, W, ctx->class_cnt);
+  const int64_t nwg = std::max<int64_t>(
+      1, std::min<int64_t>({m, 2 * (int64_t)ctx->cu_count, (8ll << 30) / per}));
+  int rc;
+  if ((rc = ctx->lk.ensure((size_t)(per * nwg)))) return rc;
+  snprintf(ctx->last_kernel, sizeof ctx->last_kernel, "large_k_kernel<%d>", metric);
+  ctx->last_kmetric = -1;
+  launch_large_k(metric, t, dQ, m, W, ctx->class_cnt, (unsigned char*)ctx->lk.p, per, (int)nwg,
+                 sink, s);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(ctx->done_ev, s));
+  return KNN_OK;
+}
+
 static int check_query_args(knn_ctx* ctx, int64_t m, int32_t k, int32_t metric) {
   if (!ctx->trained) return knn_fail(KNN_ERR_STATE, "classify before set_train");
   if (m < 0) return knn_fail(KNN_ERR_ARG, "m must be >= 0");
@@ -672,7 +691,6 @@ static int check_query_args(knn_ctx* ctx, int64_t m, int32_t k, int32_t metric) 
   if (k < 0) return knn_fail(KNN_ERR_ARG, "k must be >= 0");
   if (k > ctx->train.n)
     return knn_fail(KNN_ERR_ARG, "k exceeds n_train (the reference reads past its array, cpp:328)");
-  if (k > kMaxK) return knn_fail(KNN_ERR_ARG, "k above the supported maximum (1000)");
   if (metric != KNN_METRIC_L2 && metric != KNN_METRIC_L1)
     return knn_fail(KNN_ERR_ARG, "metric must be 0 (L2) or 1 (L1)");
   return KNN_OK;
@@ -705,6 +723,7 @@ int knn_classify_device(knn_ctx* ctx, const double* dQ, int64_t m, int32_t k, in
   sink.dist = d_dist;
   sink.flags = d_flags;
   const int W = (int)std::min<int64_t>((int64_t)k + 1, ctx->train.n);
+  if (k > kMaxK) return run_large_k(ctx, dQ, m, W, metric, sink, s);
   return knn_run_search(ctx, dQ, m, W, metric, sink, s);
 }
 
@@ -750,7 +769,7 @@ int knn_search_partial_device(knn_ctx* ctx, const double* dQ, int64_t m, int32_t
   int rc;
   if ((rc = device_guard(ctx))) return rc;
   if (!ctx->trained) return knn_fail(KNN_ERR_STATE, "search before set_train");
-  if (w <= 0 || w > kMaxK + 1) return knn_fail(KNN_ERR_ARG, "w must be in [1, 1001]");
+  if (w <= 0) return knn_fail(KNN_ERR_ARG, "w must be >= 1");
   if (metric != KNN_METRIC_L2 && metric != KNN_METRIC_L1)
     return knn_fail(KNN_ERR_ARG, "metric must be 0 (L2) or 1 (L1)");
   if (m < 0 || m >= (int64_t)INT32_MAX) return knn_fail(KNN_ERR_ARG, "bad m");
@@ -766,6 +785,7 @@ int knn_search_partial_device(knn_ctx* ctx, const double* dQ, int64_t m, int32_t
   sink.plab = d_lab;
   // a shard smaller than w yields min(w, n) entries; the tail is padded
   const int W = (int)std::min<int64_t>(w, ctx->train.n);
+  if (w > kMaxK + 1) return run_large_k(ctx, dQ, m, W, metric, sink, s);
   return knn_run_search(ctx, dQ, m, W, metric, sink, s);
 }
 

@@ -63,7 +63,7 @@ struct knn_ctx {
   DevBuf X64_own, lab_own, X32, xl2, xl1, stats, XB, XS, XH, XT16, XS16, mu, mu_part;
   // per-classify workspace
   DevBuf Q64, Q32, qvalid, cand_v, cand_i, gthr, rescan_q, rescan_tau, rescan_cnt, fr_cnt, fr_buf,
-      fr_q, fr_thr, slow_q, totals;
+      fr_q, fr_thr, slow_q, totals, lk;
   // host-API outputs
   DevBuf o_lab, o_idx, o_dist, o_flags;
   // normalisation: per-thread partial max/min, bounds, host-API staging
@@ -72,7 +72,7 @@ struct knn_ctx {
     return {&X64_own, &lab_own, &X32,   &xl2,   &xl1,    &stats,  &XB,       &XS,
             &XH,      &XT16,    &XS16,  &mu,      &mu_part, &Q64, &Q32,    &qvalid, &cand_v,   &cand_i,
             &gthr,    &rescan_q, &rescan_tau, &rescan_cnt, &fr_cnt, &fr_buf, &fr_q, &fr_thr,
-            &slow_q,  &totals,  &o_lab, &o_idx, &o_dist, &o_flags, &nrm_part, &nrm_mm, &nrm_X};
+            &slow_q,  &totals,  &lk, &o_lab, &o_idx, &o_dist, &o_flags, &nrm_part, &nrm_mm, &nrm_X};
   }
 };
 

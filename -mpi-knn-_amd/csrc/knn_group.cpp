@@ -193,7 +193,7 @@ int knn_group_classify(knn_group* g, const double* Q, int64_t m, int32_t k, int3
                        int32_t* out_flags) {
   if (!g || !g->trained) return knn_fail(KNN_ERR_STATE, "group classify before set_train");
   if (m < 0 || !out_labels || (m > 0 && !Q)) return knn_fail(KNN_ERR_ARG, "bad classify arguments");
-  if (k < 0 || k > g->n || k > knnk::kMaxK) return knn_fail(KNN_ERR_ARG, "bad k");
+  if (k < 0 || k > g->n) return knn_fail(KNN_ERR_ARG, "bad k");
   if (m == 0) return KNN_OK;
   const int G = g->ndev;
   const int d = g->d;

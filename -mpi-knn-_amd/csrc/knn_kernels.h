@@ -165,6 +165,12 @@ void launch_merge_vote_partials(const double* dist, const int64_t* idx, const in
                                 int64_t pstride = 0);
 // byte stride of one part's packed [dist | idx | label] lists of m x w entries
 inline int64_t packed_part_bytes(int64_t m, int w) { return (m * w * 20 + 15) / 16 * 16; }
+// k beyond kMaxK (knn_select.hip, large_k_kernel): the exact path over every
+// row, nwg workgroups with per_wg bytes of scratch each (large_k_scratch_bytes)
+int64_t large_k_scratch_bytes(int64_t n, int W, int class_cnt);
+void launch_large_k(int metric, const TrainDev& t, const double* Q64, int64_t m, int W,
+                    int class_cnt, unsigned char* scratch, int64_t per_wg, int nwg,
+                    const Sink& sink, hipStream_t s);
 void launch_fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t s);
 // fp64 rows -> [hi(DP) | lo(DP)] bf16 rows of scale*x (candidate metric 2 = L2 via bf16x3)
 // rows of `out` are row_shorts 16-bit words; xl2/xl1 (train only, else null)

@@ -890,6 +890,215 @@ void launch_rescan(int metric, const TrainDev& t, const double* Q64, const Resca
                        rb.cnt, cap, rb.slow_q, W, sink, rb.counts, rb.totals);
 }
 
+// ------------------------------------------------ large k (k > kMaxK)
+// The candidate lists hold at most kMaxUnion entries, so a k beyond kMaxK
+// (the reference accepts any K <= N_train, cpp:328) runs this exact path
+// instead: one 1024-thread workgroup per query (a loop over the queries),
+// with its own global scratch.
+//  1. every row's exact fp64 distance in the reference's operation order
+//     (per-wave staged 64-B row pieces as in rescan_full) -> D[n];
+//  2. the key (bit pattern; distances are >= 0) of the W-th smallest by a
+//     radix select, 11 bits per pass, LDS histograms;
+//  3. rows below the pivot plus the lowest-index rows equal to it (an
+//     index-ordered scan) -> W entries, sorted by (dist, idx) (bitonic in the
+//     scratch);
+//  4. the reference vote, sequentially as in cpp:324-337 (per-class counts
+//     in the scratch), flags, outputs.
+constexpr int kLkThreads = 1024;
+constexpr int kLkBits = 11;
+__device__ __forceinline__ uint64_t lk_key(double v) { return (uint64_t)__double_as_longlong(v); }
+
+template <int METRIC>
+__global__ void __launch_bounds__(kLkThreads)
+large_k_kernel(TrainDev t, const double* __restrict__ Q64, int64_t m, int W, int class_cnt,
+               unsigned char* __restrict__ scratch, int64_t scratch_per_wg, Sink sink) {
+  __shared__ double tiles[kLkThreads / 64][64 * (kFullDC + 1)];
+  __shared__ unsigned hist[1 << kLkBits];
+  __shared__ uint64_t s_prefix;
+  __shared__ int s_rank, s_nlt, s_neq, s_bad;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int d = t.d;
+  const int64_t n = t.n;
+  int W2 = 1;
+  while (W2 < W) W2 <<= 1;
+  unsigned char* base = scratch + (int64_t)blockIdx.x * scratch_per_wg;
+  double* D = (double*)base;                       // [n]
+  double* od = D + n;                              // [W2]
+  int* oi = (int*)(od + W2);                       // [W2]
+  int* ol = oi + W2;                               // [W2] labels in sorted order
+  int* cnt = ol + W2;                              // [class_cnt] vote counts
+  double* tb = tiles[wv];
+  for (int64_t q = blockIdx.x; q < m; q += gridDim.x) {
+    const double* qrow = Q64 + q * d;
+    __syncthreads();
+    if (tid == 0) s_bad = 0;
+    __syncthreads();
+    for (int c = tid; c < d; c += kLkThreads)
+      if (!__builtin_isfinite(qrow[c])) s_bad = 1;
+    __syncthreads();
+    if (s_bad) {  // a NaN / inf coordinate: no neighbours (as the merge reports it)
+      if (tid < 64) finish_nonfinite(q, sink);
+      continue;
+    }
+    // 1. exact distances
+    for (int64_t s0 = 0; s0 < n; s0 += kLkThreads) {
+      const int64_t r0 = s0 + wv * 64;
+      const int nr = (int)max((int64_t)0, min((int64_t)64, n - r0));
+      double r = 0.0;
+      for (int c0 = 0; c0 < d && nr > 0; c0 += kFullDC) {
+        const int nd = min(kFullDC, d - c0);
+#pragma unroll
+        for (int i = 0; i < kFullDC; ++i) {
+          const int e = lane + 64 * i, rr = e / kFullDC, j = e % kFullDC;
+          double val = 0.0;
+          if (rr < nr && j < nd) {
+            const double tq = qrow[c0 + j] - t.X64[(r0 + rr) * d + c0 + j];
+            val = METRIC == 0 ? tq * tq : __builtin_fabs(tq);
+          }
+          tb[rr * (kFullDC + 1) + j] = val;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (lane < nr) {
+          const double* row = tb + lane * (kFullDC + 1);
+          for (int j = 0; j < nd; ++j) r = r + row[j];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
+      if (lane < nr) D[r0 + lane] = METRIC == 0 ? __builtin_sqrt(r) : r;
+    }
+    // 2. radix select of the W-th smallest key (digits from the top)
+    if (tid == 0) {
+      s_prefix = 0;
+      s_rank = W;  // rank still to find among keys matching the prefix
+    }
+    for (int shift = 64 - kLkBits; shift > -kLkBits; shift -= kLkBits) {
+      const int sh = max(shift, 0);
+      const int nbits = shift >= 0 ? kLkBits : kLkBits + shift;  // last digit: the low bits
+      const uint64_t hi_mask = (sh + nbits >= 64) ? 0 : (~0ull << (sh + nbits));
+      __syncthreads();  // the previous pass's digit choice has read hist
+      for (int b = tid; b < (1 << kLkBits); b += kLkThreads) hist[b] = 0;
+      __syncthreads();  // (also publishes D and the previous pass's prefix)
+      const uint64_t pre = s_prefix;
+      for (int64_t r = tid; r < n; r += kLkThreads) {
+        const uint64_t k = lk_key(D[r]);
+        if ((k & hi_mask) == pre) atomicAdd(&hist[(k >> sh) & ((1u << nbits) - 1)], 1u);
+      }
+      __syncthreads();
+      if (tid == 0) {
+        int rank = s_rank;
+        unsigned b = 0;
+        for (; b < (1u << nbits); ++b) {
+          if ((int)hist[b] >= rank) break;
+          rank -= hist[b];
+        }
+        s_prefix = pre | ((uint64_t)b << sh);
+        s_rank = rank;
+      }
+    }
+    __syncthreads();
+    const uint64_t pivot = s_prefix;  // key of the W-th smallest distance
+    // 3. the W smallest by (dist, idx): all keys below the pivot (unordered),
+    //    then the lowest-index rows equal to it (ordered scan)
+    if (tid == 0) { s_nlt = 0; s_neq = 0; }
+    __syncthreads();
+    for (int64_t r = tid; r < n; r += kLkThreads)
+      if (lk_key(D[r]) < pivot) {
+        const int p = atomicAdd(&s_nlt, 1);
+        od[p] = D[r];
+        oi[p] = (int)r;
+      }
+    __syncthreads();
+    const int nlt = s_nlt;  // < W
+    for (int64_t s0 = 0; s0 < n; s0 += kLkThreads) {
+      const int64_t r = s0 + tid;
+      const bool eq = r < n && lk_key(D[r]) == pivot;
+      // index-ordered positions: wave prefix, then the waves in order
+      const unsigned long long mk = __ballot(eq);
+      const int before_w = __popcll(mk & ((1ull << lane) - 1));
+      if (lane == 0) hist[wv] = __popcll(mk);
+      __syncthreads();
+      int off = s_neq;
+      for (int x = 0; x < wv; ++x) off += hist[x];
+      const int p = nlt + off + before_w;
+      if (eq && p < W) {
+        od[p] = D[r];
+        oi[p] = (int)r;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        int tot = 0;
+        for (int x = 0; x < kLkThreads / 64; ++x) tot += hist[x];
+        s_neq += tot;
+      }
+      __syncthreads();
+      if (nlt + s_neq >= W) break;
+    }
+    for (int c = W + tid; c < W2; c += kLkThreads) {
+      od[c] = KNN_INF_D;
+      oi[c] = INT_MAX;
+    }
+    bitonic_sort_lds(od, oi, W2, tid, kLkThreads);  // (global scratch; same code path)
+    // 4. labels, vote, outputs
+    const int need = sink.mode == MODE_SINGLE ? sink.k : sink.w;
+    for (int c = tid; c < need && c < W; c += kLkThreads) ol[c] = t.lab[oi[c]];
+    for (int c = tid; c < class_cnt; c += kLkThreads) cnt[c] = 0;
+    __syncthreads();
+    if (sink.mode == MODE_SINGLE) {
+      const int k = sink.k;
+      if (tid == 0) {  // cpp:324-337, sequentially: the first label to strictly exceed
+        int best = 0, lab = -1;
+        for (int i = 0; i < k; ++i) {
+          const int c = ++cnt[ol[i]];
+          if (c > best) { best = c; lab = ol[i]; }
+        }
+        sink.labels[q] = lab;
+      }
+      int tie = 0;
+      for (int i = tid; i + 1 < k; i += kLkThreads)
+        if (od[i] == od[i + 1]) tie |= ol[i] != ol[i + 1] ? 4 : 8;
+      if (tie) atomicOr(&s_bad, tie);  // s_bad is 0 here: reused for the flags
+      __syncthreads();
+      if (tid == 0 && sink.flags) {
+        int f = s_bad;
+        if (k < W && od[k - 1] == od[k]) f |= 2;  // KNN_FLAG_TIE_BOUNDARY
+        sink.flags[q] = f;
+      }
+      for (int i = tid; i < k; i += kLkThreads) {
+        if (sink.idx) sink.idx[q * k + i] = (int64_t)oi[i] + sink.idx_off;
+        if (sink.dist) sink.dist[q * k + i] = od[i];
+      }
+    } else {
+      for (int i = tid; i < sink.w; i += kLkThreads) {
+        const bool ok = i < W;
+        sink.dist[q * sink.w + i] = ok ? od[i] : KNN_INF_D;
+        sink.idx[q * sink.w + i] = ok ? (int64_t)oi[i] + sink.idx_off : -1;
+        sink.plab[q * sink.w + i] = ok ? ol[i] : -1;
+      }
+    }
+  }
+}
+
+int64_t large_k_scratch_bytes(int64_t n, int W, int class_cnt) {
+  int64_t W2 = 1;
+  while (W2 < W) W2 <<= 1;
+  return ((n * 8 + W2 * 16 + (int64_t)class_cnt * 4) + 255) / 256 * 256;
+}
+
+void launch_large_k(int metric, const TrainDev& t, const double* Q64, int64_t m, int W,
+                    int class_cnt, unsigned char* scratch, int64_t per_wg, int nwg,
+                    const Sink& sink, hipStream_t s) {
+  if (m <= 0) return;
+  const dim3 g((unsigned)std::min<int64_t>(m, nwg));
+  if (metric == 0)
+    hipLaunchKernelGGL(large_k_kernel<0>, g, dim3(kLkThreads), 0, s, t, Q64, m, W, class_cnt,
+                       scratch, per_wg, sink);
+  else
+    hipLaunchKernelGGL(large_k_kernel<1>, g, dim3(kLkThreads), 0, s, t, Q64, m, W, class_cnt,
+                       scratch, per_wg, sink);
+}
+
 // ------------------------------------------ train-sharded k-way merge + vote
 // lists [parts][m][w] sorted by (dist, global idx); one wave per query merges
 // them (bitonic in LDS) and runs the reference vote on the first k.

@@ -202,6 +202,36 @@ def test_k_zero_and_errors(clf, knn):
         clf.set_train(tr, np.full(500, 2, np.int32), 2)  # label out of range
 
 
+@pytest.mark.parametrize("n,m,d,k,metric,grid", [
+    (3000, 40, 20, 1500, 0, 1024.0),   # k > 1000: the exact large-k path (L2)
+    (2600, 33, 7, 1200, 1, 1024.0),    # L1
+    (1500, 20, 4, 1499, 0, 16.0),      # k = n - 1 on a coarse grid: long exact-tie runs
+])
+def test_large_k(n, m, d, k, metric, grid, clf, knn):
+    """k beyond the candidate lists' capacity (the reference accepts any
+    K <= N_train, cpp:328): the exact large-k path -- labels, neighbour
+    distances and indices against the oracle, and a partial (w > 1001) list."""
+    rng = np.random.default_rng(n + k)
+    tr, lab, te = _mix(rng, n, m, d, 5, grid=grid)
+    run_case(clf, knn, tr, lab, te, k, metric, 5)
+    import torch
+    dev = torch.device("cuda", 0)
+    X = torch.from_numpy(tr).to(dev)
+    L = torch.from_numpy(lab).to(dev)
+    Q = torch.from_numpy(te).to(dev)
+    clf.set_train_device(X.data_ptr(), L.data_ptr(), n, d, 5, keep=(X, L))
+    w = k + 1
+    pd = torch.empty((m, w), dtype=torch.float64, device=dev)
+    pi = torch.empty((m, w), dtype=torch.int64, device=dev)
+    pl = torch.empty((m, w), dtype=torch.int32, device=dev)
+    clf.search_partial_device(Q.data_ptr(), m, w, metric, pd.data_ptr(), pi.data_ptr(),
+                              pl.data_ptr())
+    clf.sync()
+    _, widx, wdist = oracle.knn(tr, lab, te, k, metric == 0, 5, n_out=w)
+    assert_neighbors_match(pi.cpu().numpy(), pd.cpu().numpy(), widx, wdist)
+    np.testing.assert_array_equal(pl.cpu().numpy(), lab[pi.cpu().numpy()])
+
+
 def test_device_api_and_partial_merge(clf, knn):
     """knn_classify_device + search_partial/merge_vote (train-sharded building
     blocks) on one GPU: shard the train set in two contexts, merge, compare."""
