@@ -382,9 +382,15 @@ static void choose_geometry(knn_ctx* ctx, int metric, bool streamed, int DP, int
     int S_lo = std::max(1, (C + lps * R - 1) / (lps * R));
     // quad lists: S >= 2W where every split still walks >= 32 tiles (a list
     // then expects at most 1/8 of the query's top W; an overflow, 5 of them in
-    // one list, has probability ~C(W,5)/(8S)^5 -- 0.7 % of cfg3's queries
-    // failed at S = W, each an exact rescan), at least S >= W
-    if (quad) S_lo = std::max(S_lo, std::max<int>(W, (int)std::min<int64_t>(2 * W, n_tiles / 32)));
+    // one list, fails the query's certification: 0.35 % of cfg3's 1M queries
+    // at S = W, 0.05 % at 2W, 0.007 % at 4W, each an exact rescan); 4W for
+    // batches of >= 128K queries, whose many workgroup rounds make the longer
+    // walks of fewer splits worth nothing (cfg3: candidate +0.8 %, rescan
+    // phase 11.9 -> 1.8 ms); at least S >= W
+    if (quad) {
+      const int mult = n_qt >= 512 ? 4 : 2;
+      S_lo = std::max(S_lo, std::max<int>(W, (int)std::min<int64_t>(mult * W, n_tiles / 32)));
+    }
     // R = 8 needs an expected share of the top W per list (2S lists) of at
     // most 0.8 (S >= W / 1.6): a list overflow (9 of them in one list -> the
     // query fails certification) then has probability < 1e-6 per list; at a
