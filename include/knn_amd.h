@@ -104,7 +104,8 @@ int knn_set_train_device(knn_ctx* ctx, const double* dX, const int32_t* dlabels,
 /* Classify m queries Q (row-major m x d fp64, same d as the train set).
  * out_labels[m] (Test_label_buffer, cpp:380) required; out_idx[m*k]
  * (global train indices) and out_dist[m*k] (fp64 reference distances) and
- * out_flags[m] nullable.  Host pointers. */
+ * out_flags[m] nullable.  Host pointers.  0 <= k <= n_train (k > 1000 runs
+ * the exact large-k path). */
 int knn_classify(knn_ctx* ctx, const double* Q, int64_t m, int32_t k, int32_t metric,
                  int32_t* out_labels, int64_t* out_idx, double* out_dist,
                  int32_t* out_flags);
