@@ -448,10 +448,11 @@ def main():
                 Q3 = None
             if Q3 is not None:
                 lab3 = torch.empty(q1 - q0, dtype=torch.int32, device=dev)
+                flg3 = torch.empty(q1 - q0, dtype=torch.int32, device=dev)
 
                 def step3():
                     clf.classify_device(Q3.data_ptr(), q1 - q0, k, knn.L2, lab3.data_ptr(), None,
-                                        None, None, stream)
+                                        None, flg3.data_ptr(), stream)
 
                 s3 = max(2, args.steps // 4)
                 r3 = timed_run(kd, clf, step3, s3, 1, sync, dev, knn.PRECISION_AUTO)
@@ -462,8 +463,13 @@ def main():
                     "steps": s3, "ms_per_step": r3["el"] / s3 * 1e3, "scaling": "strong",
                     "kernel_ms": r3["t_cand"] * 1e3, "rescanned_queries": r3["resc"],
                     "candidate_path": r3["path"]}
+                tv3 = torch.tensor([int(((flg3 & knn.FLAG_TIE_VOTE) != 0).sum().item())],
+                                   dtype=torch.int64, device=dev)
+                if world > 1:
+                    dist.all_reduce(tv3)
+                extra["cfg3_strong"]["tie_vote_queries"] = int(tv3.item())
                 log("cfg3 strong leg: %.1f ms/step" % (r3["el"] / s3 * 1e3))
-                del Q3, lab3
+                del Q3, lab3, flg3
 
         if not args.no_continuous and args.data == "grid" and world == 1:
             # the same workload on continuous (min-max normalised, off-grid) data
