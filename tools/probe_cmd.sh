@@ -1,7 +1,7 @@
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-for v in base spread base spread; do
-  if [ $v = base ]; then unset KNN_AMD_VARIANT; else export KNN_AMD_VARIANT=$v; fi
-  echo "variant $v"
-  timeout -k 10 200 python tools/tune.py --rounds 3 --d 960 --k 100 fp16:0:0 2>&1 | grep -v amdgpu.ids | grep cand || exit 1
-done
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/r2_tests_n.log 2>&1
+rc=$?; echo "tests rc=$rc"; tail -4 gpurun_out/r2_tests_n.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+timeout -k 10 300 python3 tools/tune.py --rounds 3 --d 960 --k 100 "fp16:0:0" "fp16:0:0:4" > gpurun_out/r2_tune_cfg5n.log 2>&1 || exit 1
+grep -v amdgpu.ids gpurun_out/r2_tune_cfg5n.log
