@@ -364,17 +364,21 @@ int knn_set_train_device(knn_ctx* ctx, const double* dX, const int32_t* dlabels,
 // workgroup duration.  The union of the 2S lists must hold the C re-rank
 // candidates; R grows to 16 when the expected per-list share of C is large.
 static void choose_geometry(knn_ctx* ctx, int metric, bool streamed, int DP, int nw, int n_qt,
-                            int64_t n_tiles, int W, int C, int& S_out, int& R_out) {
-  const int S_hi = (int)std::max<int64_t>(1, std::min<int64_t>(64, n_tiles));
+                            int64_t n_tiles, int W, int C, bool s3q, int& S_out, int& R_out) {
+  int S_hi = (int)std::max<int64_t>(1, std::min<int64_t>(64, n_tiles));
   int bestS = 1, bestR = 8;
   const bool quad = !streamed && (metric == 3 || metric == 4);  // 16x16 layouts
-  const int lps = quad ? 4 : 2;  // lists per query per split
+  const int lps = quad || s3q ? 4 : 2;  // lists per query per split
+  // S3 on 16x16x32 (s3q): R = 8 quad lists, 4 * S * 8 <= kMaxUnion entries
+  if (s3q) S_hi = std::min(S_hi, kMaxUnion / (4 * 8));
   for (int R : {4, 8, 16}) {
+    if (s3q && R != 8) continue;
     // kernel metrics 3, 4 (16x16x32 layout) have R = 4 only; elsewhere R = 4
     // only on request (resident kernel; tuning experiments)
     if (quad ? R != 4 : (ctx->tune_R ? R != ctx->tune_R : R == 4)) continue;
     if (R == 4 && (DP > 256 || metric == 1)) continue;
-    const int64_t slots = (int64_t)cand_blocks_per_cu(metric, DP, R, nw) * ctx->cu_count;
+    const int64_t slots =
+        (int64_t)(s3q ? s3q_blocks_per_cu() : cand_blocks_per_cu(metric, DP, R, nw)) * ctx->cu_count;
     // the union of the lists must hold the C re-rank candidates; with R = 4
     // lists (16x16 layouts) also S >= W, i.e. at most W/4S of the query's
     // top W expected per list: a list holding 5 of them (an overflow ->
@@ -397,7 +401,7 @@ static void choose_geometry(knn_ctx* ctx, int metric, bool streamed, int DP, int
     // share of 1.6 (cfg5, W = 101, S = 32) 1.6 % of the queries failed.
     // Where no such S exists R = 16 runs instead.
     if (R == 8 && !ctx->tune_R) {
-      const int s8 = (W * 5 + 7) / 8;
+      const int s8 = s3q ? (W * 5 + 15) / 16 : (W * 5 + 7) / 8;  // share W / (lps S) <= 0.8
       if (s8 > S_hi) continue;
       S_lo = std::max(S_lo, s8);
     }
@@ -545,9 +549,14 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   int C = (int)std::min<int64_t>(t.n, std::max(2 * W, W + 16));
   C = std::min(C, kMaxUnion);
   int S = 1, R = 8;
-  choose_geometry(ctx, kmetric, s3, DP, nw, n_qt, n_tiles, W, C, S, R);
-  const bool quad_lists = !s3 && (kmetric == 3 || kmetric == 4);  // 16x16: 4 lists per split
-  if (quad_lists) R = 4;
+  // fp16 S3 on v_mfma_f32_16x16x32_f16 (quad lists of R = 8) where its lists
+  // can hold the query's top W (share W / 4S <= 0.8 at S <= 32, i.e. W <= 102);
+  // tuning key "s3q": -1 auto, 0 off (32x32x16), 1 on where feasible
+  const bool s3q = s3h && ctx->tune_s3q != 0 && (W * 5 + 15) / 16 <= kMaxUnion / 32;
+  choose_geometry(ctx, kmetric, s3, DP, nw, n_qt, n_tiles, W, C, s3q, S, R);
+  // 16x16 layouts: 4 lists per query per split
+  const bool quad_lists = (!s3 && (kmetric == 3 || kmetric == 4)) || s3q;
+  if (quad_lists && !s3q) R = 4;
   const int NL = (quad_lists ? 4 : 2) * S;
   C = std::min(C, NL * R);
   // rescan workspace: the fast path serves the first `cap` failed queries
@@ -559,7 +568,18 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   // per-query global thresholds of the resident candidate kernel
   // (tuning switch "ablate" bit 2 turns the exchange off; results stay exact)
   const bool use_gthr = DP <= 256 && !(ctx->tune_ablate & 4);
-  if (use_gthr && (rc = ctx->gthr.ensure((size_t)m_pad * 4 * sizeof(uint32_t)))) return rc;
+  if (use_gthr && (rc = ctx->gthr.ensure((size_t)m_pad * kGthrSlots * sizeof(uint32_t))))
+    return rc;
+  // what the lists publish into gthr (cand_kernel): the K-th smallest of the
+  // union of a query's lists in a workgroup, 8 groups, with 8K >= W + 5 rows
+  // guaranteed below the threshold (K <= 4, so W <= 27); else the lists'
+  // R-th entries in 4 groups.  cfg2 (W = 11): K = 2, the candidate pass 3 %
+  // faster than K = 3 and 2-4 % faster than the list thresholds (in-process
+  // A/B, gpurun_out/r2f_ab_gk.log, r2g_ab_pair.log); K = 1 (8 rows < W)
+  // sends 5 % of the queries to the rescan.
+  int gk = (W + 5 + kGthrSlots - 1) / kGthrSlots;
+  if (gk > 4) gk = 0;
+  if (ctx->tune_gk >= 0) gk = ctx->tune_gk;
   if ((rc = ctx->rescan_q.ensure((size_t)m * sizeof(int) + 16))) return rc;
   if ((rc = ctx->rescan_tau.ensure((size_t)m * sizeof(double) + 16))) return rc;
   if ((rc = ctx->rescan_cnt.ensure(4 * sizeof(int)))) return rc;
@@ -576,8 +596,8 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   ctx->last_nw = nw;
   ctx->geom[3] = C;
   if (s3)
-    snprintf(ctx->last_kernel, sizeof ctx->last_kernel, "cand_s3_kernel<%d,%s>", R,
-             s3h ? "true" : "false");
+    snprintf(ctx->last_kernel, sizeof ctx->last_kernel, "cand_s3_kernel<%d,%s,%s>", R,
+             s3h ? "true" : "false", s3q ? "true" : "false");
   else if (DP <= 256)
     snprintf(ctx->last_kernel, sizeof ctx->last_kernel, "cand_kernel<%d,%d,%d,%d>", DP, R, kmetric,
              nw);
@@ -623,11 +643,13 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   cl.ablate = ctx->tune_ablate;
   cl.nw = nw;
   cl.gthr = use_gthr ? (uint32_t*)ctx->gthr.p : nullptr;
-  if (use_gthr) launch_fill_i32((int32_t*)ctx->gthr.p, m_pad * 4, (int32_t)kGthrInit, s);
+  cl.gk = gk;
+  // slots of groups without a split stay 0 (never the max)
+  if (use_gthr) launch_fill_gthr(cl.gthr, m_pad, std::min(S, gk ? 8 : 4), s);
   if (s3h)
     launch_cand_s3h((const unsigned short*)ctx->XT16.p, (const float*)ctx->XS16.p,
                     (const unsigned short*)ctx->Q32.p, DP, n_pad3, R, S, n_qt, cl.out_v, cl.out_i,
-                    cl.ablate, s);
+                    cl.ablate, s3q, s);
   else if (s3)
     launch_cand_s3((const unsigned short*)ctx->XB.p, (const float*)ctx->XS.p,
                    (const unsigned short*)ctx->Q32.p, DP, n_pad3, R, S, n_qt, cl.out_v, cl.out_i,
@@ -946,6 +968,12 @@ int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value) {
   } else if (!strcmp(key, "S")) {
     if (value < 0 || value > 64) return knn_fail(KNN_ERR_ARG, "S must be 0 (auto) .. 64");
     ctx->tune_S = (int)value;
+  } else if (!strcmp(key, "s3q")) {
+    if (value < -1 || value > 1) return knn_fail(KNN_ERR_ARG, "s3q must be -1, 0 or 1");
+    ctx->tune_s3q = (int)value;
+  } else if (!strcmp(key, "gk")) {
+    if (value < -1 || value > 4) return knn_fail(KNN_ERR_ARG, "gk must be -1 (auto) .. 4");
+    ctx->tune_gk = (int)value;
   } else {
     return knn_fail(KNN_ERR_ARG, std::string("unknown tuning key ") + key);
   }

@@ -47,6 +47,8 @@ struct knn_ctx {
   int tune_R = 0, tune_S = 0;  // 0 = automatic
   int tune_ablate = 0;         // timing-only kernel ablations
   int tune_nw = 0;             // resident kernel waves per workgroup (0 = auto)
+  int tune_s3q = -1;           // fp16 S3 on the 16x16x32 layout: -1 auto, 0 off, 1 on
+  int tune_gk = -1;            // resident kernel gthr publish rank (-1 auto, 0 list R-th, 1..4)
   int tune_fp16 = -1;          // fp16 candidate pass: -1 auto, 0 off, 1 on
   int tune_m16 = -1;           // bf16x3 on the 16x16x32 MFMA layout: -1 auto, 0 off, 1 on
   int last_nw = 0;

@@ -99,7 +99,7 @@ __global__ void __launch_bounds__(NW * 64)
 __attribute__((amdgpu_waves_per_eu((METRIC == 4 ? DP / 2 : DP) <= 160 && R <= 8 ? 4 : 1)))
 cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
             int n_qt, float* __restrict__ out_v, int* __restrict__ out_i, int abl,
-            uint32_t* gthr) {
+            uint32_t* gthr, int gk) {
 #if KNN_SETPRIO
   // the second-dispatched half of the workgroup at priority 1 (MI355X_MICROARCH
   // "Two waves per SIMD", item 4)
@@ -201,17 +201,23 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   }
 
   // Global per-query threshold.  The query's lists are spread over S
-  // workgroups; they form 4 groups by split % 4, and slot g of gthr[query]
-  // holds the min over group g's published list thresholds (order-preserving
-  // keys, atomicMin).  Each slot is a list's R-th entry, so group g has a list
-  // with R rows at or below it, and tq = max over the 4 slots has >= 4R
-  // distinct rows at or below it: any row above tq is outside the query's 4R
-  // best and may be dropped.  The merge bounds dropped rows by the final tq.
-  // Lists then stop filling with rows only a cold list would keep -- the
-  // insertions (64 independent lists per wave) that dominate the epilogue.
-  // The 4 slots come back by LDS-DMA into this wave's 1-KiB area of gls
-  // (16 B per lane) and are read after the next barrier: a plain load into
-  // VGPRs would be consumed (or copied) by compiler code before it lands.
+  // workgroups; they form G groups by split % G (disjoint row sets), and slot
+  // g of gthr[query] (kGthrSlots keys) holds the min over group g's published
+  // values (order-preserving keys, atomicMin).  gk = 0 (G = 4): a value is a
+  // list's R-th entry, so group g has R rows at or below its slot.  gk = K in
+  // 1..4 (G = 8): a value is the K-th smallest of the union of the query's
+  // lists in this workgroup (its 2 or 4 lanes), so group g has K rows at or
+  // below its slot -- a far smaller value than any one list's R-th entry
+  // (the K-th of a whole split against the R-th of a quarter of it).  Either
+  // way tq = max over the slots has >= G x (R or K) distinct rows at or below
+  // it: any row above tq is outside the query's best G x (R or K) and may be
+  // dropped.  The merge bounds dropped rows by the final tq.  Lists then stop
+  // filling with rows only a cold list would keep -- the insertions (64
+  // independent lists per wave) that dominate the epilogue.
+  // Lanes l and l+32 (same query) fetch slots 0-3 and 4-7 by LDS-DMA into this
+  // wave's 1-KiB area of gls (16 B per lane); they are read after the next
+  // barrier: a plain load into VGPRs would be consumed (or copied) by
+  // compiler code before it lands.
   __shared__ __attribute__((aligned(16))) u32x4 gls[NW * 64];
   const uint32_t gls_addr =
       (uint32_t)(uintptr_t)(__attribute__((address_space(3))) u32x4*)gls + wv * 1024;
@@ -223,8 +229,9 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   // byte offset of gthr[query][0]: the lane's query, or for METRIC 3/4 query
   // (l & 31) of the wave (lanes 0-15 block 0, 16-31 block 1; 32-63 repeat)
   const uint32_t goff =
-      M16 ? (uint32_t)(((int64_t)qt * (NW * QW) + wv * QW + (lane & (QW - 1))) * 16)
-          : (uint32_t)(qg * 16);
+      M16 ? (uint32_t)(((int64_t)qt * (NW * QW) + wv * QW + (lane & (QW - 1))) * (4 * kGthrSlots))
+          : (uint32_t)(qg * (4 * kGthrSlots));
+  const uint32_t* gslot = gthr + (gk ? (split & 7) : (split & 3));
   float tq[NQL], te[NQL];
 #pragma unroll
   for (int b = 0; b < NQL; ++b) tq[b] = te[b] = KNN_INF_F;
@@ -286,8 +293,11 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
         if (x_age == PD) {
 #pragma unroll
           for (int b = 0; b < NQL; ++b) {
-            const u32x4 gv = gls[wv * 64 + (M16 ? 16 * b + c16 : lane)];
-            tq[b] = key2f(max(max(gv.x, gv.y), max(gv.z, gv.w)));
+            // slots 0-3 as fetched by lane qi, 4-7 by lane qi + 32
+            const int qi = M16 ? 16 * b + c16 : j;
+            const u32x4 g0 = gls[wv * 64 + qi], g1 = gls[wv * 64 + qi + 32];
+            tq[b] = key2f(max(max(max(g0.x, g0.y), max(g0.z, g0.w)),
+                              max(max(g1.x, g1.y), max(g1.z, g1.w))));
           }
           x_age = -1;
         }
@@ -297,25 +307,45 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
           uint32_t pk;
           bool pub;
           if constexpr (M16) {
-            const float m0 = quad_min(thr[0]), m1 = quad_min(thr[1]);
+            float m0, m1;
+            if (gk) {
+              float u[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) u[e] = L[0][e];
+              m0 = union_kth<4>(u, gk);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) u[e] = L[1][e];
+              m1 = union_kth<4>(u, gk);
+            } else {
+              m0 = quad_min(thr[0]);
+              m1 = quad_min(thr[1]);
+            }
             pk = f2key(g16 == 0 ? m0 : m1);
             pub = g16 < 2 && pk < last_pub;
           } else {
-            const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(thr[0]),
-                                                             __float_as_uint(thr[0]), false, false);
-            pk = f2key(fminf(__uint_as_float(sw[0]), __uint_as_float(sw[1])));
+            float m;
+            if (gk) {
+              float u[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) u[e] = L[0][e];
+              m = union_kth<2>(u, gk);
+            } else {
+              const auto sw = __builtin_amdgcn_permlane32_swap(
+                  __float_as_uint(thr[0]), __float_as_uint(thr[0]), false, false);
+              m = fminf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+            }
+            pk = f2key(m);
             pub = h == 0 && pk < last_pub;
           }
           x_ops = 1;
           if (__ballot(pub)) {
             if (pub)
-              asm volatile("global_atomic_umin %0, %1, %2" ::"v"(goff), "v"(pk),
-                           "s"(gthr + (split & 3))
+              asm volatile("global_atomic_umin %0, %1, %2" ::"v"(goff), "v"(pk), "s"(gslot)
                            : "memory");
             x_ops = 2;
           }
           if (pub) last_pub = pk;
-          glds16((const char*)gthr + goff, gls_addr);
+          glds16((const char*)gthr + goff + 16 * h, gls_addr);
           x_age = 0;
         }
       }
@@ -498,7 +528,7 @@ static void launch_res(const CandLaunch& c, hipStream_t s) {
   hipLaunchKernelGGL((cand_kernel<DP, R, METRIC, NW>), dim3((unsigned)(c.n_qt * c.S)),
                      dim3(NW * 64), 0, s, c.X32, c.Q32, (int)(c.n_pad / (kTR * res_tpb<METRIC>())), c.S,
                      c.n_qt,
-                     c.out_v, c.out_i, c.ablate, c.gthr);
+                     c.out_v, c.out_i, c.ablate, c.gthr, c.gk);
 }
 
 // Instantiated variants: R in {4, 8, 16}; METRIC 0/2 with NW in {4, 8};

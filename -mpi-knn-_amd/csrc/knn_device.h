@@ -229,7 +229,11 @@ __device__ __forceinline__ float quad_min(float x) {
   const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false,
                                                    false);
   x = __builtin_fminf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
-  return __builtin_fminf(x, __shfl_xor(x, 16, 64));
+  // v_permlane16_swap: r[0], r[1] = the values of lanes l and l^16 (in some
+  // order) -- a VALU op, no LDS round trip as a ds_swizzle would take
+  const auto s2 = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false,
+                                                   false);
+  return __builtin_fminf(__uint_as_float(s2[0]), __uint_as_float(s2[1]));
 }
 
 // Top-R selection for the 16x16 layout: 8 values of one query (rows row0 + i
@@ -256,6 +260,29 @@ __device__ __forceinline__ void select_quad(const f32x4& a, const f32x4& b, int 
   }
 }
 
+// select_quad with a filter tf fixed by the caller for a whole tile (the
+// quad's shared threshold at the tile's start) and this lane's own R-th entry:
+// no cross-lane operation per call.
+template <int R>
+__device__ __forceinline__ void select_quad_f(const f32x4& a, const f32x4& b, int row0,
+                                              float (&L)[R], int (&I)[R], float tf) {
+  float te = __builtin_fminf(tf, L[R - 1]);
+  const float mn = __builtin_fminf(__builtin_fminf(__builtin_fminf(a[0], a[1]),
+                                                   __builtin_fminf(a[2], a[3])),
+                                   __builtin_fminf(__builtin_fminf(b[0], b[1]),
+                                                   __builtin_fminf(b[2], b[3])));
+  if (mn < te) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float v = i < 4 ? a[i] : b[i - 4];
+      if (v < te) {
+        list_insert<R>(L, I, v, row0 + (i < 4 ? i : 16 + i - 4));
+        te = __builtin_fminf(te, L[R - 1]);
+      }
+    }
+  }
+}
+
 // select_quad with the quad's filter te kept by the caller (refreshed from
 // the 4 lanes' thresholds once per staged tile); an insertion lowers it to
 // this lane's new R-th entry.  thr is then L[R-1] and needs no copy.
@@ -273,6 +300,53 @@ __device__ __forceinline__ int row_at(int row0, int c) {
 #else
   return row0 + c;
 #endif
+}
+
+// The 4 smallest of the union of two ascending 4-lists, ascending: the
+// elementwise min of a and reversed b is bitonic and holds them; two
+// compare-exchange stages sort it.
+__device__ __forceinline__ void merge_top4(float (&a)[4], const float (&b)[4]) {
+  float m0 = __builtin_fminf(a[0], b[3]), m1 = __builtin_fminf(a[1], b[2]);
+  float m2 = __builtin_fminf(a[2], b[1]), m3 = __builtin_fminf(a[3], b[0]);
+  const float n0 = __builtin_fminf(m0, m2), n2 = __builtin_fmaxf(m0, m2);
+  const float n1 = __builtin_fminf(m1, m3), n3 = __builtin_fmaxf(m1, m3);
+  a[0] = __builtin_fminf(n0, n1);
+  a[1] = __builtin_fmaxf(n0, n1);
+  a[2] = __builtin_fminf(n2, n3);
+  a[3] = __builtin_fmaxf(n2, n3);
+}
+
+// K-th smallest (K in 1..4, wave-uniform) of the union of the ascending
+// lists t[0..3] held by lanes l and l^32 (LANES = 2) or by the four lanes
+// l&15 + 16r (LANES = 4, the 16x16 MFMA layout's quad).  The lanes hold
+// disjoint row sets, so the result has >= K distinct rows at or below it.
+template <int LANES>
+__device__ __forceinline__ float union_kth(const float (&t)[4], int K) {
+  float lo[4], hi[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    // r[0] = the value of lane l&31, r[1] = that of lane (l&31)+32
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(t[e]), __float_as_uint(t[e]),
+                                                    false, false);
+    lo[e] = __uint_as_float(r[0]);
+    hi[e] = __uint_as_float(r[1]);
+  }
+  merge_top4(lo, hi);
+  if constexpr (LANES == 4) {
+    float a[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      // the lists of lanes l and l^16 (order irrelevant: the merge is symmetric)
+      const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(lo[e]),
+                                                      __float_as_uint(lo[e]), false, false);
+      a[e] = __uint_as_float(r[0]);
+      hi[e] = __uint_as_float(r[1]);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) lo[e] = a[e];
+    merge_top4(lo, hi);
+  }
+  return K <= 1 ? lo[0] : K == 2 ? lo[1] : K == 3 ? lo[2] : lo[3];
 }
 
 template <int R>
@@ -313,6 +387,13 @@ constexpr int kS3R = 256;   // train rows per tile
 constexpr int kS3DC = 16;   // dims per staged chunk
 
 __device__ __forceinline__ int s3_slot(int r, int s) { return s ^ ((r >> 2) & 3); }
+// fp16 S3 images: slot s of row r at s ^ g((r >> 2) & 3), g = (0, 2, 3, 1).
+// Conflict-free for both read patterns of a 16-B-per-lane ds_read_b128:
+// the 32x32x16 one (lanes on rows 0-31, one slot per half-wave) and the
+// 16x16x32 one (lanes on rows l & 15, slot l >> 4): every 16-lane group of the
+// instruction lands on 16 distinct 16-B bank groups.
+__device__ __forceinline__ int s3h_swz(int q) { return (0x78 >> (2 * (q & 3))) & 3; }
+__device__ __forceinline__ int s3h_slot(int r, int s) { return s ^ s3h_swz(r >> 2); }
 
 template <class KernelT>
 static int occupancy_of(KernelT k, int threads) {

@@ -64,10 +64,12 @@ void launch_prep_split_tiled(const double* X64, const double* mu, int64_t n, int
                              int64_t n_pad, double scale, unsigned short* out,
                              const float* seed_src, float* seed_out, hipStream_t s);
 // fp16 S3 kernel (DP > 256, DP % 32 == 0): XT/QT made by launch_prep_half_tiled
+// q16: the v_mfma_f32_16x16x32_f16 form (R = 8 quad lists: [m_pad][4S][8])
 void launch_cand_s3h(const unsigned short* XT, const float* XS, const unsigned short* QT, int DP,
                      int64_t n_pad, int R, int S, int n_qt, float* out_v, int* out_i, int ablate,
-                     hipStream_t s);
+                     bool q16, hipStream_t s);
 int s3h_blocks_per_cu(int R);
+int s3q_blocks_per_cu();
 // S3 workgroup grouping for n_qt query tiles and S splits (knn_cand.hip, s3_map)
 int s3_group(int n_qt, int S);
 int pad_dim_fp16_s3(int d);         // padded dim of the fp16 S3 image (multiple of 32, > 256)
@@ -95,9 +97,15 @@ struct CandLaunch {
   int* out_i;
   int ablate;   // timing-only ablation bits (0 in production)
   int nw;       // resident kernel: waves (x32 queries) per workgroup, 4 or 8
-  uint32_t* gthr;  // resident kernel: per-query global thresholds [m_pad][4] (keys)
+  uint32_t* gthr;  // resident kernel: per-query global thresholds [m_pad][kGthrSlots] (keys)
+  int gk;          // what a list group publishes into gthr (see cand_kernel): 0 = the
+                   // lists' R-th entries into split % 4, K = 1..4: the K-th smallest of
+                   // the union of the query's lists in the workgroup into split % 8
 };
 constexpr uint32_t kGthrInit = 0xFF800000u;  // order-preserving key of +inf
+constexpr int kGthrSlots = 8;                // slots per query in gthr
+// gthr init: slots [0, active) = +inf keys, the rest 0 (never the max)
+void launch_fill_gthr(uint32_t* g, int64_t m_pad, int active, hipStream_t s);
 
 // Candidate-pass operands are centred on the train column means mu (see knn_prep.hip).
 int col_mean_blocks(int64_t n);  // rows of the `partial` scratch (x d doubles)
@@ -116,7 +124,7 @@ void launch_prep_queries(const double* Q64, const double* mu, int64_t m, int d, 
                          int64_t m_pad, double scale, int jx, float* Q32, hipStream_t s);
 // false: no kernel instantiated for this (DP, R, metric, nw) -- nothing launched
 bool launch_cand(const CandLaunch& c, hipStream_t s);
-// gthr: the candidate kernel's per-query global thresholds ([m_pad][4] keys)
+// gthr: the candidate kernel's per-query global thresholds ([m_pad][kGthrSlots] keys)
 // or null when the kernel kept none
 // failed queries are appended to rescan_q with rescan_tau = the W-th exact
 // distance among their re-ranked rows (+inf if unknown)

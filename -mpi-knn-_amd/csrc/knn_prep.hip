@@ -354,11 +354,23 @@ void launch_fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t s) {
   hipLaunchKernelGGL(fill_i32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p, n, v);
 }
 
+__global__ void fill_gthr_kernel(uint32_t* g, int64_t n, int active) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256)
+    g[e] = (int)(e % kGthrSlots) < active ? kGthrInit : 0u;
+}
+void launch_fill_gthr(uint32_t* g, int64_t m_pad, int active, hipStream_t s) {
+  const int64_t n = m_pad * kGthrSlots;
+  if (n <= 0) return;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(fill_gthr_kernel, dim3((unsigned)blocks), dim3(256), 0, s, g, n, active);
+}
+
 // ------------------------------- fp16 S3 images (DP > 256; cand_s3h_kernel)
 // Tile-chunk images: block (tile of kS3R rows, chunk of 32 dims) = kS3R rows
 // x 64 B, the four 16-B slots of row r (dims 0-7, 8-15, 16-23, 24-31 of the
-// chunk) at slot position s ^ ((r >> 2) & 3) -- the bf16x3 S3 layout with
-// one fp16 k-step of 16 dims in place of each hi/lo pair.  One wave per row,
+// chunk) at slot position s3h_slot(r, s) -- the bf16x3 S3 layout with one
+// fp16 k-step of 16 dims in place of each hi/lo pair and its own swizzle.  One wave per row,
 // lane g < DP/8 converting dims 8g .. 8g+7 of mult * (x - mu) at scale 2^jx.
 // Train (mult 1): the row's representation error ||h / 2^jx - (x - mu)||^2
 // is measured as in prep_half_train, seeds fl32(||x32||^2) (+inf on pad
@@ -402,7 +414,7 @@ prep_half_tiled_kernel(const double* __restrict__ X64, const double* __restrict_
       v.z = hv[4] | (uint32_t)hv[5] << 16;
       v.w = hv[6] | (uint32_t)hv[7] << 16;
       unsigned char* blk = (unsigned char*)out + (((int64_t)tile * nch + (g >> 2)) * kS3R + r) * 64;
-      *(uint4*)(blk + s3_slot(r, g & 3) * 16) = v;
+      *(uint4*)(blk + s3h_slot(r, g & 3) * 16) = v;
     }
     if (seed_out && lane == 0) seed_out[row] = row < n ? seed_src[row] : KNN_INF_F;
     if (dx2max) m = fmax(m, wave_sum_d(e2));

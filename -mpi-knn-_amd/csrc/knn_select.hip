@@ -333,8 +333,11 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
     // (cand_kernel): rows it dropped have proxy >= its final value
     float tq = KNN_INF_F;
     if (gthr) {
-      const uint32_t* g = gthr + q * 4;
-      tq = key2f(max(max(g[0], g[1]), max(g[2], g[3])));
+      const uint32_t* g = gthr + q * kGthrSlots;
+      uint32_t mk = g[0];
+#pragma unroll
+      for (int e = 1; e < kGthrSlots; ++e) mk = max(mk, g[e]);
+      tq = key2f(mk);
     }
     if (lane == 0) {
       // void proxies: exact rescan below; non-finite query: no neighbours

@@ -180,14 +180,20 @@ def test_cfg5_d960_k100(knn):
     got, idx, dist, flags = classify(knn, clf, Q, k)
     assert clf.last_candidate_path() == 4, "cfg5 should run the fp16 candidate pass (S3 kernel)"
     assert clf.last_kernel_name().startswith("cand_s3_kernel<")
-    assert clf.last_kernel_name().endswith(",true>")
+    assert clf.last_kernel_name() == "cand_s3_kernel<8,true,true>"
     assert clf.last_rescan_count() * 16 <= m
     lab_all = lab.cpu().numpy()
     sample = np.arange(0, m, 4)
     check_properties(X, lab_all, Q, k, got, idx, dist, sample)
     check_oracle(X, lab_all, Q, k, got, idx, dist, np.arange(0, m, m // 8))
     check_optimal(X, Q, k, dist, np.arange(0, m, m // 128))
-    # the bf16x3 S3 kernel gives the same exact answer
+    # the fp16 S3 kernel on 32x32x16 and the bf16x3 S3 kernel give the same
+    # exact answer
+    clf.set_tuning("s3q", 0)
+    gotw, _, distw, _ = classify(knn, clf, Q, k)
+    assert clf.last_kernel_name() == "cand_s3_kernel<8,true,false>"
+    np.testing.assert_array_equal(gotw, got)
+    assert (distw.view(np.int64) == dist.view(np.int64)).all()
     clf.set_precision(knn.PRECISION_BF16X3)
     gotb, _, distb, _ = classify(knn, clf, Q, k)
     assert clf.last_candidate_path() == 2

@@ -34,16 +34,22 @@ def knn():
     return mod
 
 
-@pytest.fixture(scope="module", params=["auto", "fp32", "m16", "fp16"])
+@pytest.fixture(scope="module", params=["auto", "fp32", "m16", "fp16", "fp16w"])
 def clf(knn, request):
     """Every parity test runs with the default candidate path (AUTO: fp16 for
     batches of >= 4096 queries at d <= 256, else bf16x3 on 32x32x16 for L2),
     with the fp32 path forced, with bf16x3 on the 16x16x32 MFMA layout forced,
-    and with the fp16 path forced (every batch size)."""
+    with the fp16 path forced (every batch size), and with the fp16 path's
+    alternative forms (fp16w: the S3 kernel on 32x32x16 above 256 dims, the
+    resident kernel publishing list thresholds, gk = 0)."""
     c = knn.Classifier(0)
     c.set_precision({"auto": knn.PRECISION_AUTO, "fp32": knn.PRECISION_FP32,
-                     "m16": knn.PRECISION_BF16X3, "fp16": knn.PRECISION_FP16}[request.param])
+                     "m16": knn.PRECISION_BF16X3, "fp16": knn.PRECISION_FP16,
+                     "fp16w": knn.PRECISION_FP16}[request.param])
     c.set_tuning("mfma16", 1 if request.param == "m16" else -1)
+    if request.param == "fp16w":
+        c.set_tuning("s3q", 0)
+        c.set_tuning("gk", 0)
     yield c
     c.close()
 

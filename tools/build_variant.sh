@@ -10,10 +10,12 @@ make -s -j8 >/dev/null
 mkdir -p build/$name
 HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-honor-nans"
 rm -f build/$name/res_*.o build/$name/cand.o
-for g in 0 1 2 3; do
+# VGROUPS: the resident-kernel groups to rebuild (default all); VCAND=0 keeps
+# the default knn_cand.o (S3 / stream kernels)
+for g in ${VGROUPS:-0 1 2 3}; do
   /opt/rocm/bin/hipcc $HIPFLAGS "$@" -DKNN_GROUP=$g -c csrc/knn_cand_res.hip -o build/$name/res_$g.o 2>/dev/null &
 done
-/opt/rocm/bin/hipcc $HIPFLAGS "$@" -c csrc/knn_cand.hip -o build/$name/cand.o 2>/dev/null &
+[ "${VCAND:-1}" = 0 ] || /opt/rocm/bin/hipcc $HIPFLAGS "$@" -c csrc/knn_cand.hip -o build/$name/cand.o 2>/dev/null &
 wait
 [ -f build/$name/cand.o ] || cp build/knn_cand.o build/$name/cand.o
 # a group whose kernels do not fit the variant's geometry (LDS) keeps the

@@ -20,7 +20,7 @@ nc=0
 for s in "$@"; do
   case $s in
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) step tests 900 python -m pytest tests -m gpu -q -p no:cacheprovider -x ;;
+    tests) step tests 1000 python -u -m pytest tests -m gpu -q -p no:cacheprovider -x --timeout 300 --timeout-method thread ;;
     testsall) step testsall 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) step bench 600 python bench.py --steps 10 --warmup 2 ;;
     prof)
