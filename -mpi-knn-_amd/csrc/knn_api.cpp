@@ -567,19 +567,21 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   if ((rc = ctx->cand_i.ensure((size_t)m_pad * NL * R * sizeof(int)))) return rc;
   // per-query global thresholds of the resident candidate kernel
   // (tuning switch "ablate" bit 2 turns the exchange off; results stay exact)
-  const bool use_gthr = DP <= 256 && !(ctx->tune_ablate & 4);
+  // gk: what the lists publish into gthr (cand_kernel, cand_s3_kernel's q16
+  // form): the K-th smallest of the union of a query's lists in a workgroup,
+  // 8 groups, with 8K >= W + 5 rows guaranteed below the threshold (K <= 4
+  // for the resident kernel's 4-entry lists, so W <= 27; K <= 16 in S3,
+  // W <= 123); else, in the resident kernel, the lists' R-th entries in 4
+  // groups.  cfg2 (W = 11): K = 2, the candidate pass 3 % faster than K = 3
+  // and 2-4 % faster than the list thresholds (in-process A/B,
+  // gpurun_out/r2f_ab_gk.log, r2g_ab_pair.log); K = 1 (8 rows < W) sends 5 %
+  // of the queries to the rescan.
+  int gk = (W + 5 + kGthrSlots - 1) / kGthrSlots;
+  if (gk > (s3 ? 16 : 4)) gk = 0;
+  if (ctx->tune_gk >= 0) gk = std::min(ctx->tune_gk, s3 ? 16 : 4);
+  const bool use_gthr = (s3 ? s3q && gk > 0 : DP <= 256) && !(ctx->tune_ablate & 4);
   if (use_gthr && (rc = ctx->gthr.ensure((size_t)m_pad * kGthrSlots * sizeof(uint32_t))))
     return rc;
-  // what the lists publish into gthr (cand_kernel): the K-th smallest of the
-  // union of a query's lists in a workgroup, 8 groups, with 8K >= W + 5 rows
-  // guaranteed below the threshold (K <= 4, so W <= 27); else the lists'
-  // R-th entries in 4 groups.  cfg2 (W = 11): K = 2, the candidate pass 3 %
-  // faster than K = 3 and 2-4 % faster than the list thresholds (in-process
-  // A/B, gpurun_out/r2f_ab_gk.log, r2g_ab_pair.log); K = 1 (8 rows < W)
-  // sends 5 % of the queries to the rescan.
-  int gk = (W + 5 + kGthrSlots - 1) / kGthrSlots;
-  if (gk > 4) gk = 0;
-  if (ctx->tune_gk >= 0) gk = ctx->tune_gk;
   if ((rc = ctx->rescan_q.ensure((size_t)m * sizeof(int) + 16))) return rc;
   if ((rc = ctx->rescan_tau.ensure((size_t)m * sizeof(double) + 16))) return rc;
   if ((rc = ctx->rescan_cnt.ensure(4 * sizeof(int)))) return rc;
@@ -649,7 +651,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   if (s3h)
     launch_cand_s3h((const unsigned short*)ctx->XT16.p, (const float*)ctx->XS16.p,
                     (const unsigned short*)ctx->Q32.p, DP, n_pad3, R, S, n_qt, cl.out_v, cl.out_i,
-                    cl.ablate, s3q, s);
+                    cl.ablate, s3q, cl.gthr, gk, s);
   else if (s3)
     launch_cand_s3((const unsigned short*)ctx->XB.p, (const float*)ctx->XS.p,
                    (const unsigned short*)ctx->Q32.p, DP, n_pad3, R, S, n_qt, cl.out_v, cl.out_i,
@@ -972,7 +974,7 @@ int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value) {
     if (value < -1 || value > 1) return knn_fail(KNN_ERR_ARG, "s3q must be -1, 0 or 1");
     ctx->tune_s3q = (int)value;
   } else if (!strcmp(key, "gk")) {
-    if (value < -1 || value > 4) return knn_fail(KNN_ERR_ARG, "gk must be -1 (auto) .. 4");
+    if (value < -1 || value > 16) return knn_fail(KNN_ERR_ARG, "gk must be -1 (auto) .. 16");
     ctx->tune_gk = (int)value;
   } else {
     return knn_fail(KNN_ERR_ARG, std::string("unknown tuning key ") + key);

@@ -275,8 +275,14 @@ template <int R, bool F16, bool Q16>
 __global__ void __launch_bounds__(512)
 cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* QT, int nch,
                int n_tiles, int S, int n_qt, float* __restrict__ out_v, int* __restrict__ out_i,
-               int abl, int gq) {
+               int abl, int gq, uint32_t* gthr, int gk) {
   static_assert(F16 || !Q16, "the 16x16x32 S3 layout is fp16 only");
+  // gthr / gk (Q16 only; null / 0: none): the per-query global threshold of
+  // cand_kernel -- at tiles 0, 1, 2, 4 and every 4th tile each workgroup
+  // publishes, per query, the gk-th smallest of the union of the query's 4
+  // lists (quad_union_kth16) into slot split % 8 (atomicMin) and fetches the
+  // 8 slots by LDS-DMA; the max over them has >= 8 gk rows at or below it and
+  // joins the quad's filter at the tile's epilogue.
   // abl: timing-only ablations as in cand_kernel (bit0 no staging after the
   // first steps, bit1 no selection epilogue); 0 in production.
   constexpr int BLK = kS3R * 64;        // bytes of one operand image
@@ -285,6 +291,7 @@ cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* 
   constexpr int PD = NB - 1;
   static_assert(4 * (PD - 1) + PD <= 15, "vmcnt wait range");
   __shared__ __attribute__((aligned(16))) unsigned char lds[NB * BUFB];
+  __shared__ __attribute__((aligned(16))) u32x4 gls[Q16 ? 8 * 64 : 1];
 
   int qt, split;
   s3_map(blockIdx.x, gridDim.x, n_qt, gq, qt, split);
@@ -340,7 +347,17 @@ cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* 
 
   f32x16 acc[8];
   f32x4 aq[16][2];  // Q16: [row block][query block]
-  int c = 0, t = split, cb = 0;
+  // Q16 global threshold state (see above); the exchange's ops stay in flight
+  // across PD barriers (counted into their waits) and the slots are read
+  // after the barrier that retires them
+  const bool gx = Q16 && gthr && gk > 0;
+  const uint32_t goff = (uint32_t)(((int64_t)qt * kS3Q + wv * 32 + (lane & 31)) * (4 * kGthrSlots));
+  const uint32_t gls_addr =
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) u32x4*)gls + wv * 1024;
+  float tq[2] = {KNN_INF_F, KNN_INF_F};
+  uint32_t last_pub = kKeyInf;
+  int x_ops = 0, x_age = -1;
+  int c = 0, t = split, cb = 0, ti = 0;
   for (int st = 0; st < total; ++st) {
     // own pieces of step st landed (those of st+1 may still be in flight),
     // then the barrier publishes every wave's pieces and retires all reads
@@ -353,10 +370,42 @@ cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* 
       if (wv == 0)
         for (int jj = 1; jj <= y; ++jj) n += (c + jj) % nch == 0;
       if (abl & 1) n = 0;
+      if (x_age >= 0) ++x_age;
+      if (x_age >= 1 && x_age <= PD) n += x_ops;
       s3_wait_barrier(n);
     }
     __builtin_amdgcn_sched_barrier(0);
     if (st + PD < total && !(abl & 1)) issue();
+    if constexpr (Q16) {
+      if (gx) {
+        if (x_age == PD + 1) {
+#pragma unroll
+          for (int qb = 0; qb < 2; ++qb) {
+            const u32x4 g0 = gls[wv * 64 + 16 * qb + c16], g1 = gls[wv * 64 + 16 * qb + c16 + 32];
+            tq[qb] = key2f(max(max(max(g0.x, g0.y), max(g0.z, g0.w)),
+                               max(max(g1.x, g1.y), max(g1.z, g1.w))));
+          }
+          x_age = -1;
+        }
+        if (x_age < 0 && c == 0 && st + PD < total &&
+            (ti < 4 ? ti != 3 : (ti & 3) == 0)) {
+          const float m0 = quad_union_kth16(L[0], gk), m1 = quad_union_kth16(L[1], gk);
+          const uint32_t pk = f2key(g16 == 0 ? m0 : m1);
+          const bool pub = g16 < 2 && pk < last_pub;
+          x_ops = 1;
+          if (__ballot(pub)) {
+            if (pub)
+              asm volatile("global_atomic_umin %0, %1, %2" ::"v"(goff), "v"(pk),
+                           "s"(gthr + (split & 7))
+                           : "memory");
+            x_ops = 2;
+          }
+          if (pub) last_pub = pk;
+          glds16((const char*)gthr + goff + 16 * h, gls_addr);
+          x_age = 0;
+        }
+      }
+    }
 
     const unsigned char* buf = lds + cb * BUFB;
     if constexpr (Q16) {
@@ -382,7 +431,7 @@ cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* 
           for (int qb = 0; qb < 2; ++qb) {
             // the quad's shared filter once per tile (min over its 4 lists'
             // R-th entries: anything dropped is >= some list's final R-th)
-            const float tf = quad_min(L[qb][R - 1]);
+            const float tf = __builtin_fminf(quad_min(L[qb][R - 1]), tq[qb]);
 #pragma unroll
             for (int rb = 0; rb < 16; rb += 2)
               select_quad_f<R>(aq[rb][qb], aq[rb + 1][qb], t * kS3R + 16 * rb + 4 * g16, L[qb],
@@ -392,7 +441,7 @@ cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* 
           thr[0] = aq[7][0][2];  // keep the accumulators live
         }
       }
-      if (++c == nch) { c = 0; t += S; }
+      if (++c == nch) { c = 0; t += S; ++ti; }
       if (++cb == NB) cb = 0;
       continue;
     }
@@ -521,28 +570,28 @@ void launch_cand_s3(const unsigned short* XT, const float* XS, const unsigned sh
   const int n_tiles = (int)(n_pad / kS3R);
   if (R == 8)
     hipLaunchKernelGGL((cand_s3_kernel<8, false, false>), dim3((unsigned)(n_qt * S)), dim3(512), 0, s, XT,
-                       XS, QT, nch, n_tiles, S, n_qt, out_v, out_i, ablate, gq);
+                       XS, QT, nch, n_tiles, S, n_qt, out_v, out_i, ablate, gq, nullptr, 0);
   else
     hipLaunchKernelGGL((cand_s3_kernel<16, false, false>), dim3((unsigned)(n_qt * S)), dim3(512), 0, s, XT,
-                       XS, QT, nch, n_tiles, S, n_qt, out_v, out_i, ablate, gq);
+                       XS, QT, nch, n_tiles, S, n_qt, out_v, out_i, ablate, gq, nullptr, 0);
 }
 
 void launch_cand_s3h(const unsigned short* XT, const float* XS, const unsigned short* QT, int DP,
                      int64_t n_pad, int R, int S, int n_qt, float* out_v, int* out_i, int ablate,
-                     bool q16, hipStream_t s) {
+                     bool q16, uint32_t* gthr, int gk, hipStream_t s) {
   const int gq = s3_group(n_qt, S);
   const int nch = DP / 32;
   const int n_tiles = (int)(n_pad / kS3R);
   const dim3 g((unsigned)(n_qt * S)), b(512);
   if (q16)
     hipLaunchKernelGGL((cand_s3_kernel<8, true, true>), g, b, 0, s, XT, XS, QT, nch, n_tiles, S,
-                       n_qt, out_v, out_i, ablate, gq);
+                       n_qt, out_v, out_i, ablate, gq, q16 ? gthr : nullptr, q16 ? gk : 0);
   else if (R == 8)
     hipLaunchKernelGGL((cand_s3_kernel<8, true, false>), g, b, 0, s, XT, XS, QT, nch, n_tiles, S,
-                       n_qt, out_v, out_i, ablate, gq);
+                       n_qt, out_v, out_i, ablate, gq, q16 ? gthr : nullptr, q16 ? gk : 0);
   else
     hipLaunchKernelGGL((cand_s3_kernel<16, true, false>), g, b, 0, s, XT, XS, QT, nch, n_tiles, S,
-                       n_qt, out_v, out_i, ablate, gq);
+                       n_qt, out_v, out_i, ablate, gq, q16 ? gthr : nullptr, q16 ? gk : 0);
 }
 
 int s3q_blocks_per_cu() { return occupancy_of(cand_s3_kernel<8, true, true>, 512); }

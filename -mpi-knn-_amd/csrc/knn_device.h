@@ -349,6 +349,54 @@ __device__ __forceinline__ float union_kth(const float (&t)[4], int K) {
   return K <= 1 ? lo[0] : K == 2 ? lo[1] : K == 3 ? lo[2] : lo[3];
 }
 
+// Ascending sort of a bitonic sequence of N (power of two) in registers.
+template <int N>
+__device__ __forceinline__ void bitonic_sort_reg(float (&x)[N]) {
+#pragma unroll
+  for (int st = N / 2; st > 0; st >>= 1) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      if ((i & st) == 0) {
+        const float lo = __builtin_fminf(x[i], x[i + st]), hi = __builtin_fmaxf(x[i], x[i + st]);
+        x[i] = lo;
+        x[i + st] = hi;
+      }
+    }
+  }
+}
+
+// K-th smallest (K in 1..16, wave-uniform) of the union of the ascending
+// 8-lists t held by the four lanes l&15 + 16r (the 16x16 layout's quad):
+// both 8-lists of lanes l, l^32 merged into a sorted 16, then the 16
+// smallest of that and lane l^16's 16.  Rows of different lanes are
+// distinct, so >= K distinct rows lie at or below the result.
+__device__ __forceinline__ float quad_union_kth16(const float (&t)[8], int K) {
+  float a[16], b[16];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(t[e]), __float_as_uint(t[e]),
+                                                    false, false);
+    a[e] = __uint_as_float(r[0]);       // ascending
+    a[15 - e] = __uint_as_float(r[1]);  // descending: a is bitonic
+  }
+  bitonic_sort_reg<16>(a);
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a[e]), __float_as_uint(a[e]),
+                                                    false, false);
+    a[e] = __uint_as_float(r[0]);
+    b[e] = __uint_as_float(r[1]);
+  }
+  // the 16 smallest of two ascending 16-lists, as a bitonic sequence
+#pragma unroll
+  for (int e = 0; e < 16; ++e) a[e] = __builtin_fminf(a[e], b[15 - e]);
+  bitonic_sort_reg<16>(a);
+  float v = a[0];
+#pragma unroll
+  for (int e = 1; e < 16; ++e) v = K == e + 1 ? a[e] : v;
+  return v;
+}
+
 template <int R>
 __device__ __forceinline__ void select_quad_te(const f32x4& a, const f32x4& b, int row0,
                                                float (&L)[R], int (&I)[R], float& te) {

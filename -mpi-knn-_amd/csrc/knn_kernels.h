@@ -65,9 +65,10 @@ void launch_prep_split_tiled(const double* X64, const double* mu, int64_t n, int
                              const float* seed_src, float* seed_out, hipStream_t s);
 // fp16 S3 kernel (DP > 256, DP % 32 == 0): XT/QT made by launch_prep_half_tiled
 // q16: the v_mfma_f32_16x16x32_f16 form (R = 8 quad lists: [m_pad][4S][8])
+// gthr / gk: the global threshold exchange of the q16 form (null / 0: none)
 void launch_cand_s3h(const unsigned short* XT, const float* XS, const unsigned short* QT, int DP,
                      int64_t n_pad, int R, int S, int n_qt, float* out_v, int* out_i, int ablate,
-                     bool q16, hipStream_t s);
+                     bool q16, uint32_t* gthr, int gk, hipStream_t s);
 int s3h_blocks_per_cu(int R);
 int s3q_blocks_per_cu();
 // S3 workgroup grouping for n_qt query tiles and S splits (knn_cand.hip, s3_map)
