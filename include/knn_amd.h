@@ -200,9 +200,12 @@ const char* knn_last_kernel_name(knn_ctx* ctx);
  * lane (4, 8, 16), "S" train splits per query tile (1..64), "nw" waves per
  * candidate workgroup (4 or 8; 32 queries per wave), "ablate" (bits 0/1:
  * timing-only kernel ablations, results invalid; bit 2: no per-query global
- * threshold exchange in the resident kernel, results stay exact); -1 = auto
- * for "fp16" (fp16 candidate pass: 0 off, 1 on) and "mfma16" (bf16x3 on the
- * 16x16x32 layout: 0 off, 1 on). */
+ * threshold exchange, results stay exact); -1 = auto for "fp16" (fp16
+ * candidate pass: 0 off, 1 on), "mfma16" (bf16x3 on the 16x16x32 layout: 0
+ * off, 1 on), "s3q" (the fp16 d > 256 kernel on 16x16x32: 0 off, 1 on) and
+ * "gk" (what the global threshold exchange publishes: 0 the lists' R-th
+ * entries (resident kernel) / no exchange (S3), K = 1..16 the K-th smallest
+ * of a workgroup's union of a query's lists; results stay exact). */
 int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value);
 
 /* Synchronise the context's stream. */

@@ -333,6 +333,36 @@ def test_fp16_workgroup_sizes(knn, nw):
         c.close()
 
 
+@pytest.mark.parametrize("gk", [0, 1, 2, 3, 4])
+def test_global_threshold_ranks(knn, gk):
+    """The resident fp16 kernel with every global-threshold publish rule (gk:
+    0 = the lists' R-th entries in 4 groups, K = 1..4 = the K-th smallest of
+    the union of a workgroup's lists in 8 groups).  K = 1 guarantees fewer
+    rows below the threshold than k+1 (certification then fails more and
+    the rescan finishes those queries): the answer is exact either way."""
+    rng = np.random.default_rng(40 + gk)
+    tr, lab, te = _mix(rng, 20000, 600, 128, 6)
+    c = knn.Classifier(0)
+    c.set_precision(knn.PRECISION_FP16)
+    c.set_tuning("gk", gk)
+    run_case(c, knn, tr, lab, te, 10, 0, 6)
+    c.close()
+
+
+@pytest.mark.parametrize("gk", [0, 1, 6, 16])
+def test_s3_global_threshold_ranks(knn, gk):
+    """The fp16 S3 kernel on 16x16x32 (d > 256) with its global threshold off
+    (gk 0) and published at ranks 1, 6 and 16 of each workgroup's quad union."""
+    rng = np.random.default_rng(50 + gk)
+    tr, lab, te = _mix(rng, 6000, 300, 300, 5)
+    c = knn.Classifier(0)
+    c.set_precision(knn.PRECISION_FP16)
+    c.set_tuning("gk", gk)
+    run_case(c, knn, tr, lab, te, 40, 0, 5)
+    assert c.last_kernel_name() == "cand_s3_kernel<8,true,true>"
+    c.close()
+
+
 def test_nonfinite_inputs(knn):
     """NaN / inf: a train set holding one is refused (host and device entry
     points; the reference's distances would be undefined for every query);
