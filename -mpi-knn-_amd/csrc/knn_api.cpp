@@ -248,13 +248,14 @@ static int ensure_fp16(knn_ctx* ctx, hipStream_t s) {
   const TrainDev& t = ctx->train;
   const int DPh = pad_dim_fp16(t.d);
   if (DPh <= 0) return knn_fail(KNN_ERR_ARG, "fp16 path supports d <= 256");
-  if (ctx->DPh == DPh) return KNN_OK;
+  const int swz = ctx->tune_xhswz != 0;  // chunk swizzle of the image (xh_swz)
+  if (ctx->DPh == DPh && ctx->xh_swz == swz) return KNN_OK;
   int rc;
   if ((rc = ctx->XH.ensure((size_t)t.n_pad * (DPh / 2 + 4) * sizeof(float) + 1024))) return rc;
   unsigned long long* st_d = (unsigned long long*)ctx->stats.p + 3;
   HIP_TRY(hipMemsetAsync(st_d, 0, 8, s));
   launch_prep_half_train(t.X64, t.mu, t.n, t.d, DPh, t.n_pad, t.jx,
-                         (unsigned short*)ctx->XH.p, t.xinit_l2, st_d, s);
+                         (unsigned short*)ctx->XH.p, t.xinit_l2, st_d, swz, s);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(ctx->h_stats + 3, st_d, 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
@@ -263,6 +264,7 @@ static int ensure_fp16(knn_ctx* ctx, hipStream_t s) {
   // + the fp64 rounding of x - mu itself (<= 2^-53 relative per element)
   ctx->train.dxmax = std::sqrt(dx2) * (1.0 + 1e-12) + 0x1p-50 * std::sqrt(t.x2max);
   ctx->DPh = DPh;
+  ctx->xh_swz = swz;
   return KNN_OK;
 }
 
@@ -646,6 +648,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   cl.nw = nw;
   cl.gthr = use_gthr ? (uint32_t*)ctx->gthr.p : nullptr;
   cl.gk = gk;
+  cl.xsw = ctx->xh_swz;
   // slots of groups without a split stay 0 (never the max)
   if (use_gthr) launch_fill_gthr(cl.gthr, m_pad, std::min(S, gk ? 8 : 4), s);
   if (s3h)
@@ -973,6 +976,9 @@ int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value) {
   } else if (!strcmp(key, "s3q")) {
     if (value < -1 || value > 1) return knn_fail(KNN_ERR_ARG, "s3q must be -1, 0 or 1");
     ctx->tune_s3q = (int)value;
+  } else if (!strcmp(key, "xhswz")) {
+    if (value < 0 || value > 1) return knn_fail(KNN_ERR_ARG, "xhswz must be 0 or 1");
+    ctx->tune_xhswz = (int)value;
   } else if (!strcmp(key, "gk")) {
     if (value < -1 || value > 16) return knn_fail(KNN_ERR_ARG, "gk must be -1 (auto) .. 16");
     ctx->tune_gk = (int)value;

@@ -35,6 +35,7 @@ struct knn_ctx {
   int precision = 0;     // KNN_PRECISION_*
   int DPb = 0;           // padded dim of the bf16x3 copy (0 = not built)
   int DPh = 0;           // padded dim of the fp16 copy (0 = not built)
+  int xh_swz = 0;        // the fp16 copy's chunks are swizzled (xh_swz)
   int DPs = 0;           // padded dim of the fp16 S3 image (0 = not built)
   double xamax = 0.0;    // max |x_i - mu_i| over the train set
   bool fp16_off = false; // AUTO: fp16 candidate pass retired for this train set
@@ -48,7 +49,8 @@ struct knn_ctx {
   int tune_ablate = 0;         // timing-only kernel ablations
   int tune_nw = 0;             // resident kernel waves per workgroup (0 = auto)
   int tune_s3q = -1;           // fp16 S3 on the 16x16x32 layout: -1 auto, 0 off, 1 on
-  int tune_gk = -1;            // resident kernel gthr publish rank (-1 auto, 0 list R-th, 1..4)
+  int tune_gk = -1;
+  int tune_xhswz = 1;          // fp16 train image chunk swizzle (xh_swz): 1 on, 0 off (A/B)            // resident kernel gthr publish rank (-1 auto, 0 list R-th, 1..4)
   int tune_fp16 = -1;          // fp16 candidate pass: -1 auto, 0 off, 1 on
   int tune_m16 = -1;           // bf16x3 on the 16x16x32 MFMA layout: -1 auto, 0 off, 1 on
   int last_nw = 0;

@@ -99,7 +99,7 @@ __global__ void __launch_bounds__(NW * 64)
 __attribute__((amdgpu_waves_per_eu((METRIC == 4 ? DP / 2 : DP) <= 160 && R <= 8 ? 4 : 1)))
 cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
             int n_qt, float* __restrict__ out_v, int* __restrict__ out_i, int abl,
-            uint32_t* gthr, int gk) {
+            uint32_t* gthr, int gk, int xsw) {
 #if KNN_SETPRIO
   // the second-dispatched half of the workgroup at priority 1 (MI355X_MICROARCH
   // "Two waves per SIMD", item 4)
@@ -382,12 +382,15 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
         }
       }
       if constexpr (F16) {
-        // fp16 x fp16 products are exact in fp32: one MFMA per 32 dims
+        // fp16 x fp16 products are exact in fp32: one MFMA per 32 dims; the
+        // lane's chunk 4ks + g16 sits at 4ks + (g16 ^ xh_swz(row)) (rows of a
+        // sub-tile start at multiples of 32, so row & 15 = c16)
+        const int g16s = g16 ^ (xsw ? xh_swz(c16) : 0);
 #pragma unroll
         for (int ks = 0; ks < DP / 32; ++ks) {
 #pragma unroll
           for (int rb = 0; rb < 2; ++rb) {
-            const float* ar = base + (rb * 16 + c16) * RSF + 16 * ks + 4 * g16;
+            const float* ar = base + (rb * 16 + c16) * RSF + 16 * ks + 4 * g16s;
             const f16x8 a = __builtin_bit_cast(f16x8, *(const float4*)ar);
 #pragma unroll
             for (int qb = 0; qb < QB; ++qb) {
@@ -528,7 +531,7 @@ static void launch_res(const CandLaunch& c, hipStream_t s) {
   hipLaunchKernelGGL((cand_kernel<DP, R, METRIC, NW>), dim3((unsigned)(c.n_qt * c.S)),
                      dim3(NW * 64), 0, s, c.X32, c.Q32, (int)(c.n_pad / (kTR * res_tpb<METRIC>())), c.S,
                      c.n_qt,
-                     c.out_v, c.out_i, c.ablate, c.gthr, c.gk);
+                     c.out_v, c.out_i, c.ablate, c.gthr, c.gk, c.xsw);
 }
 
 // Instantiated variants: R in {4, 8, 16}; METRIC 0/2 with NW in {4, 8};

@@ -429,6 +429,15 @@ __device__ __forceinline__ void write_lists(float* __restrict__ out_v, int* __re
   }
 }
 
+// fp16 resident-kernel image (XH): 16-B chunk ch of row r's payload is
+// stored at chunk ch ^ xh_swz(r).  With the odd row stride of DP/8 + 1 chunks
+// the 16x16x32 A-fragment reads (lane l: row l & 15, chunk 4ks + (l >> 4))
+// then hit 16 distinct 16-B bank groups in every 16-lane group of a
+// ds_read_b128 for every DP the kernel serves; unswizzled, each group had a
+// 2-way conflict at DP = 128 (4 extra LDS cycles per read) and more at
+// other DPs (exhaustive check over DP = 32 .. 256).
+__device__ __forceinline__ int xh_swz(int r) { return ((r >> 2) ^ (r >> 3)) & 1; }
+
 // S3 (bf16x3, DP > 256) image geometry; see knn_cand.hip
 constexpr int kS3Q = 256;   // queries per workgroup
 constexpr int kS3R = 256;   // train rows per tile

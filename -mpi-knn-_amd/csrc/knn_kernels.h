@@ -99,6 +99,7 @@ struct CandLaunch {
   int ablate;   // timing-only ablation bits (0 in production)
   int nw;       // resident kernel: waves (x32 queries) per workgroup, 4 or 8
   uint32_t* gthr;  // resident kernel: per-query global thresholds [m_pad][kGthrSlots] (keys)
+  int xsw;         // fp16 (metric 4): the train image's chunks are swizzled (xh_swz)
   int gk;          // what a list group publishes into gthr (see cand_kernel): 0 = the
                    // lists' R-th entries into split % 4, K = 1..4: the K-th smallest of
                    // the union of the query's lists in the workgroup into split % 8
@@ -189,9 +190,10 @@ void launch_fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t s);
 // (zero for queries launch_query_check marked invalid)
 // dx2max: running max (u64 bits of a non-negative double) of the rows'
 // ||fp16 / 2^jx - (x - mu)||_2^2 (measured representation error)
+// swz: store the payload chunks swizzled (xh_swz, knn_device.h)
 void launch_prep_half_train(const double* X64, const double* mu, int64_t n, int d, int DP,
                             int64_t n_pad, int jx, unsigned short* out, const float* xl2,
-                            unsigned long long* dx2max, hipStream_t s);
+                            unsigned long long* dx2max, int swz, hipStream_t s);
 // mu <- mu rounded to a multiple of 2^-g (the centre then sits on any data
 // grid at least as coarse, so such data is exact in the fp16 operands)
 void launch_round_mu(double* mu, int d, int g, hipStream_t s);

@@ -264,7 +264,8 @@ void launch_prep_split(const double* X64, const double* mu, int64_t n, int d, in
 __global__ void __launch_bounds__(256)
 prep_half_train_kernel(const double* __restrict__ X64, const double* __restrict__ mu, int64_t n,
                        int d, int DP, int64_t n_pad, int jx, unsigned short* __restrict__ out,
-                       const float* __restrict__ xl2, unsigned long long* __restrict__ dx2max) {
+                       const float* __restrict__ xl2, unsigned long long* __restrict__ dx2max,
+                       int swz) {
   // one wave per row; the row's representation error ||h / 2^jx - (x - mu)||^2
   // is measured in fp64 (h / 2^jx - x is exact: Sterbenz, or h = 0)
   const int row_shorts = DP + 8;
@@ -274,6 +275,7 @@ prep_half_train_kernel(const double* __restrict__ X64, const double* __restrict_
   double m = 0.0;
   for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n_pad; row += wstride) {
     double e2 = 0.0;
+    const int cx = swz ? xh_swz((int)(row & 15)) << 3 : 0;
     for (int c = lane; c < DP; c += 64) {
       _Float16 h = (_Float16)0.0f;
       if (row < n && c < d) {
@@ -282,7 +284,8 @@ prep_half_train_kernel(const double* __restrict__ X64, const double* __restrict_
         const double e = (double)h * sinv - x;
         e2 += e * e;
       }
-      out[row * row_shorts + c] = __builtin_bit_cast(unsigned short, h);
+      // 16-B chunk c >> 3 stored at (c >> 3) ^ xh_swz(row) (knn_device.h)
+      out[row * row_shorts + (c ^ cx)] = __builtin_bit_cast(unsigned short, h);
     }
     if (lane < 4) {
       // slot 0: the row's own seed; the pad of row 4g also carries the seeds
@@ -297,11 +300,11 @@ prep_half_train_kernel(const double* __restrict__ X64, const double* __restrict_
 
 void launch_prep_half_train(const double* X64, const double* mu, int64_t n, int d, int DP,
                             int64_t n_pad, int jx, unsigned short* out, const float* xl2,
-                            unsigned long long* dx2max, hipStream_t s) {
+                            unsigned long long* dx2max, int swz, hipStream_t s) {
   int64_t blocks = (n_pad + 3) / 4;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(prep_half_train_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X64, mu, n, d,
-                     DP, n_pad, jx, out, xl2, dx2max);
+                     DP, n_pad, jx, out, xl2, dx2max, swz);
 }
 
 __global__ void round_mu_kernel(double* mu, int d, int g) {
