@@ -432,9 +432,13 @@ void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int
 #define KNN_MR(M_, NT_, EPL_) \
   launch_mr<M_, NT_, EPL_>(cv, ci, U, R, t, Q64, m, W, C, C2, f_err, ps, gthr, sink, rescan_q, \
                            rescan_tau, rescan_cnt, s)
+  // fewer entries per lane when the union is small (cfg2: 152 lists x 4 =
+  // 608 entries -> 10 per lane): every radix-select step and the selection
+  // loops run over EPL unrolled entries
+  const bool narrow = U <= 640;
   if (metric == 0) {
     if (big) { if (wide) KNN_MR(0, 256, 32); else KNN_MR(0, 256, 16); }
-    else { if (wide) KNN_MR(0, 64, 32); else KNN_MR(0, 64, 16); }
+    else { if (wide) KNN_MR(0, 64, 32); else if (narrow) KNN_MR(0, 64, 10); else KNN_MR(0, 64, 16); }
   } else {
     if (big) { if (wide) KNN_MR(1, 256, 32); else KNN_MR(1, 256, 16); }
     else { if (wide) KNN_MR(1, 64, 32); else KNN_MR(1, 64, 16); }
