@@ -109,7 +109,9 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   // fragments as invariant and re-loads them inside the tile loop instead of
   // keeping them in VGPRs (its waits would then also drain the LDS-DMA queue).
   // abl: timing-only ablations (results invalid): bit0 = no staging loads
-  // after the first tiles, bit1 = no selection epilogue.  0 in production.
+  // after the first tiles, bit1 = no selection epilogue, bit3 = staging
+  // pieces always of an L2-resident tile, bit4 = no workgroup barrier (own
+  // vmcnt wait only).  0 in production.
   // fp16 operands: METRIC 4 on the 16x16x32 layout
   constexpr bool F16 = METRIC == 4;
   constexpr bool TEC = METRIC == 4 && KNN_M4_TE_CACHE;
@@ -278,7 +280,11 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       const int ahead = min(PD - 1, my_nt - 1 - it);
       if (x_age >= 0) ++x_age;
       const int extra = (x_age >= 1 && x_age <= PD - 1) ? x_ops : 0;
-      if (ahead >= 2 && PD >= 3) {
+      if (abl & 16) {
+        // timing-only ablation: this wave's own waits, no workgroup barrier
+        // (other waves' pieces may not have landed: results invalid)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else if (ahead >= 2 && PD >= 3) {
         if (g_hi) wait_barrier_x<2 * G_HI>(extra); else wait_barrier_x<2 * G_LO>(extra);
       } else if (ahead == 1) {
         if (g_hi) wait_barrier_x<G_HI>(extra); else wait_barrier_x<G_LO>(extra);
