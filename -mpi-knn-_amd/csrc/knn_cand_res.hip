@@ -28,6 +28,12 @@ static_assert(KNN_RES_TPB * knnk::kTR == knnk::kResTileRows || KNN_RES_TPB != 2,
 #ifndef KNN_M4_SEED4
 #define KNN_M4_SEED4 1
 #endif
+// fp16 kernel: the selection of sub-tile s runs after the MFMAs of sub-tile
+// s+1 are issued (its accumulators are complete by then), so a wave never
+// waits for its own MFMA chains to drain before its min-trees
+#ifndef KNN_M4_PIPE
+#define KNN_M4_PIPE 1
+#endif
 
 namespace knnk {
 
@@ -241,6 +247,10 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   int x_ops = 0, x_age = -1;  // ops of the pending exchange, tiles since it
 
   const int my_nt = split < n_tiles ? (n_tiles - split + S - 1) / S : 0;
+  constexpr bool PIPE = TEC && KNN_M4_PIPE;
+  f32x4 accp[2][QB];  // PIPE: the previous sub-tile's accumulators
+  int rowp = 0;
+  bool havep = false;
 
   // ---- staging: this wave's LDS-DMA pieces i = wv, wv+NW, ... of tile t ->
   // buffer b.  The last piece may read past the tile (and past the last row:
@@ -425,7 +435,23 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       }
       }
       const int row0 = (t * TPB + sub) * kTR + 4 * g16;
-      if (!(abl & 2)) {
+      if constexpr (PIPE) {
+        if (!(abl & 2)) {
+          if (havep) {
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb)
+              select_quad_te<R>(accp[0][qb], accp[1][qb], rowp, L[qb], I[qb], te[qb]);
+          }
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb) accp[rb][qb] = acc[rb][qb];
+          rowp = row0;
+          havep = true;
+        } else if (acc[0][0][0] == 1234.5f && acc[1][1][3] == 1234.5f) {
+          thr[0] = acc[0][1][2];  // keep the accumulators live
+        }
+      } else if (!(abl & 2)) {
         if constexpr (TEC) {
 #pragma unroll
           for (int qb = 0; qb < QB; ++qb)
@@ -496,6 +522,13 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
 
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (PIPE) {
+    if (havep) {
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb)
+        select_quad_te<R>(accp[0][qb], accp[1][qb], rowp, L[qb], I[qb], te[qb]);
+    }
+  }
 
   if constexpr (M16) {
     // 4 lists per query per split (lane groups l>>4): [query][4S][R]
