@@ -247,7 +247,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   int x_ops = 0, x_age = -1;  // ops of the pending exchange, tiles since it
 
   const int my_nt = split < n_tiles ? (n_tiles - split + S - 1) / S : 0;
-  constexpr bool PIPE = TEC && KNN_M4_PIPE;
+  constexpr bool PIPE = TEC && KNN_M4_PIPE && DP <= 192;  // DP 256: no registers to spare
   f32x4 accp[2][QB];  // PIPE: the previous sub-tile's accumulators
   int rowp = 0;
   bool havep = false;
