@@ -552,9 +552,12 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   C = std::min(C, kMaxUnion);
   int S = 1, R = 8;
   // fp16 S3 on v_mfma_f32_16x16x32_f16 (quad lists of R = 8) where its lists
-  // can hold the query's top W (share W / 4S <= 0.8 at S <= 32, i.e. W <= 102);
-  // tuning key "s3q": -1 auto, 0 off (32x32x16), 1 on where feasible
-  const bool s3q = s3h && ctx->tune_s3q != 0 && (W * 5 + 15) / 16 <= kMaxUnion / 32;
+  // can hold the query's top W (share W / 4S <= 0.8 at S <= 32, i.e. W <= 102)
+  // and the train set has that many tiles to split (else the 32x32x16 form,
+  // whose R = 16 lists need fewer splits); tuning key "s3q": -1 auto, 0 off
+  // (32x32x16), 1 on where feasible
+  const int s3q_S = (W * 5 + 15) / 16;
+  const bool s3q = s3h && ctx->tune_s3q != 0 && s3q_S <= kMaxUnion / 32 && s3q_S <= n_tiles;
   choose_geometry(ctx, kmetric, s3, DP, nw, n_qt, n_tiles, W, C, s3q, S, R);
   // 16x16 layouts: 4 lists per query per split
   const bool quad_lists = (!s3 && (kmetric == 3 || kmetric == 4)) || s3q;
@@ -688,13 +691,17 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   const bool abl = ctx->tune_ablate & 11;
   launch_rescan(metric, t, dQ, rb, abl ? 0 : cap, W, err_factor(metric, t.DP), sink,
                 abl ? 0 : (int)std::min<int64_t>(m, ctx->cu_count), s);
+  // (without the full-scan launch nothing writes this call's counts)
+  if (abl) launch_fill_i32(ctx->d_counts, 2, 0, s);
   HIP_TRY(hipGetLastError());
   if (tc) HIP_TRY(hipEventRecord(tc->ev[4], s));
   HIP_TRY(hipEventRecord(ctx->done_ev, s));
-  if (kmetric == 4 && ctx->precision == KNN_PRECISION_AUTO && ctx->tune_fp16 < 0) {
-    ctx->auto_pending = true;
-    ctx->auto_m = m;
-  }
+  // the deferred AUTO decision reads done_ev and h_counts, which belong to
+  // the LAST call: it is armed by an fp16 call and dropped by any other
+  // (a later fp16 call re-arms it with its own count)
+  ctx->auto_pending =
+      kmetric == 4 && ctx->precision == KNN_PRECISION_AUTO && ctx->tune_fp16 < 0 && !abl;
+  ctx->auto_m = m;
   return KNN_OK;
 }
 
@@ -712,8 +719,10 @@ static int run_large_k(knn_ctx* ctx, const double* dQ, int64_t m, int W, int met
   ctx->last_kmetric = -1;
   launch_large_k(metric, t, dQ, m, W, ctx->class_cnt, (unsigned char*)ctx->lk.p, per, (int)nwg,
                  sink, s);
+  launch_fill_i32(ctx->d_counts, 2, 0, s);  // exact path: no query fails certification
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(ctx->done_ev, s));
+  ctx->auto_pending = false;  // done_ev / h_counts now belong to this call
   return KNN_OK;
 }
 
@@ -828,14 +837,17 @@ int knn_merge_vote_device(knn_ctx* ctx, const double* d_dist, const int64_t* d_i
                           double* d_out_dist, int32_t* d_flags, void* stream) {
   int rc;
   if ((rc = device_guard(ctx))) return rc;
-  if (parts <= 0 || w <= 0 || k < 0 || k > w || (int64_t)parts * w > 4096)
-    return knn_fail(KNN_ERR_ARG, "bad merge geometry (need 0 <= k <= w, parts*w <= 4096)");
+  if (parts <= 0 || w <= 0 || k < 0 || k > w || (int64_t)parts * w >= INT32_MAX)
+    return knn_fail(KNN_ERR_ARG, "bad merge geometry (need 0 <= k <= w)");
   if (q0 < 0 || mq < 0 || q0 + mq > m) return knn_fail(KNN_ERR_ARG, "query slice out of range");
   if (!d_labels) return knn_fail(KNN_ERR_ARG, "null labels output");
   if (mq == 0) return KNN_OK;
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  // unions beyond the LDS kernel's 4096 entries: rank merge through scratch
+  if (const int64_t sb = merge_scratch_bytes(parts, w, k, mq))
+    if ((rc = ctx->mrg.ensure((size_t)sb))) return rc;
   launch_merge_vote_partials(d_dist, d_idx, d_lab, parts, m, w, k, d_labels, d_out_idx,
-                             d_out_dist, d_flags, s, q0, mq);
+                             d_out_dist, d_flags, s, q0, mq, 0, ctx->mrg.p);
   HIP_TRY(hipGetLastError());
   return KNN_OK;
 }

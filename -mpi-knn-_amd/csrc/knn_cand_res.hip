@@ -92,11 +92,12 @@ constexpr int res_tpb() {
 // NW waves (32 queries each) share every staged tile: NW = 8 halves the
 // staging instructions and L2 traffic per MFMA relative to NW = 4.
 //
-// Staging: global_load_lds (LDS-DMA, no VGPRs), 3 LDS buffers: tile it+2 is
-// issued right after the barrier that opens tile it, and each wave waits
-// with a counted vmcnt for its own pieces of tile it before that barrier --
-// two tiles of latency hidden, one barrier per tile.  (A register-staged
-// variant measured the same or slower; removed.)
+// Staging: global_load_lds (LDS-DMA, no VGPRs) into NB = KNN_RES_NB LDS
+// buffers (2 by default): tile it+NB-1 is issued right after the barrier
+// that opens tile it, and each wave waits with a counted vmcnt for its own
+// pieces of tile it before that barrier -- NB-1 tiles of latency hidden, one
+// barrier per tile.  (A register-staged variant measured the same or
+// slower; removed.)
 // waves_per_eu(4): 4 waves per SIMD (<= 128 VGPRs), so two 8-wave workgroups
 // share a CU and one's barrier/epilogue gaps are filled by the other's MFMAs
 // (not for R = 16 lists or DP > 160, whose registers do not fit: spills).

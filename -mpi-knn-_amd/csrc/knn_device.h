@@ -6,7 +6,10 @@
 #include <float.h>
 #include <limits.h>
 
+#include <map>
+#include <mutex>
 #include <type_traits>
+#include <utility>
 
 #pragma clang fp contract(off)
 
@@ -86,6 +89,12 @@ __device__ __forceinline__ double exact_dist(const double* __restrict__ q,
                                              const double* __restrict__ x, int d) {
   const double r = exact_dist_raw<METRIC>(q, x, d);
   return METRIC == 0 ? __builtin_sqrt(r) : r;  // llvm.sqrt.f64: correctly rounded
+}
+
+// NaN / inf test on the exponent bits: survives -fno-honor-nans (which lets
+// clang fold __builtin_isfinite / isnan to constants), so every TU may use it.
+__device__ __forceinline__ bool nonfinite_bits(double x) {
+  return (__double_as_longlong(x) & 0x7FF0000000000000ll) == 0x7FF0000000000000ll;
 }
 
 template <typename K, typename I>
@@ -452,11 +461,21 @@ __device__ __forceinline__ int s3_slot(int r, int s) { return s ^ ((r >> 2) & 3)
 __device__ __forceinline__ int s3h_swz(int q) { return (0x78 >> (2 * (q & 3))) & 3; }
 __device__ __forceinline__ int s3h_slot(int r, int s) { return s ^ s3h_swz(r >> 2); }
 
+// Resident workgroups per CU of a kernel variant: a property of the code
+// object (registers, LDS), asked of the runtime once per (kernel, block
+// size) and cached -- choose_geometry runs on every classify call, which
+// must stay enqueue-only with no runtime queries in the timed loop.
 template <class KernelT>
 static int occupancy_of(KernelT k, int threads) {
+  static std::mutex mu;
+  static std::map<std::pair<const void*, int>, int> cache;
+  const auto key = std::make_pair((const void*)k, threads);
+  std::lock_guard<std::mutex> lock(mu);
+  const auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
   int nb = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, threads, 0) != hipSuccess) return 1;
-  return nb > 0 ? nb : 1;
+  return cache[key] = nb > 0 ? nb : 1;
 }
 
 #define KNN_DP_LIST(X) X(8) X(16) X(24) X(32) X(48) X(64) X(96) X(128) X(160) X(192) X(256)

@@ -15,7 +15,6 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
-#include <chrono>
 #include <string>
 #include <thread>
 #include <vector>
@@ -34,6 +33,7 @@ struct knn_group {
   std::vector<DevBuf> Q, olab, oidx, odist, oflags;
   std::vector<DevBuf> pk, gk;                  // train-sharded packed partial / gathered lists
   std::vector<DevBuf> nX, nmm;                 // normalisation shards / per-dim bounds
+  std::vector<hipEvent_t> ev0, ev1;            // per device: around the last call's device work
   int64_t n = 0;
   int d = 0;
   int class_cnt = 0;
@@ -102,6 +102,15 @@ int knn_group_create(knn_group** out, int ndev, const int* devs, int mode) {
   for (auto* v : {&g->X, &g->lab, &g->Q, &g->olab, &g->oidx, &g->odist, &g->oflags, &g->pk,
                   &g->gk, &g->nX, &g->nmm})
     v->resize(ndev);
+  g->ev0.assign(ndev, nullptr);
+  g->ev1.assign(ndev, nullptr);
+  for (int i = 0; i < ndev; i++) {
+    if (hipSetDevice(g->devs[i]) != hipSuccess || hipEventCreate(&g->ev0[i]) != hipSuccess ||
+        hipEventCreate(&g->ev1[i]) != hipSuccess) {
+      knn_group_destroy(g);
+      return knn_fail(KNN_ERR_DEVICE, "hipEventCreate failed");
+    }
+  }
   *out = g;
   return KNN_OK;
 }
@@ -116,6 +125,8 @@ int knn_group_destroy(knn_group* g) {
     for (auto* v : {&g->X, &g->lab, &g->Q, &g->olab, &g->oidx, &g->odist, &g->oflags, &g->pk,
                     &g->gk, &g->nX, &g->nmm})
       if (i < (int)v->size()) (*v)[i].release();
+    for (auto* ev : {&g->ev0, &g->ev1})
+      if (i < (int)ev->size() && (*ev)[i]) (void)hipEventDestroy((*ev)[i]);
   }
   for (auto c : g->comms)
     if (c) ncclCommDestroy(c);
@@ -197,57 +208,79 @@ int knn_group_classify(knn_group* g, const double* Q, int64_t m, int32_t k, int3
   if (m == 0) return KNN_OK;
   const int G = g->ndev;
   const int d = g->d;
-  using clk = std::chrono::steady_clock;
+  // Every step of a call is enqueued from this thread on the devices'
+  // context streams (H2D, compute, collectives, D2H: all asynchronous) and
+  // the host waits once per device at the end; the compute span is read
+  // from events around the device work (max over devices).
+  auto slice = [&](int i, int64_t& q0, int64_t& mi) {
+    q0 = m * i / G;
+    mi = m * (i + 1) / G - q0;
+  };
+  auto d2h = [&](int i, int64_t q0, int64_t mi) -> int {
+    hipStream_t s = g->ctx[i]->stream;
+    HIP_G(hipMemcpyAsync(out_labels + q0, g->olab[i].p, mi * sizeof(int32_t),
+                         hipMemcpyDeviceToHost, s));
+    if (out_flags)
+      HIP_G(hipMemcpyAsync(out_flags + q0, g->oflags[i].p, mi * sizeof(int32_t),
+                           hipMemcpyDeviceToHost, s));
+    if (out_idx && k > 0)
+      HIP_G(hipMemcpyAsync(out_idx + q0 * k, g->oidx[i].p, mi * k * sizeof(int64_t),
+                           hipMemcpyDeviceToHost, s));
+    if (out_dist && k > 0)
+      HIP_G(hipMemcpyAsync(out_dist + q0 * k, g->odist[i].p, mi * k * sizeof(double),
+                           hipMemcpyDeviceToHost, s));
+    return KNN_OK;
+  };
+  auto finish = [&]() -> int {
+    double span = 0.0;
+    for (int i = 0; i < G; i++) {
+      HIP_G(hipSetDevice(g->devs[i]));
+      HIP_G(hipStreamSynchronize(g->ctx[i]->stream));
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, g->ev0[i], g->ev1[i]) == hipSuccess)
+        span = std::max(span, (double)ms * 1e-3);
+    }
+    g->last_compute = span;
+    return KNN_OK;
+  };
+  int rc;
   if (g->mode == 0) {
     // query shards: [m*i/G, m*(i+1)/G)  (ragged shards allowed, unlike cpp:127-129)
-    int rc = for_each_dev(g, [&](int i) {
-      const int64_t q0 = m * i / G, q1 = m * (i + 1) / G, mi = q1 - q0;
-      if (mi <= 0) return KNN_OK;
-      int e;
-      if ((e = g->Q[i].ensure((size_t)mi * d * sizeof(double)))) return e;
-      if ((e = g->olab[i].ensure((size_t)mi * sizeof(int32_t)))) return e;
-      if ((e = g->oflags[i].ensure((size_t)mi * sizeof(int32_t)))) return e;
-      if ((e = g->oidx[i].ensure((size_t)mi * std::max(k, 1) * sizeof(int64_t)))) return e;
-      if ((e = g->odist[i].ensure((size_t)mi * std::max(k, 1) * sizeof(double)))) return e;
+    for (int i = 0; i < G; i++) {
+      int64_t q0, mi;
+      slice(i, q0, mi);
+      HIP_G(hipSetDevice(g->devs[i]));
       hipStream_t s = g->ctx[i]->stream;
-      if (hipMemcpyAsync(g->Q[i].p, Q + q0 * d, (size_t)mi * d * sizeof(double),
-                         hipMemcpyHostToDevice, s) != hipSuccess ||
-          hipStreamSynchronize(s) != hipSuccess)
-        return knn_fail(KNN_ERR_DEVICE, "H2D of query shard failed");
-      return KNN_OK;
-    });
-    if (rc) return rc;
-    auto t0 = clk::now();
-    rc = for_each_dev(g, [&](int i) {
-      const int64_t q0 = m * i / G, q1 = m * (i + 1) / G, mi = q1 - q0;
-      if (mi <= 0) return KNN_OK;
-      int e = knn_classify_device(g->ctx[i], (const double*)g->Q[i].p, mi, k, metric,
-                                  (int32_t*)g->olab[i].p, out_idx ? (int64_t*)g->oidx[i].p : nullptr,
-                                  out_dist ? (double*)g->odist[i].p : nullptr,
-                                  (int32_t*)g->oflags[i].p, nullptr);
-      if (e) return e;
-      return knn_sync(g->ctx[i]);
-    });
-    g->last_compute = std::chrono::duration<double>(clk::now() - t0).count();
-    if (rc) return rc;
-    return for_each_dev(g, [&](int i) {
-      const int64_t q0 = m * i / G, q1 = m * (i + 1) / G, mi = q1 - q0;
-      if (mi <= 0) return KNN_OK;
-      hipStream_t s = g->ctx[i]->stream;
-      bool ok = hipMemcpyAsync(out_labels + q0, g->olab[i].p, mi * sizeof(int32_t),
-                               hipMemcpyDeviceToHost, s) == hipSuccess;
-      if (out_flags)
-        ok = ok && hipMemcpyAsync(out_flags + q0, g->oflags[i].p, mi * sizeof(int32_t),
-                                  hipMemcpyDeviceToHost, s) == hipSuccess;
-      if (out_idx && k > 0)
-        ok = ok && hipMemcpyAsync(out_idx + q0 * k, g->oidx[i].p, mi * k * sizeof(int64_t),
-                                  hipMemcpyDeviceToHost, s) == hipSuccess;
-      if (out_dist && k > 0)
-        ok = ok && hipMemcpyAsync(out_dist + q0 * k, g->odist[i].p, mi * k * sizeof(double),
-                                  hipMemcpyDeviceToHost, s) == hipSuccess;
-      ok = ok && hipStreamSynchronize(s) == hipSuccess;
-      return ok ? KNN_OK : knn_fail(KNN_ERR_DEVICE, "D2H of labels failed");
-    });
+      if (mi <= 0) {
+        HIP_G(hipEventRecord(g->ev0[i], s));
+        HIP_G(hipEventRecord(g->ev1[i], s));
+        continue;
+      }
+      if ((rc = g->Q[i].ensure((size_t)mi * d * sizeof(double)))) return rc;
+      if ((rc = g->olab[i].ensure((size_t)mi * sizeof(int32_t)))) return rc;
+      if ((rc = g->oflags[i].ensure((size_t)mi * sizeof(int32_t)))) return rc;
+      if ((rc = g->oidx[i].ensure((size_t)mi * std::max(k, 1) * sizeof(int64_t)))) return rc;
+      if ((rc = g->odist[i].ensure((size_t)mi * std::max(k, 1) * sizeof(double)))) return rc;
+      HIP_G(hipMemcpyAsync(g->Q[i].p, Q + q0 * d, (size_t)mi * d * sizeof(double),
+                           hipMemcpyHostToDevice, s));
+      HIP_G(hipEventRecord(g->ev0[i], s));
+      if ((rc = knn_classify_device(g->ctx[i], (const double*)g->Q[i].p, mi, k, metric,
+                                    (int32_t*)g->olab[i].p,
+                                    out_idx ? (int64_t*)g->oidx[i].p : nullptr,
+                                    out_dist ? (double*)g->odist[i].p : nullptr,
+                                    (int32_t*)g->oflags[i].p, s)))
+        return rc;
+      HIP_G(hipEventRecord(g->ev1[i], s));
+    }
+    // the copies back only once every device has its work queued (a copy
+    // into pageable host memory may hold this thread until it completes)
+    for (int i = 0; i < G; i++) {
+      int64_t q0, mi;
+      slice(i, q0, mi);
+      HIP_G(hipSetDevice(g->devs[i]));
+      if (mi > 0 && (rc = d2h(i, q0, mi))) return rc;
+    }
+    return finish();
   }
 
   // ---- train-sharded
@@ -257,29 +290,33 @@ int knn_group_classify(knn_group* g, const double* Q, int64_t m, int32_t k, int3
       for (int64_t q = 0; q < m; q++) out_flags[q] = 0;
     return KNN_OK;
   }
+  // each GPU's exact local top-w (w <= its shard: padded with idx -1); any
+  // K <= N_train like cpp:328 (unions beyond 4096 entries: the rank merge)
   const int w = (int)std::min<int64_t>((int64_t)k + 1, g->n);
-  if ((int64_t)G * w > 4096)  // merge_vote_partials holds the G*w entries of a query in LDS
-    return knn_fail(KNN_ERR_ARG, "train-sharded merge needs ngpus * (k+1) <= 4096");
   const int64_t PB = knnk::packed_part_bytes(m, w);
-  int rc = for_each_dev(g, [&](int i) {
-    int e;
-    if ((e = g->Q[i].ensure((size_t)m * d * sizeof(double)))) return e;
+  for (int i = 0; i < G; i++) {
+    int64_t q0, mi;
+    slice(i, q0, mi);
+    HIP_G(hipSetDevice(g->devs[i]));
+    if ((rc = g->Q[i].ensure((size_t)m * d * sizeof(double)))) return rc;
     // this GPU's lists packed [dist | idx | label] (one all-gather per step)
-    if ((e = g->pk[i].ensure((size_t)PB))) return e;
-    if (G > 1 && (e = g->gk[i].ensure((size_t)G * PB))) return e;
-    if ((e = g->olab[i].ensure((size_t)m * sizeof(int32_t)))) return e;
-    if ((e = g->oflags[i].ensure((size_t)m * sizeof(int32_t)))) return e;
-    if ((e = g->oidx[i].ensure((size_t)m * k * sizeof(int64_t)))) return e;
-    if ((e = g->odist[i].ensure((size_t)m * k * sizeof(double)))) return e;
-    return KNN_OK;
-  });
-  if (rc) return rc;
+    if ((rc = g->pk[i].ensure((size_t)PB))) return rc;
+    if (G > 1 && (rc = g->gk[i].ensure((size_t)G * PB))) return rc;
+    if ((rc = g->olab[i].ensure((size_t)std::max<int64_t>(mi, 1) * sizeof(int32_t)))) return rc;
+    if ((rc = g->oflags[i].ensure((size_t)std::max<int64_t>(mi, 1) * sizeof(int32_t)))) return rc;
+    if ((rc = g->oidx[i].ensure((size_t)std::max<int64_t>(mi, 1) * k * sizeof(int64_t)))) return rc;
+    if ((rc = g->odist[i].ensure((size_t)std::max<int64_t>(mi, 1) * k * sizeof(double)))) return rc;
+    if (const int64_t sb = knnk::merge_scratch_bytes(G, w, k, mi))
+      if ((rc = g->ctx[i]->mrg.ensure((size_t)sb))) return rc;
+  }
   // queries to the first GPU, RCCL broadcast to the rest
   HIP_G(hipSetDevice(g->devs[0]));
   HIP_G(hipMemcpyAsync(g->Q[0].p, Q, (size_t)m * d * sizeof(double), hipMemcpyHostToDevice,
                        g->ctx[0]->stream));
-  HIP_G(hipStreamSynchronize(g->ctx[0]->stream));
-  auto t0 = clk::now();
+  for (int i = 0; i < G; i++) {
+    HIP_G(hipSetDevice(g->devs[i]));
+    HIP_G(hipEventRecord(g->ev0[i], g->ctx[i]->stream));
+  }
   if (G > 1) {
     NCCL_G(ncclGroupStart());
     for (int i = 0; i < G; i++)
@@ -287,13 +324,13 @@ int knn_group_classify(knn_group* g, const double* Q, int64_t m, int32_t k, int3
                            g->ctx[i]->stream));
     NCCL_G(ncclGroupEnd());
   }
-  rc = for_each_dev(g, [&](int i) {
+  for (int i = 0; i < G; i++) {
     unsigned char* pb = (unsigned char*)g->pk[i].p;
-    return knn_search_partial_device(g->ctx[i], (const double*)g->Q[i].p, m, w, metric,
-                                     (double*)pb, (int64_t*)(pb + 8 * m * w),
-                                     (int32_t*)(pb + 16 * m * w), nullptr);
-  });
-  if (rc) return rc;
+    if ((rc = knn_search_partial_device(g->ctx[i], (const double*)g->Q[i].p, m, w, metric,
+                                        (double*)pb, (int64_t*)(pb + 8 * m * w),
+                                        (int32_t*)(pb + 16 * m * w), nullptr)))
+      return rc;
+  }
   if (G > 1) {  // one all-gather of the packed lists (≙ the reference's MPI_Gather, cpp:340)
     NCCL_G(ncclGroupStart());
     for (int i = 0; i < G; i++)
@@ -301,38 +338,27 @@ int knn_group_classify(knn_group* g, const double* Q, int64_t m, int32_t k, int3
                            g->ctx[i]->stream));
     NCCL_G(ncclGroupEnd());
   }
-  rc = for_each_dev(g, [&](int i) {
-    const int64_t q0 = m * i / G, q1 = m * (i + 1) / G, mi = q1 - q0;
-    if (mi <= 0) return KNN_OK;
+  for (int i = 0; i < G; i++) {
+    int64_t q0, mi;
+    slice(i, q0, mi);
+    HIP_G(hipSetDevice(g->devs[i]));
     hipStream_t s = g->ctx[i]->stream;
-    const double* sk = (const double*)(G > 1 ? g->gk[i].p : g->pk[i].p);
-    knnk::launch_merge_vote_partials(sk, nullptr, nullptr, G, m, w, k, (int32_t*)g->olab[i].p,
-                                     (int64_t*)g->oidx[i].p, (double*)g->odist[i].p,
-                                     (int32_t*)g->oflags[i].p, s, q0, mi, PB);
-    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
-      return knn_fail(KNN_ERR_DEVICE, "merge/vote failed");
-    return KNN_OK;
-  });
-  g->last_compute = std::chrono::duration<double>(clk::now() - t0).count();
-  if (rc) return rc;
-  return for_each_dev(g, [&](int i) {
-    const int64_t q0 = m * i / G, q1 = m * (i + 1) / G, mi = q1 - q0;
-    if (mi <= 0) return KNN_OK;
-    hipStream_t s = g->ctx[i]->stream;
-    bool ok = hipMemcpyAsync(out_labels + q0, g->olab[i].p, mi * sizeof(int32_t),
-                             hipMemcpyDeviceToHost, s) == hipSuccess;
-    if (out_flags)
-      ok = ok && hipMemcpyAsync(out_flags + q0, g->oflags[i].p, mi * sizeof(int32_t),
-                                hipMemcpyDeviceToHost, s) == hipSuccess;
-    if (out_idx)
-      ok = ok && hipMemcpyAsync(out_idx + q0 * k, g->oidx[i].p, mi * k * sizeof(int64_t),
-                                hipMemcpyDeviceToHost, s) == hipSuccess;
-    if (out_dist)
-      ok = ok && hipMemcpyAsync(out_dist + q0 * k, g->odist[i].p, mi * k * sizeof(double),
-                                hipMemcpyDeviceToHost, s) == hipSuccess;
-    ok = ok && hipStreamSynchronize(s) == hipSuccess;
-    return ok ? KNN_OK : knn_fail(KNN_ERR_DEVICE, "D2H of labels failed");
-  });
+    if (mi > 0) {
+      const double* sk = (const double*)(G > 1 ? g->gk[i].p : g->pk[i].p);
+      knnk::launch_merge_vote_partials(sk, nullptr, nullptr, G, m, w, k, (int32_t*)g->olab[i].p,
+                                       (int64_t*)g->oidx[i].p, (double*)g->odist[i].p,
+                                       (int32_t*)g->oflags[i].p, s, q0, mi, PB, g->ctx[i]->mrg.p);
+      HIP_G(hipGetLastError());
+    }
+    HIP_G(hipEventRecord(g->ev1[i], s));
+  }
+  for (int i = 0; i < G; i++) {
+    int64_t q0, mi;
+    slice(i, q0, mi);
+    HIP_G(hipSetDevice(g->devs[i]));
+    if (mi > 0 && (rc = d2h(i, q0, mi))) return rc;
+  }
+  return finish();
 }
 
 double knn_group_last_compute_seconds(knn_group* g) { return g ? g->last_compute : -1.0; }

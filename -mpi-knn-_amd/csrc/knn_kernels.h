@@ -168,11 +168,16 @@ struct RescanBufs {
 // error factor of t.DP; full_blocks: workgroups of the full-scan kernel.
 void launch_rescan(int metric, const TrainDev& t, const double* Q64, const RescanBufs& rb, int cap,
                    int W, double f_err, const Sink& sink, int full_blocks, hipStream_t s);
+// k-way merge + vote of [parts][m][w] sorted lists for queries [q0, q0+mq).
+// Unions of up to 4096 entries sort in LDS; larger ones (any k <= n) rank
+// each entry by binary searches and need merge_scratch_bytes() of device
+// scratch (0 when the LDS kernel serves the geometry).
+int64_t merge_scratch_bytes(int parts, int w, int k, int64_t mq);
 void launch_merge_vote_partials(const double* dist, const int64_t* idx, const int32_t* lab,
                                 int parts, int64_t m, int w, int k, int32_t* out_lab,
                                 int64_t* out_idx, double* out_dist, int32_t* out_flags,
                                 hipStream_t s, int64_t q0 = 0, int64_t mq = -1,
-                                int64_t pstride = 0);
+                                int64_t pstride = 0, void* scratch = nullptr);
 // byte stride of one part's packed [dist | idx | label] lists of m x w entries
 inline int64_t packed_part_bytes(int64_t m, int w) { return (m * w * 20 + 15) / 16 * 16; }
 // k beyond kMaxK (knn_select.hip, large_k_kernel): the exact path over every

@@ -55,10 +55,7 @@ void launch_col_mean(const double* X64, int64_t n, int d, double* partial, doubl
 // u64 bits): fixes the operand scale 2^jx before any rounding to fp32.
 // Also counts the non-finite train values (exponent bits all ones: a bit
 // test, this file is built with -fno-honor-nans) into nonfinite[0] --
-// set_train rejects such a train set.
-__device__ __forceinline__ bool nonfinite_bits(double x) {
-  return (__double_as_longlong(x) & 0x7FF0000000000000ll) == 0x7FF0000000000000ll;
-}
+// set_train rejects such a train set (nonfinite_bits: knn_device.h).
 
 __global__ void __launch_bounds__(256)
 absmax_kernel(const double* __restrict__ X64, const double* __restrict__ mu, int64_t n, int d,

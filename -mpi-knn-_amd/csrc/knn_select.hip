@@ -941,7 +941,7 @@ large_k_kernel(TrainDev t, const double* __restrict__ Q64, int64_t m, int W, int
     if (tid == 0) s_bad = 0;
     __syncthreads();
     for (int c = tid; c < d; c += kLkThreads)
-      if (!__builtin_isfinite(qrow[c])) s_bad = 1;
+      if (nonfinite_bits(qrow[c])) s_bad = 1;  // (this TU: -fno-honor-nans)
     __syncthreads();
     if (s_bad) {  // a NaN / inf coordinate: no neighbours (as the merge reports it)
       if (tid < 64) finish_nonfinite(q, sink);
@@ -1200,14 +1200,173 @@ merge_vote_partials_kernel(const double* __restrict__ dist, const int64_t* __res
   }
 }
 
+// ---- the same merge for unions beyond the LDS image (parts * w > 4096:
+// e.g. 8 GPUs at k >= 512; the reference accepts any K <= N_train, cpp:328).
+// No sort at all: the lists are already sorted by (dist, global idx), keys
+// distinct, so entry c of list p lands at merged position
+//   c + sum over the other lists p' of #{entries of p' before it}
+// (one binary search per other list).  Pass 1 scatters the entries that land
+// below k+1 into a per-query scratch row; pass 2 (a kernel boundary later:
+// the row is complete and visible) votes over the first k in order.
+constexpr int kMergeLdsEntries = 4096;  // union size the LDS kernel holds (80 KiB)
+constexpr int kMergeRankThreads = 256;
+constexpr int kVoteLdsClasses = 8192;  // sequential vote with per-class counts in LDS
+
+struct PartLists {
+  const double* dist;
+  const int64_t* idx;
+  const int32_t* lab;
+  int64_t m, pstride;  // pstride > 0: packed parts (see merge_vote_partials_kernel)
+  int w;
+  __device__ __forceinline__ void at(int p, int64_t q, int c, double& v, int64_t& id,
+                                     int32_t& lb) const {
+    if (pstride > 0) {
+      const unsigned char* pb = (const unsigned char*)dist + p * pstride;
+      const int64_t o = q * w + c, mw = m * w;
+      v = ((const double*)pb)[o];
+      id = ((const int64_t*)(pb + 8 * mw))[o];
+      lb = ((const int32_t*)(pb + 16 * mw))[o];
+    } else {
+      const int64_t src = ((int64_t)p * m + q) * w + c;
+      v = dist[src];
+      id = idx[src];
+      lb = lab[src];
+    }
+  }
+};
+
+// scratch row of one query: K1 = k + 1 slots {dist f64 | idx i64 | label i32}
+__host__ __device__ inline int64_t merge_row_bytes(int k) {
+  return ((int64_t)(k + 1) * 20 + 15) / 16 * 16;
+}
+
+__global__ void __launch_bounds__(kMergeRankThreads)
+merge_rank_scatter_kernel(PartLists L, int parts, int k, int64_t q0, int nch,
+                          unsigned char* __restrict__ scratch) {
+  const int64_t qo = blockIdx.x / nch;
+  const int ch = blockIdx.x - (int)(qo * nch);
+  const int64_t q = q0 + qo;
+  const int e = ch * kMergeRankThreads + threadIdx.x;
+  const int w = L.w;
+  if (e >= parts * w) return;
+  const int p = e / w, c = e - p * w;
+  double v;
+  int64_t id;
+  int32_t lb;
+  L.at(p, q, c, v, id, lb);
+  if (id < 0) return;  // padding (short shard, non-finite query): not a neighbour
+  int64_t rank = c;
+  if (rank > k) return;
+  for (int p2 = 0; p2 < parts; ++p2) {
+    if (p2 == p) continue;
+    int lo = 0, hi = w;  // first entry of list p2 not before (v, id)
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      double v2;
+      int64_t id2;
+      int32_t lb2;
+      L.at(p2, q, mid, v2, id2, lb2);
+      // padding (+inf, -1) sorts after every neighbour
+      if (id2 >= 0 && pair_less(v2, id2, v, id)) lo = mid + 1; else hi = mid;
+    }
+    rank += lo;
+    if (rank > k) return;
+  }
+  unsigned char* row = scratch + qo * merge_row_bytes(k);
+  const int K1 = k + 1;
+  ((double*)row)[rank] = v;
+  ((int64_t*)(row + 8 * K1))[rank] = id;
+  ((int32_t*)(row + 16 * K1))[rank] = lb;
+}
+
+__global__ void __launch_bounds__(64)
+merge_rank_vote_kernel(PartLists L, int parts, int k, int64_t q0,
+                       const unsigned char* __restrict__ scratch, Sink sink) {
+  __shared__ int counts[kVoteLdsClasses];
+  const int64_t qo = blockIdx.x, q = q0 + qo;
+  const int lane = threadIdx.x, w = L.w, K1 = k + 1;
+  // valid entries: a prefix of every list
+  int64_t cnt = 0;
+  for (int p = lane; p < parts; p += 64) {
+    int lo = 0, hi = w;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      double v;
+      int64_t id;
+      int32_t lb;
+      L.at(p, q, mid, v, id, lb);
+      if (id >= 0) lo = mid + 1; else hi = mid;
+    }
+    cnt += lo;
+  }
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+  const int kk = (int)min<int64_t>(k, cnt);  // slots [kk, k) are empty: label -1
+  const unsigned char* row = scratch + qo * merge_row_bytes(k);
+  const double* rd = (const double*)row;
+  const int64_t* ri = (const int64_t*)(row + 8 * K1);
+  const int32_t* rl = (const int32_t*)(row + 16 * K1);
+  auto slot_lab = [&](int t) { return t < kk ? rl[t] : -1; };
+  int maxlab = -1;
+  for (int t = lane; t < kk; t += 64) maxlab = max(maxlab, rl[t]);
+  maxlab = wave_max_i(maxlab);
+  int winner = -1;
+  if (maxlab + 2 <= kVoteLdsClasses) {
+    // cpp:324-337 as written: counts per class (slot 0: the empty label -1),
+    // the first label whose count strictly exceeds the running max wins
+    for (int c = lane; c < maxlab + 2; c += 64) counts[c] = 0;
+    __syncthreads();
+    if (lane == 0) {
+      int best = 0;
+      for (int t = 0; t < k; ++t) {
+        const int lb = slot_lab(t);
+        const int c = ++counts[lb + 1];
+        if (c > best) { best = c; winner = lb; }
+      }
+    }
+  } else {
+    // (labels beyond the LDS table) the same rule in parallel: the winner is
+    // the label of the first slot whose running count reaches the final max
+    int bc = 0, bt = INT_MAX;
+    for (int t = lane; t < k; t += 64) {
+      const int lt = slot_lab(t);
+      int c = 0;
+      for (int s2 = 0; s2 <= t; ++s2) c += (slot_lab(s2) == lt);
+      if (c > bc) { bc = c; bt = t; }
+    }
+    const int M = wave_max_i(bc);
+    const int tmin = wave_min_i(bc == M ? bt : INT_MAX);
+    winner = k > 0 ? slot_lab(tmin) : -1;
+  }
+  int tie = 0;
+  for (int t = lane; t + 1 < kk; t += 64)
+    if (rd[t] == rd[t + 1]) tie |= rl[t] != rl[t + 1] ? 4 : 8;
+  tie = wave_or_i(tie);
+  if (lane == 0) {
+    sink.labels[qo] = winner;
+    if (sink.flags) {
+      int f = tie;
+      if (k > 0 && k < cnt && rd[k - 1] == rd[k]) f |= 2;
+      sink.flags[qo] = f;
+    }
+  }
+  for (int t = lane; t < k; t += 64) {
+    if (sink.idx) sink.idx[qo * k + t] = t < kk ? ri[t] : -1;
+    if (sink.dist) sink.dist[qo * k + t] = t < kk ? rd[t] : KNN_INF_D;
+  }
+}
+
+int64_t merge_scratch_bytes(int parts, int w, int k, int64_t mq) {
+  if ((int64_t)parts * w <= kMergeLdsEntries) return 0;  // the LDS kernel needs none
+  return mq * merge_row_bytes(k);
+}
+
 void launch_merge_vote_partials(const double* dist, const int64_t* idx, const int32_t* lab,
                                 int parts, int64_t m, int w, int k, int32_t* out_lab,
                                 int64_t* out_idx, double* out_dist, int32_t* out_flags,
-                                hipStream_t s, int64_t q0, int64_t mq, int64_t pstride) {
+                                hipStream_t s, int64_t q0, int64_t mq, int64_t pstride,
+                                void* scratch) {
   if (mq < 0) mq = m - q0;
   if (mq <= 0) return;
-  int P2 = 1;
-  while (P2 < parts * w) P2 <<= 1;
   Sink sink{};
   sink.mode = MODE_SINGLE;
   sink.k = k;
@@ -1215,6 +1374,18 @@ void launch_merge_vote_partials(const double* dist, const int64_t* idx, const in
   sink.idx = out_idx;
   sink.dist = out_dist;
   sink.flags = out_flags;
+  if ((int64_t)parts * w > kMergeLdsEntries) {
+    const PartLists L{dist, idx, lab, m, pstride, w};
+    const int nch = (parts * w + kMergeRankThreads - 1) / kMergeRankThreads;
+    hipLaunchKernelGGL(merge_rank_scatter_kernel, dim3((unsigned)(mq * nch)),
+                       dim3(kMergeRankThreads), 0, s, L, parts, k, q0, nch,
+                       (unsigned char*)scratch);
+    hipLaunchKernelGGL(merge_rank_vote_kernel, dim3((unsigned)mq), dim3(64), 0, s, L, parts, k,
+                       q0, (const unsigned char*)scratch, sink);
+    return;
+  }
+  int P2 = 1;
+  while (P2 < parts * w) P2 <<= 1;
   const size_t lds = (size_t)P2 * (8 + 8 + 4);
   hipLaunchKernelGGL(merge_vote_partials_kernel, dim3((unsigned)mq), dim3(64), lds, s, dist, idx,
                      lab, parts, m, w, k, P2, q0, pstride, sink);

@@ -28,10 +28,12 @@
  *     unspecified -- such queries are reported in out_flags);
  *   - label = first label whose running count strictly exceeds the running
  *     maximum while scanning the k nearest in order; -1 when k == 0.
- *   - the GPU computes a certified candidate set with fp32 MFMA and re-ranks
- *     it in fp64; queries whose candidate set cannot be certified are
- *     re-run exactly (fp64 over all rows).  No CPU fallback exists: without
- *     a usable HIP device every call fails with KNN_ERR_DEVICE.
+ *   - the GPU computes a certified candidate set on MFMA (by default fp16
+ *     operands on v_mfma_f32_16x16x32_f16; bf16x3 or fp32 by precision mode,
+ *     see knn_set_precision) and re-ranks it in fp64; queries whose
+ *     candidate set cannot be certified are re-run exactly (fp64 over all
+ *     rows).  No CPU fallback exists: without a usable HIP device every call
+ *     fails with KNN_ERR_DEVICE.
  *
  * Conventions: plain pointers and sizes; return 0 on success, a negative
  * KNN_ERR_* code on failure (message via knn_last_error(), thread-local).

@@ -28,3 +28,23 @@ def cout_double(x):
 @pytest.fixture(scope="session")
 def fmt_cout():
     return cout_double
+
+
+def pytest_terminal_summary(terminalreporter):
+    """Exact-tie vote tally of the parity suite (test_gpu_parity.TIE_VOTES)."""
+    mod = sys.modules.get("test_gpu_parity")
+    tv = getattr(mod, "TIE_VOTES", None) if mod else None
+    if not tv or not tv["cases"]:
+        return
+    terminalreporter.write_line(
+        "tie-vote parity: %d cases, %d queries, %d with an exact-tie vote, %d of those with a "
+        "label other than the oracle's std::sort order" %
+        (tv["cases"], tv["queries"], tv["tie_vote"], tv["tie_vote_label_differs"]))
+    try:
+        import json
+        out = os.path.join(ROOT, "gpurun_out")
+        os.makedirs(out, exist_ok=True)
+        with open(os.path.join(out, "tie_votes.json"), "w") as f:
+            json.dump(tv, f)
+    except OSError:
+        pass

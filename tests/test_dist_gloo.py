@@ -69,6 +69,11 @@ def _worker(rank, world, port, mode, out_path):
         el = kd.timed(lambda: None, 3, 1, lambda: None)
         result = dict(labels=full.numpy(), el=np.array([el]))
     else:
+        if mode == "train_bigk":
+            # any K <= N_train like cpp:328: the union of the ranks' lists
+            # (2 x 3001) is beyond the LDS merge's 4096 entries
+            tr, lab, te = _data(n=8000, m=24, d=12)
+            n, m, k = tr.shape[0], te.shape[0], 3000
         w = k + 1
         r0, r1 = kd.shard_range(n, world, rank)
 
@@ -104,15 +109,19 @@ def test_two_rank_normalisation_matches_oracle(tmp_path):
         assert got[name].tobytes() == want.tobytes(), name
 
 
-@pytest.mark.parametrize("mode", ["query", "train"])
+@pytest.mark.parametrize("mode", ["query", "train", "train_bigk"])
 def test_two_rank_decomposition_matches_single_process(mode, tmp_path):
     import sys
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     out = str(tmp_path / "r.npz")
     mp.spawn(_worker, args=(2, _free_port(), mode, out), nprocs=2, join=True)
-    tr, lab, te = _data()
-    want, _, _ = oracle.knn(tr, lab, te, 7, True, 5)
+    if mode == "train_bigk":
+        tr, lab, te = _data(n=8000, m=24, d=12)
+        want, _, _ = oracle.knn(tr, lab, te, 3000, True, 5)
+    else:
+        tr, lab, te = _data()
+        want, _, _ = oracle.knn(tr, lab, te, 7, True, 5)
     got = np.load(out)["labels"]
     np.testing.assert_array_equal(got, want)
 

@@ -122,3 +122,7 @@ def test_cfg4_100m_train_sharded(knn):
     for a, q in enumerate(qs):
         for t in np.nonzero(idx[q] != wi[a])[0]:
             assert (dist[q] == dist[q][t]).sum() > 1, "query %d: index differs without a tie" % q
+    # exact-tie votes (equal distances, different labels in the top k): the
+    # reference cannot run this config (cpp:140 overflows), so there is no
+    # std::sort order to compare with; the count is reported
+    print("cfg4 tie-vote queries: %d of %d" % (int(((of.cpu().numpy() & knn.FLAG_TIE_VOTE) != 0).sum()), m))
