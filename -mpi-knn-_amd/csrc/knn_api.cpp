@@ -503,11 +503,34 @@ static void auto_check(knn_ctx* ctx) {
 
 // Core search: candidate pass + merge/re-rank/certify + the device-driven
 // rescan.  Enqueue only: no host synchronisation on any path.
-int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric, const Sink& sink,
-                   hipStream_t s) {
+// Reference tie order (knn_select.hip, tie_order_kernel): which tied queries
+// get the reference's own std::sort order.  Tuning key "ties": 0 none,
+// 1 (default) those whose label the tie order can change (KNN_FLAG_TIE_VOTE,
+// KNN_FLAG_TIE_BOUNDARY), 2 every query with equal distances in its top k
+// (also KNN_FLAG_TIE_ORDER: neighbour indices in the reference's order).
+static int tie_mask_of(const knn_ctx* ctx, const Sink& sink) {
+  if (sink.mode != MODE_SINGLE) return 0;  // partial lists: ordered by (dist, global idx)
+  return ctx->tune_ties == 0 ? 0 : ctx->tune_ties == 1 ? (2 | 4) : (2 | 4 | 8);
+}
+
+int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
+                   const Sink& sink_in, hipStream_t s) {
   const TrainDev& t = ctx->train;
   int rc;
   auto_check(ctx);
+  Sink sink = sink_in;
+  sink.tie_mask = tie_mask_of(ctx, sink_in);
+  int64_t tie_per = 0;
+  int tie_nwg = 0;
+  if (sink.tie_mask) {
+    // scratch for the reference-order pass: every row's distance per
+    // workgroup, at most ~2 GB in all (tied queries are rare; the pass loops)
+    tie_per = tie_scratch_bytes(t.n, ctx->class_cnt);
+    tie_nwg = (int)std::max<int64_t>(1, std::min<int64_t>(ctx->cu_count, (2ll << 30) / tie_per));
+    if ((rc = ctx->tie_q.ensure((size_t)m * sizeof(int) + 16))) return rc;
+    if ((rc = ctx->tie_ws.ensure((size_t)(tie_per * tie_nwg)))) return rc;
+    sink.tie_q = (int*)ctx->tie_q.p;
+  }
   // candidate-pass flavour: kmetric 4 = L2 via fp16 MFMA, 2/3 = bf16x3, else fp32
   int kmetric = metric, DP = t.DP;
   const float* Xk = t.X32;
@@ -590,6 +613,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   if ((rc = ctx->rescan_q.ensure((size_t)m * sizeof(int) + 16))) return rc;
   if ((rc = ctx->rescan_tau.ensure((size_t)m * sizeof(double) + 16))) return rc;
   if ((rc = ctx->rescan_cnt.ensure(4 * sizeof(int)))) return rc;
+  sink.tie_cnt = (int*)ctx->rescan_cnt.p + 2;  // zeroed with the rescan counts
   if ((rc = ctx->fr_cnt.ensure((size_t)cap * sizeof(int) + 16))) return rc;
   if ((rc = ctx->fr_buf.ensure((size_t)cap * kRescanCap * sizeof(int) + 16))) return rc;
   if ((rc = ctx->fr_q.ensure((size_t)cap * t.DP * sizeof(float) + 16))) return rc;
@@ -693,6 +717,10 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
                 abl ? 0 : (int)std::min<int64_t>(m, ctx->cu_count), s);
   // (without the full-scan launch nothing writes this call's counts)
   if (abl) launch_fill_i32(ctx->d_counts, 2, 0, s);
+  // queries with exact distance ties: the reference's std::sort order
+  if (sink.tie_mask && !abl)
+    launch_tie_order(metric, t, dQ, sink.tie_q, sink.tie_cnt, ctx->class_cnt,
+                     (unsigned char*)ctx->tie_ws.p, tie_per, tie_nwg, sink, s);
   HIP_TRY(hipGetLastError());
   if (tc) HIP_TRY(hipEventRecord(tc->ev[4], s));
   HIP_TRY(hipEventRecord(ctx->done_ev, s));
@@ -708,8 +736,10 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
 // k > kMaxK: the exact large-k path (knn_select.hip, large_k_kernel); the
 // scratch (every row's distance per workgroup) is capped at ~8 GB.
 static int run_large_k(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
-                       const Sink& sink, hipStream_t s) {
+                       const Sink& sink_in, hipStream_t s) {
   const TrainDev& t = ctx->train;
+  Sink sink = sink_in;
+  sink.tie_mask = tie_mask_of(ctx, sink_in);  // resolved inside large_k_kernel
   const int64_t per = large_k_scratch_bytes(t.n, W, ctx->class_cnt);
   const int64_t nwg = std::max<int64_t>(
       1, std::min<int64_t>({m, 2 * (int64_t)ctx->cu_count, (8ll << 30) / per}));
@@ -991,6 +1021,9 @@ int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value) {
   } else if (!strcmp(key, "xhswz")) {
     if (value < 0 || value > 1) return knn_fail(KNN_ERR_ARG, "xhswz must be 0 or 1");
     ctx->tune_xhswz = (int)value;
+  } else if (!strcmp(key, "ties")) {
+    if (value < 0 || value > 2) return knn_fail(KNN_ERR_ARG, "ties must be 0, 1 or 2");
+    ctx->tune_ties = (int)value;
   } else if (!strcmp(key, "gk")) {
     if (value < -1 || value > 16) return knn_fail(KNN_ERR_ARG, "gk must be -1 (auto) .. 16");
     ctx->tune_gk = (int)value;

@@ -52,6 +52,7 @@ struct knn_ctx {
   int tune_gk = -1;            // what the lists publish into gthr (-1 auto, 0 list R-th, 1..16)
   int tune_xhswz = 1;          // fp16 train image chunk swizzle (xh_swz): 1 on, 0 off (A/B)
   int tune_fp16 = -1;          // fp16 candidate pass: -1 auto, 0 off, 1 on
+  int tune_ties = 1;           // reference tie order: 0 off, 1 vote-affecting ties, 2 all ties
   int tune_m16 = -1;           // bf16x3 on the 16x16x32 MFMA layout: -1 auto, 0 off, 1 on
   int last_nw = 0;
   int last_kmetric = -1; // candidate kernel metric of the last search (knn_kernels.h)
@@ -70,6 +71,8 @@ struct knn_ctx {
       fr_q, fr_thr, slow_q, totals, lk;
   // train-sharded merge of unions beyond 4096 entries (rank merge scratch)
   DevBuf mrg;
+  // reference tie order pass: queued queries, per-workgroup scratch
+  DevBuf tie_q, tie_ws;
   // host-API outputs
   DevBuf o_lab, o_idx, o_dist, o_flags;
   // normalisation: per-thread partial max/min, bounds, host-API staging
@@ -78,7 +81,7 @@ struct knn_ctx {
     return {&X64_own, &lab_own, &X32,   &xl2,   &xl1,    &stats,  &XB,       &XS,
             &XH,      &XT16,    &XS16,  &mu,      &mu_part, &Q64, &Q32,    &qvalid, &cand_v,   &cand_i,
             &gthr,    &rescan_q, &rescan_tau, &rescan_cnt, &fr_cnt, &fr_buf, &fr_q, &fr_thr,
-            &slow_q,  &totals,  &lk, &mrg, &o_lab, &o_idx, &o_dist, &o_flags, &nrm_part, &nrm_mm, &nrm_X};
+            &slow_q,  &totals,  &lk, &mrg, &tie_q, &tie_ws, &o_lab, &o_idx, &o_dist, &o_flags, &nrm_part, &nrm_mm, &nrm_X};
   }
 };
 

@@ -91,10 +91,15 @@ __device__ __forceinline__ double exact_dist(const double* __restrict__ q,
   return METRIC == 0 ? __builtin_sqrt(r) : r;  // llvm.sqrt.f64: correctly rounded
 }
 
-// NaN / inf test on the exponent bits: survives -fno-honor-nans (which lets
-// clang fold __builtin_isfinite / isnan to constants), so every TU may use it.
+// NaN / inf test on the exponent bits, usable in every TU.  The bits pass
+// through an empty asm first: LLVM rewrites the plain mask test into an
+// fp-class test (is-inf-or-nan), and under -fno-honor-nans it then drops the
+// NaN half -- measured on the large-k path: a NaN query went through as
+// finite while -inf was caught.
 __device__ __forceinline__ bool nonfinite_bits(double x) {
-  return (__double_as_longlong(x) & 0x7FF0000000000000ll) == 0x7FF0000000000000ll;
+  long long b = __double_as_longlong(x);
+  asm volatile("" : "+v"(b));
+  return (b & 0x7FF0000000000000ll) == 0x7FF0000000000000ll;
 }
 
 template <typename K, typename I>

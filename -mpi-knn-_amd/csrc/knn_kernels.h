@@ -29,6 +29,12 @@ struct Sink {
   double* dist;          // single: [m*k] (nullable); partial: [m*w]
   int32_t* flags;        // single: [m] (nullable)
   int32_t* plab;         // partial: [m*w]
+  // single: queries whose tie bits (KNN_FLAG_TIE_*) intersect tie_mask are
+  // appended to tie_q (count in tie_cnt[0]) for the reference-order pass
+  // (launch_tie_order); tie_mask 0 = off
+  int tie_mask;
+  int* tie_q;
+  int* tie_cnt;
 };
 
 // Train-set side state resident in HBM.
@@ -187,6 +193,15 @@ void launch_large_k(int metric, const TrainDev& t, const double* Q64, int64_t m,
                     int class_cnt, unsigned char* scratch, int64_t per_wg, int nwg,
                     const Sink& sink, hipStream_t s);
 void launch_fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t s);
+// The reference's exact neighbour order on exact distance ties (knn_select.hip,
+// "reference tie order"): libstdc++ std::sort (introsort) emulated over all
+// n exact distances of each listed query, restricted to the ranges that
+// reach the first k positions.  Per workgroup scratch: tie_scratch_bytes.
+constexpr int kFlagTieRef = 32;  // KNN_FLAG_TIE_REF: order resolved as the reference's
+int64_t tie_scratch_bytes(int64_t n, int class_cnt);
+void launch_tie_order(int metric, const TrainDev& t, const double* Q64, const int* tie_q,
+                      const int* tie_cnt, int class_cnt, unsigned char* scratch, int64_t per_wg,
+                      int nwg, const Sink& sink, hipStream_t s);
 // fp64 rows -> [hi(DP) | lo(DP)] bf16 rows of scale*x (candidate metric 2 = L2 via bf16x3)
 // rows of `out` are row_shorts 16-bit words; xl2/xl1 (train only, else null)
 // fill the padded row's seed floats after the 2*DP bf16 payload

@@ -32,11 +32,12 @@ __device__ void finish_single(int64_t q, const double* dk, const int* di, const 
   tie = wave_or_i(tie);
   if (lane == 0) {
     sink.labels[q] = k > 0 ? ls[tmin] : -1;
-    if (sink.flags) {
-      int f = flag0 | tie;
-      if (k > 0 && k < cnt && dk[k - 1] == dk[k]) f |= 2;  // KNN_FLAG_TIE_BOUNDARY
-      sink.flags[q] = f;
-    }
+    int f = flag0 | tie;
+    if (k > 0 && k < cnt && dk[k - 1] == dk[k]) f |= 2;  // KNN_FLAG_TIE_BOUNDARY
+    if (sink.flags) sink.flags[q] = f;
+    // the order among exactly equal distances is the reference's std::sort's:
+    // queue the query for the reference-order pass (tie_order_kernel)
+    if (f & sink.tie_mask) sink.tie_q[atomicAdd(sink.tie_cnt, 1)] = (int)q;
   }
   for (int t = lane; t < k; t += 64) {
     if (sink.idx) sink.idx[q * k + t] = (int64_t)di[t] + idx_off;
@@ -897,6 +898,323 @@ void launch_rescan(int metric, const TrainDev& t, const double* Q64, const Resca
                        rb.cnt, cap, rb.slow_q, W, sink, rb.counts, rb.totals);
 }
 
+// ------------------------------------------------ reference tie order
+// The reference sorts all N_train records {label, dis} of a query with
+// std::sort (cpp:323/366): libstdc++'s introsort, which is not stable -- the
+// order it leaves among EXACTLY equal distances follows from its pivots and
+// swaps over the whole array.  The vote (cpp:324-337) reads the labels in that
+// order, so a query whose top k holds equal distances with different labels
+// (or a tie across the k-th place) can get a different label under any other
+// tie order.  For such queries this pass recomputes every row's exact
+// distance in the reference's fill order (d[j] for j = 0..n-1, cpp:360-365)
+// and runs the libstdc++ (GCC 11, bits/stl_algo.h / stl_heap.h) algorithm
+// itself, restricted to the sub-ranges that can reach the first k positions:
+//   __introsort_loop: while a range holds > 16 records: depth limit 0 ->
+//     heap sort (__partial_sort of the whole range); else median-of-3 of
+//     (first+1, mid, last-1) swapped to first, Hoare-style
+//     __unguarded_partition of [first+1, last) around *first, recurse on the
+//     right part, loop on the left;
+//   __final_insertion_sort: insertion sort (strict <) over the whole array.
+// Every partition leaves left <= pivot <= right, so a record never leaves the
+// range it was partitioned into: ranges starting at or beyond k cannot reach
+// positions < k and are skipped, and the insertion sort over [0, E) -- E the
+// end of the last range that starts below k -- gives positions < k exactly.
+// The partition itself runs in parallel: its left scan stops at the records
+// >= pivot (ascending), its right scan at the records <= pivot (descending);
+// the t-th swap exchanges the t-th of each until they cross (T), and the
+// cut is min(L[T], R[T-1]) (after a swap the left scan also stops at the
+// swapped-in record).  Pairs t < T never share a position, so the swaps are
+// independent.
+constexpr int kTieThreads = 1024;
+constexpr int kTieStack = 64;  // > 2 log2(2^31): one pending left range per depth level
+
+struct RefSortShared {
+  int sc[2 * (kTieThreads / 64) + 2];  // block scan
+  int st_f[kTieStack], st_l[kTieStack], st_d[kTieStack];
+  int sp, cut, T, done, emax;
+  double pv;
+};
+
+// Exclusive prefix of a and inclusive prefix of b over the threads (in
+// thread order), and their totals.  All threads; sh is reused on return.
+__device__ void block_scan2(int a, int b, int& a_ex, int& b_in, int& a_tot, int& b_tot, int* sh) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  int ai = a, bi = b;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int x = __shfl_up(ai, o, 64), y = __shfl_up(bi, o, 64);
+    if (lane >= o) { ai += x; bi += y; }
+  }
+  if (lane == 63) { sh[wv] = ai; sh[nw + wv] = bi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int sa = 0, sb = 0;
+    for (int w = 0; w < nw; ++w) {
+      const int ta = sh[w], tb = sh[nw + w];
+      sh[w] = sa; sh[nw + w] = sb;
+      sa += ta; sb += tb;
+    }
+    sh[2 * nw] = sa; sh[2 * nw + 1] = sb;
+  }
+  __syncthreads();
+  a_ex = sh[wv] + ai - a;
+  b_in = sh[nw + wv] + bi;
+  a_tot = sh[2 * nw];
+  b_tot = sh[2 * nw + 1];
+  __syncthreads();
+}
+
+__device__ __forceinline__ void rec_swap(double* D, int* P, int a, int b) {
+  const double t = D[a]; D[a] = D[b]; D[b] = t;
+  const int p = P[a]; P[a] = P[b]; P[b] = p;
+}
+
+// std::__unguarded_partition_pivot on [f, l) (l - f > 16); returns the cut.
+__device__ int ref_partition(double* D, int* P, int* Lb, int* Rb, int f, int l, RefSortShared& s) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  if (tid == 0) {  // __move_median_to_first(first, first + 1, mid, last - 1)
+    const int a = f + 1, b = f + (l - f) / 2, c = l - 1;
+    const double da = D[a], db = D[b], dc = D[c];
+    int m;
+    if (da < db) m = db < dc ? b : (da < dc ? c : a);
+    else m = da < dc ? a : (db < dc ? c : b);
+    rec_swap(D, P, f, m);
+    s.pv = D[f];
+  }
+  __syncthreads();
+  const double pv = s.pv;
+  const int seg = (l - f + nt - 1) / nt;
+  const int a0 = min(l, f + tid * seg), a1 = min(l, a0 + seg);
+  int cg = 0, ce = 0;
+  for (int i = a0; i < a1; ++i) {
+    const double v = D[i];
+    cg += i > f && !(v < pv);  // left scan stops: !(*first < pivot)
+    ce += !(pv < v);           // right scan stops: !(pivot < *last)
+  }
+  int g_ex, e_in, g_tot, e_tot;
+  block_scan2(cg, ce, g_ex, e_in, g_tot, e_tot, s.sc);
+  for (int i = a0, r = g_ex; i < a1; ++i)
+    if (i > f && !(D[i] < pv)) Lb[r++] = i;
+  for (int i = a1 - 1, r = e_tot - e_in; i >= a0; --i)  // right stops in descending order
+    if (!(pv < D[i])) Rb[r++] = i;
+  __syncthreads();
+  if (tid == 0) {
+    int lo = 0, hi = min(g_tot, e_tot);  // first t with L[t] >= R[t] (monotone)
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (Lb[mid] >= Rb[mid]) hi = mid; else lo = mid + 1;
+    }
+    const int LT = lo < g_tot ? Lb[lo] : l;
+    s.T = lo;
+    s.cut = lo == 0 ? LT : min(LT, Rb[lo - 1]);
+  }
+  __syncthreads();
+  const int T = s.T;
+  for (int t = tid; t < T; t += nt) rec_swap(D, P, Lb[t], Rb[t]);
+  __syncthreads();
+  return s.cut;
+}
+
+// std::__adjust_heap / __push_heap over records [f, f + len) (one thread)
+__device__ void ref_adjust_heap(double* D, int* P, int f, int hole, int len, double v, int pv) {
+  const int top = hole;
+  int sc = hole;
+  while (sc < (len - 1) / 2) {
+    sc = 2 * (sc + 1);
+    if (D[f + sc] < D[f + sc - 1]) sc--;
+    D[f + hole] = D[f + sc]; P[f + hole] = P[f + sc];
+    hole = sc;
+  }
+  if ((len & 1) == 0 && sc == (len - 2) / 2) {
+    sc = 2 * (sc + 1);
+    D[f + hole] = D[f + sc - 1]; P[f + hole] = P[f + sc - 1];
+    hole = sc - 1;
+  }
+  int parent = (hole - 1) / 2;
+  while (hole > top && D[f + parent] < v) {
+    D[f + hole] = D[f + parent]; P[f + hole] = P[f + parent];
+    hole = parent;
+    parent = (hole - 1) / 2;
+  }
+  D[f + hole] = v; P[f + hole] = pv;
+}
+
+// std::__partial_sort(first, last, last): __make_heap + __sort_heap (one thread)
+__device__ void ref_heap_sort(double* D, int* P, int f, int l) {
+  const int len = l - f;
+  if (len >= 2)
+    for (int parent = (len - 2) / 2;; --parent) {
+      ref_adjust_heap(D, P, f, parent, len, D[f + parent], P[f + parent]);
+      if (parent == 0) break;
+    }
+  for (int last = len; last > 1;) {  // __pop_heap(first, last, last)
+    --last;
+    const double v = D[f + last];
+    const int pv = P[f + last];
+    D[f + last] = D[f]; P[f + last] = P[f];
+    ref_adjust_heap(D, P, f, 0, last, v, pv);
+  }
+}
+
+// std::sort of records (D[j], P[j]), j < n, by D, as libstdc++ leaves
+// positions [0, k) (above).  All threads of the block.
+__device__ void ref_sort_prefix(double* D, int* P, int* Lb, int* Rb, int n, int k,
+                                RefSortShared& s) {
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    s.sp = 0;
+    s.emax = 0;
+  }
+  int f = 0, l = n, dl = n > 1 ? 2 * (31 - __clz(n)) : 0;  // std::__lg(n) * 2
+  __syncthreads();
+  while (true) {
+    if (l - f > 16 && f < k) {
+      if (dl == 0) {
+        if (tid == 0) {
+          ref_heap_sort(D, P, f, l);
+          s.emax = max(s.emax, l);
+        }
+        __syncthreads();
+      } else {
+        --dl;
+        const int cut = ref_partition(D, P, Lb, Rb, f, l, s);
+        // recurse on the right part first (as __introsort_loop), keep the left
+        if (tid == 0) {
+          s.st_f[s.sp] = f; s.st_l[s.sp] = cut; s.st_d[s.sp] = dl;
+          ++s.sp;
+        }
+        f = cut;
+        continue;
+      }
+    } else if (f < k && tid == 0) {
+      s.emax = max(s.emax, l);  // a range left to the final insertion sort
+    }
+    __syncthreads();
+    if (tid == 0) {
+      s.done = s.sp == 0;
+      if (!s.done) --s.sp;
+    }
+    __syncthreads();
+    if (s.done) break;
+    f = s.st_f[s.sp]; l = s.st_l[s.sp]; dl = s.st_d[s.sp];
+    __syncthreads();
+  }
+  if (tid == 0) {  // __final_insertion_sort, positions [0, emax)
+    const int e = min(n, s.emax);
+    for (int i = 1; i < e; ++i) {
+      const double v = D[i];
+      const int p = P[i];
+      int j = i;
+      for (; j > 0 && v < D[j - 1]; --j) { D[j] = D[j - 1]; P[j] = P[j - 1]; }
+      D[j] = v; P[j] = p;
+    }
+  }
+  __syncthreads();
+}
+
+// Every row's exact distance to qrow (reference operation order, as
+// rescan_full) into D[0..n): per-wave staged 64-B row pieces.  All threads.
+template <int METRIC>
+__device__ void exact_all_dist(const TrainDev& t, const double* qrow, double* D, double* tb) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nt = blockDim.x;
+  const int d = t.d;
+  const int64_t n = t.n;
+  for (int64_t s0 = 0; s0 < n; s0 += nt) {
+    const int64_t r0 = s0 + wv * 64;
+    const int nr = (int)max((int64_t)0, min((int64_t)64, n - r0));
+    double r = 0.0;
+    for (int c0 = 0; c0 < d && nr > 0; c0 += kFullDC) {
+      const int nd = min(kFullDC, d - c0);
+#pragma unroll
+      for (int i = 0; i < kFullDC; ++i) {
+        const int e = lane + 64 * i, rr = e / kFullDC, j = e % kFullDC;
+        double val = 0.0;
+        if (rr < nr && j < nd) {
+          const double tq = qrow[c0 + j] - t.X64[(r0 + rr) * d + c0 + j];
+          val = METRIC == 0 ? tq * tq : __builtin_fabs(tq);
+        }
+        tb[rr * (kFullDC + 1) + j] = val;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      if (lane < nr) {
+        const double* row = tb + lane * (kFullDC + 1);
+        for (int j = 0; j < nd; ++j) r = r + row[j];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (lane < nr) D[r0 + lane] = METRIC == 0 ? __builtin_sqrt(r) : r;
+  }
+}
+
+// Outputs of a query whose first k records are in reference order: the
+// vote exactly as cpp:324-337 (sequential, per-class counts in `cnt`),
+// idx / dist, flags |= KNN_FLAG_TIE_REF.  All threads.
+__device__ void ref_finish(int64_t q, const double* D, const int* P, int k, const TrainDev& t,
+                           int class_cnt, int* cnt, const Sink& sink) {
+  const int tid = threadIdx.x;
+  for (int c = tid; c < class_cnt; c += blockDim.x) cnt[c] = 0;
+  __syncthreads();
+  if (tid == 0) {
+    int best = 0, lab = -1;
+    for (int i = 0; i < k; ++i) {
+      const int lb = t.lab[P[i]];
+      const int c = ++cnt[lb];
+      if (c > best) { best = c; lab = lb; }
+    }
+    sink.labels[q] = lab;
+    if (sink.flags) sink.flags[q] |= kFlagTieRef;
+  }
+  for (int i = tid; i < k; i += blockDim.x) {
+    if (sink.idx) sink.idx[q * k + i] = (int64_t)P[i] + sink.idx_off;
+    if (sink.dist) sink.dist[q * k + i] = D[i];
+  }
+  __syncthreads();
+}
+
+// per workgroup: D[n] f64 | P[n] | Lb[n] | Rb[n] | class counts
+int64_t tie_scratch_bytes(int64_t n, int class_cnt) {
+  return (n * 20 + (int64_t)class_cnt * 4 + 255) / 256 * 256;
+}
+
+template <int METRIC>
+__global__ void __launch_bounds__(kTieThreads)
+tie_order_kernel(TrainDev t, const double* __restrict__ Q64, const int* __restrict__ tie_q,
+                 const int* __restrict__ tie_cnt, int class_cnt, unsigned char* __restrict__ scratch,
+                 int64_t per_wg, Sink sink) {
+  __shared__ double tiles[kTieThreads / 64][64 * (kFullDC + 1)];
+  __shared__ RefSortShared s;
+  const int count = *tie_cnt;
+  const int64_t n = t.n;
+  unsigned char* base = scratch + (int64_t)blockIdx.x * per_wg;
+  double* D = (double*)base;
+  int* P = (int*)(D + n);
+  int* Lb = P + n;
+  int* Rb = Lb + n;
+  int* cnt = Rb + n;
+  for (int i = blockIdx.x; i < count; i += gridDim.x) {
+    const int64_t q = tie_q[i];
+    exact_all_dist<METRIC>(t, Q64 + q * t.d, D, tiles[threadIdx.x >> 6]);
+    for (int64_t j = threadIdx.x; j < n; j += kTieThreads) P[j] = (int)j;
+    __syncthreads();
+    ref_sort_prefix(D, P, Lb, Rb, (int)n, sink.k, s);
+    ref_finish(q, D, P, sink.k, t, class_cnt, cnt, sink);
+  }
+}
+
+void launch_tie_order(int metric, const TrainDev& t, const double* Q64, const int* tie_q,
+                      const int* tie_cnt, int class_cnt, unsigned char* scratch, int64_t per_wg,
+                      int nwg, const Sink& sink, hipStream_t s) {
+  if (nwg <= 0) return;
+  if (metric == 0)
+    hipLaunchKernelGGL(tie_order_kernel<0>, dim3(nwg), dim3(kTieThreads), 0, s, t, Q64, tie_q,
+                       tie_cnt, class_cnt, scratch, per_wg, sink);
+  else
+    hipLaunchKernelGGL(tie_order_kernel<1>, dim3(nwg), dim3(kTieThreads), 0, s, t, Q64, tie_q,
+                       tie_cnt, class_cnt, scratch, per_wg, sink);
+}
+
 // ------------------------------------------------ large k (k > kMaxK)
 // The candidate lists hold at most kMaxUnion entries, so a k beyond kMaxK
 // (the reference accepts any K <= N_train, cpp:328) runs this exact path
@@ -934,6 +1252,11 @@ large_k_kernel(TrainDev t, const double* __restrict__ Q64, int64_t m, int W, int
   int* oi = (int*)(od + W2);                       // [W2]
   int* ol = oi + W2;                               // [W2] labels in sorted order
   int* cnt = ol + W2;                              // [class_cnt] vote counts
+  int* P = cnt + (class_cnt + 1) / 2 * 2;          // [n] reference-order pass (tie_mask)
+  int* Lb = P + n;                                 // [n]
+  int* Rb = Lb + n;                                // [n]
+  __shared__ RefSortShared rs;
+  __shared__ int s_flags;
   double* tb = tiles[wv];
   for (int64_t q = blockIdx.x; q < m; q += gridDim.x) {
     const double* qrow = Q64 + q * d;
@@ -948,33 +1271,7 @@ large_k_kernel(TrainDev t, const double* __restrict__ Q64, int64_t m, int W, int
       continue;
     }
     // 1. exact distances
-    for (int64_t s0 = 0; s0 < n; s0 += kLkThreads) {
-      const int64_t r0 = s0 + wv * 64;
-      const int nr = (int)max((int64_t)0, min((int64_t)64, n - r0));
-      double r = 0.0;
-      for (int c0 = 0; c0 < d && nr > 0; c0 += kFullDC) {
-        const int nd = min(kFullDC, d - c0);
-#pragma unroll
-        for (int i = 0; i < kFullDC; ++i) {
-          const int e = lane + 64 * i, rr = e / kFullDC, j = e % kFullDC;
-          double val = 0.0;
-          if (rr < nr && j < nd) {
-            const double tq = qrow[c0 + j] - t.X64[(r0 + rr) * d + c0 + j];
-            val = METRIC == 0 ? tq * tq : __builtin_fabs(tq);
-          }
-          tb[rr * (kFullDC + 1) + j] = val;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        if (lane < nr) {
-          const double* row = tb + lane * (kFullDC + 1);
-          for (int j = 0; j < nd; ++j) r = r + row[j];
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-      }
-      if (lane < nr) D[r0 + lane] = METRIC == 0 ? __builtin_sqrt(r) : r;
-    }
+    exact_all_dist<METRIC>(t, qrow, D, tb);
     // 2. radix select of the W-th smallest key (digits from the top)
     if (tid == 0) {
       s_prefix = 0;
@@ -1067,14 +1364,24 @@ large_k_kernel(TrainDev t, const double* __restrict__ Q64, int64_t m, int W, int
         if (od[i] == od[i + 1]) tie |= ol[i] != ol[i + 1] ? 4 : 8;
       if (tie) atomicOr(&s_bad, tie);  // s_bad is 0 here: reused for the flags
       __syncthreads();
-      if (tid == 0 && sink.flags) {
+      if (tid == 0) {
         int f = s_bad;
         if (k < W && od[k - 1] == od[k]) f |= 2;  // KNN_FLAG_TIE_BOUNDARY
-        sink.flags[q] = f;
+        if (sink.flags) sink.flags[q] = f;
+        s_flags = f;
       }
       for (int i = tid; i < k; i += kLkThreads) {
         if (sink.idx) sink.idx[q * k + i] = (int64_t)oi[i] + sink.idx_off;
         if (sink.dist) sink.dist[q * k + i] = od[i];
+      }
+      __syncthreads();
+      if (s_flags & sink.tie_mask) {
+        // exact ties: the reference's std::sort order (D still holds every
+        // row's distance in fill order)
+        for (int64_t j = tid; j < n; j += kLkThreads) P[j] = (int)j;
+        __syncthreads();
+        ref_sort_prefix(D, P, Lb, Rb, (int)n, k, rs);
+        ref_finish(q, D, P, k, t, class_cnt, cnt, sink);
       }
     } else {
       for (int i = tid; i < sink.w; i += kLkThreads) {
@@ -1090,7 +1397,7 @@ large_k_kernel(TrainDev t, const double* __restrict__ Q64, int64_t m, int W, int
 int64_t large_k_scratch_bytes(int64_t n, int W, int class_cnt) {
   int64_t W2 = 1;
   while (W2 < W) W2 <<= 1;
-  return ((n * 8 + W2 * 16 + (int64_t)class_cnt * 4) + 255) / 256 * 256;
+  return ((n * 8 + W2 * 16 + (int64_t)(class_cnt + 1) / 2 * 8 + n * 12) + 255) / 256 * 256;
 }
 
 void launch_large_k(int metric, const TrainDev& t, const double* Q64, int64_t m, int W,

@@ -27,7 +27,7 @@ DRIVER_PATH = os.path.join(HERE, "bin", "knn_mpi_amd")
 
 L2, L1 = 0, 1
 FLAG_EXACT_RESCAN, FLAG_TIE_BOUNDARY, FLAG_TIE_VOTE, FLAG_TIE_ORDER = 1, 2, 4, 8
-FLAG_NONFINITE = 16
+FLAG_NONFINITE, FLAG_TIE_REF = 16, 32
 EXPORTED = (
     "knn_version", "knn_last_error", "knn_device_count", "knn_create", "knn_destroy",
     "knn_set_train", "knn_set_train_device", "knn_classify", "knn_classify_device",

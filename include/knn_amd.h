@@ -23,9 +23,13 @@
  *   - distances are the reference's fp64 values: sqrt of the sequential
  *     sum of (q_i - x_i)^2 (no FMA) for metric 0, sum of |q_i - x_i| for
  *     metric 1;
- *   - neighbours are ordered by ascending distance; exact distance ties are
- *     ordered by train index (the reference's std::sort leaves tie order
- *     unspecified -- such queries are reported in out_flags);
+ *   - neighbours are ordered by ascending distance.  Among exactly equal
+ *     distances the reference's order is whatever its std::sort (libstdc++
+ *     introsort) leaves; queries where that order can change the label
+ *     (KNN_FLAG_TIE_VOTE / KNN_FLAG_TIE_BOUNDARY) are re-ordered exactly as
+ *     the reference's std::sort orders them (KNN_FLAG_TIE_REF), other ties
+ *     are ordered by train index (KNN_FLAG_TIE_ORDER; tuning key "ties" = 2
+ *     re-orders those too);
  *   - label = first label whose running count strictly exceeds the running
  *     maximum while scanning the k nearest in order; -1 when k == 0.
  *   - the GPU computes a certified candidate set on MFMA (by default fp16
@@ -72,6 +76,10 @@ extern "C" {
 #define KNN_FLAG_NONFINITE 16   /* the query has a NaN / inf coordinate: label -1, no
                                    neighbours (idx -1, dist NaN); the reference's
                                    distances are undefined there */
+#define KNN_FLAG_TIE_REF 32     /* a tied query re-ordered as the reference's std::sort
+                                   orders it (libstdc++ introsort emulated over all
+                                   n distances): label, indices and their order are
+                                   the reference's (knn_set_tuning "ties") */
 
 typedef struct knn_ctx knn_ctx;
 typedef struct knn_group knn_group;
@@ -207,7 +215,9 @@ const char* knn_last_kernel_name(knn_ctx* ctx);
  * off, 1 on), "s3q" (the fp16 d > 256 kernel on 16x16x32: 0 off, 1 on) and
  * "gk" (what the global threshold exchange publishes: 0 the lists' R-th
  * entries (resident kernel) / no exchange (S3), K = 1..16 the K-th smallest
- * of a workgroup's union of a query's lists; results stay exact). */
+ * of a workgroup's union of a query's lists; results stay exact); "ties"
+ * (the reference's std::sort order for tied queries: 0 off, 1 (default) the
+ * queries whose label it can change, 2 every query with a tie in its top k). */
 int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value);
 
 /* Synchronise the context's stream. */

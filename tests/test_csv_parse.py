@@ -91,3 +91,23 @@ def test_test_file_format_and_bounds(reader, tmp_path):
     assert n == wn == 300 * 5
     assert got.tobytes() == want.tobytes()
     assert got.tobytes() == X[:250].tobytes()
+
+
+def test_bench_grid_csv_roundtrip(reader, tmp_path):
+    """bench.py's drop-in inputs (8-bit grid values k/256 in the reference's
+    train / test CSV formats) read back exactly by the driver's reader."""
+    import bench
+    rng = np.random.default_rng(8)
+    codes = rng.integers(0, 256, (1000, 24)).astype(np.uint8)
+    lab = rng.integers(0, 10, 1000).astype(np.int32)
+    for labels in (lab, None):
+        p = tmp_path / ("tr.csv" if labels is not None else "te.csv")
+        bench.write_grid_csv(str(p), codes, labels, chunk=300)
+        data = np.empty((1000, 24))
+        got_l = np.empty(1000, np.int32)
+        n = reader.csv_read(str(p).encode(), 24, int(labels is not None), 1000, data.ctypes.data,
+                            got_l.ctypes.data if labels is not None else None, 4)
+        assert n == 1000 * (24 + (labels is not None))
+        assert data.tobytes() == (codes.astype(np.float64) / 256.0).tobytes()
+        if labels is not None:
+            np.testing.assert_array_equal(got_l, lab)

@@ -157,3 +157,13 @@ def test_bench_launches_its_own_ranks():
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2
     assert two["dry_run"] and two["value"] is None
     assert two["labels_sha1"] == one["labels_sha1"]
+    # the N>1 line's extra legs are wired: the native drop-in through
+    # knn_group in both modes (commands only on CPU) and the train-sharded
+    # decomposition (labels equal the query-sharded run's)
+    assert "--gpus 2 --mode query" in two["group_query"]["cmd"]
+    assert "--gpus 2 --mode train" in two["group_train"]["cmd"]
+    assert "--Normalize true" in two["group_train"]["cmd"]
+    assert two["group_query"]["value"] is None and two["train_sharded"]["value"] is None
+    assert sorted(two["dropin_inputs"]) == ["mnist_test.csv", "mnist_train.csv",
+                                            "mnist_validation.csv"]
+    assert two["train_sharded"]["labels_match"] and one["train_sharded"]["labels_match"]

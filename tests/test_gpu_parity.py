@@ -94,6 +94,13 @@ def run_case(clf, knn, train, lab, queries, k, metric, classes):
     tie_vote = (flags & knn.FLAG_TIE_VOTE) != 0
     assert (got[~tie_vote] == want[~tie_vote]).all(), "labels differ on untied queries"
     differs = int((got[tie_vote] != want[tie_vote]).sum())
+    # queries re-ordered as the reference's std::sort (every TIE_VOTE /
+    # TIE_BOUNDARY query by default): the same label and the same neighbour
+    # order as the oracle, index for index
+    ref = (flags & knn.FLAG_TIE_REF) != 0
+    assert (ref == ((flags & (knn.FLAG_TIE_VOTE | knn.FLAG_TIE_BOUNDARY)) != 0)).all()
+    np.testing.assert_array_equal(got[ref], want[ref])
+    np.testing.assert_array_equal(idx[ref], widx[ref])
     TIE_VOTES["cases"] += 1
     TIE_VOTES["queries"] += int(len(got))
     TIE_VOTES["tie_vote"] += int(tie_vote.sum())
@@ -102,6 +109,7 @@ def run_case(clf, knn, train, lab, queries, k, metric, classes):
         TIE_VOTES["where"].append(dict(n=int(train.shape[0]), m=int(len(got)), d=int(train.shape[1]),
                                        k=int(k), metric=int(metric), differs=differs))
     assert_neighbors_match(idx, dist, widx, wdist, flags)
+    assert differs == 0, "%d exact-tie votes differ from the reference order" % differs
     return got, want, flags
 
 
