@@ -739,16 +739,31 @@ static int run_large_k(knn_ctx* ctx, const double* dQ, int64_t m, int W, int met
                        const Sink& sink_in, hipStream_t s) {
   const TrainDev& t = ctx->train;
   Sink sink = sink_in;
-  sink.tie_mask = tie_mask_of(ctx, sink_in);  // resolved inside large_k_kernel
+  sink.tie_mask = tie_mask_of(ctx, sink_in);
+  int rc;
+  int64_t tie_per = 0;
+  int tie_nwg = 0;
+  if (sink.tie_mask) {  // tied queries: queued by large_k_kernel for the reference-order pass
+    tie_per = tie_scratch_bytes(t.n, ctx->class_cnt);
+    tie_nwg = (int)std::max<int64_t>(1, std::min<int64_t>(ctx->cu_count, (2ll << 30) / tie_per));
+    if ((rc = ctx->tie_q.ensure((size_t)m * sizeof(int) + 16))) return rc;
+    if ((rc = ctx->tie_ws.ensure((size_t)(tie_per * tie_nwg)))) return rc;
+    if ((rc = ctx->rescan_cnt.ensure(4 * sizeof(int)))) return rc;
+    sink.tie_q = (int*)ctx->tie_q.p;
+    sink.tie_cnt = (int*)ctx->rescan_cnt.p + 2;
+    HIP_TRY(hipMemsetAsync(sink.tie_cnt, 0, sizeof(int), s));
+  }
   const int64_t per = large_k_scratch_bytes(t.n, W, ctx->class_cnt);
   const int64_t nwg = std::max<int64_t>(
       1, std::min<int64_t>({m, 2 * (int64_t)ctx->cu_count, (8ll << 30) / per}));
-  int rc;
   if ((rc = ctx->lk.ensure((size_t)(per * nwg)))) return rc;
   snprintf(ctx->last_kernel, sizeof ctx->last_kernel, "large_k_kernel<%d>", metric);
   ctx->last_kmetric = -1;
   launch_large_k(metric, t, dQ, m, W, ctx->class_cnt, (unsigned char*)ctx->lk.p, per, (int)nwg,
                  sink, s);
+  if (sink.tie_mask)
+    launch_tie_order(metric, t, dQ, sink.tie_q, sink.tie_cnt, ctx->class_cnt,
+                     (unsigned char*)ctx->tie_ws.p, tie_per, tie_nwg, sink, s);
   launch_fill_i32(ctx->d_counts, 2, 0, s);  // exact path: no query fails certification
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(ctx->done_ev, s));

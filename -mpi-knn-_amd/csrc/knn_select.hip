@@ -1252,10 +1252,6 @@ large_k_kernel(TrainDev t, const double* __restrict__ Q64, int64_t m, int W, int
   int* oi = (int*)(od + W2);                       // [W2]
   int* ol = oi + W2;                               // [W2] labels in sorted order
   int* cnt = ol + W2;                              // [class_cnt] vote counts
-  int* P = cnt + (class_cnt + 1) / 2 * 2;          // [n] reference-order pass (tie_mask)
-  int* Lb = P + n;                                 // [n]
-  int* Rb = Lb + n;                                // [n]
-  __shared__ RefSortShared rs;
   __shared__ int s_flags;
   double* tb = tiles[wv];
   for (int64_t q = blockIdx.x; q < m; q += gridDim.x) {
@@ -1374,15 +1370,8 @@ large_k_kernel(TrainDev t, const double* __restrict__ Q64, int64_t m, int W, int
         if (sink.idx) sink.idx[q * k + i] = (int64_t)oi[i] + sink.idx_off;
         if (sink.dist) sink.dist[q * k + i] = od[i];
       }
-      __syncthreads();
-      if (s_flags & sink.tie_mask) {
-        // exact ties: the reference's std::sort order (D still holds every
-        // row's distance in fill order)
-        for (int64_t j = tid; j < n; j += kLkThreads) P[j] = (int)j;
-        __syncthreads();
-        ref_sort_prefix(D, P, Lb, Rb, (int)n, k, rs);
-        ref_finish(q, D, P, k, t, class_cnt, cnt, sink);
-      }
+      // exact ties: queued for the reference-order pass (tie_order_kernel)
+      if (tid == 0 && (s_flags & sink.tie_mask)) sink.tie_q[atomicAdd(sink.tie_cnt, 1)] = (int)q;
     } else {
       for (int i = tid; i < sink.w; i += kLkThreads) {
         const bool ok = i < W;
@@ -1397,7 +1386,7 @@ large_k_kernel(TrainDev t, const double* __restrict__ Q64, int64_t m, int W, int
 int64_t large_k_scratch_bytes(int64_t n, int W, int class_cnt) {
   int64_t W2 = 1;
   while (W2 < W) W2 <<= 1;
-  return ((n * 8 + W2 * 16 + (int64_t)(class_cnt + 1) / 2 * 8 + n * 12) + 255) / 256 * 256;
+  return ((n * 8 + W2 * 16 + (int64_t)class_cnt * 4) + 255) / 256 * 256;
 }
 
 void launch_large_k(int metric, const TrainDev& t, const double* Q64, int64_t m, int W,
