@@ -98,8 +98,8 @@ int knn_create(knn_ctx** out, int device) {
   if (hipHostMalloc((void**)&c->h_counts, sizeof(int) * 4, hipHostMallocMapped) != hipSuccess ||
       hipHostGetDevicePointer((void**)&c->d_counts, c->h_counts, 0) != hipSuccess ||
       hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming) != hipSuccess ||
-      c->totals.ensure(2 * sizeof(unsigned long long)) != KNN_OK ||
-      hipMemset(c->totals.p, 0, 2 * sizeof(unsigned long long)) != hipSuccess) {
+      c->totals.ensure(3 * sizeof(unsigned long long)) != KNN_OK ||
+      hipMemset(c->totals.p, 0, 3 * sizeof(unsigned long long)) != hipSuccess) {
     knn_destroy(c);
     return knn_fail(KNN_ERR_DEVICE, "context setup (pinned counters / events) failed");
   }
@@ -505,12 +505,14 @@ static void auto_check(knn_ctx* ctx) {
 // rescan.  Enqueue only: no host synchronisation on any path.
 // Reference tie order (knn_select.hip, tie_order_kernel): which tied queries
 // get the reference's own std::sort order.  Tuning key "ties": 0 none,
-// 1 (default) those whose label the tie order can change (KNN_FLAG_TIE_VOTE,
-// KNN_FLAG_TIE_BOUNDARY), 2 every query with equal distances in its top k
-// (also KNN_FLAG_TIE_ORDER: neighbour indices in the reference's order).
+// 1 (default) those whose label the tie order could change (equal distances
+// with different labels where two classes share the top count, or a tie
+// across the k-th place within reach of the runner-up: finish_single),
+// 2 every query with equal distances in its top k (neighbour indices in the
+// reference's order too).
 static int tie_mask_of(const knn_ctx* ctx, const Sink& sink) {
   if (sink.mode != MODE_SINGLE) return 0;  // partial lists: ordered by (dist, global idx)
-  return ctx->tune_ties == 0 ? 0 : ctx->tune_ties == 1 ? (2 | 4) : (2 | 4 | 8);
+  return ctx->tune_ties;
 }
 
 int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
@@ -519,10 +521,10 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   int rc;
   auto_check(ctx);
   Sink sink = sink_in;
-  sink.tie_mask = tie_mask_of(ctx, sink_in);
+  sink.tie_mode = tie_mask_of(ctx, sink_in);
   int64_t tie_per = 0;
   int tie_nwg = 0;
-  if (sink.tie_mask) {
+  if (sink.tie_mode) {
     // scratch for the reference-order pass: every row's distance per
     // workgroup, at most ~2 GB in all (tied queries are rare; the pass loops)
     tie_per = tie_scratch_bytes(t.n, ctx->class_cnt);
@@ -718,9 +720,10 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   // (without the full-scan launch nothing writes this call's counts)
   if (abl) launch_fill_i32(ctx->d_counts, 2, 0, s);
   // queries with exact distance ties: the reference's std::sort order
-  if (sink.tie_mask && !abl)
+  if (sink.tie_mode && !abl)
     launch_tie_order(metric, t, dQ, sink.tie_q, sink.tie_cnt, ctx->class_cnt,
-                     (unsigned char*)ctx->tie_ws.p, tie_per, tie_nwg, sink, s);
+                     (unsigned char*)ctx->tie_ws.p, tie_per, tie_nwg, sink,
+                     (unsigned long long*)ctx->totals.p + 2, s);
   HIP_TRY(hipGetLastError());
   if (tc) HIP_TRY(hipEventRecord(tc->ev[4], s));
   HIP_TRY(hipEventRecord(ctx->done_ev, s));
@@ -739,11 +742,11 @@ static int run_large_k(knn_ctx* ctx, const double* dQ, int64_t m, int W, int met
                        const Sink& sink_in, hipStream_t s) {
   const TrainDev& t = ctx->train;
   Sink sink = sink_in;
-  sink.tie_mask = tie_mask_of(ctx, sink_in);
+  sink.tie_mode = tie_mask_of(ctx, sink_in);
   int rc;
   int64_t tie_per = 0;
   int tie_nwg = 0;
-  if (sink.tie_mask) {  // tied queries: queued by large_k_kernel for the reference-order pass
+  if (sink.tie_mode) {  // tied queries: queued by large_k_kernel for the reference-order pass
     tie_per = tie_scratch_bytes(t.n, ctx->class_cnt);
     tie_nwg = (int)std::max<int64_t>(1, std::min<int64_t>(ctx->cu_count, (2ll << 30) / tie_per));
     if ((rc = ctx->tie_q.ensure((size_t)m * sizeof(int) + 16))) return rc;
@@ -761,9 +764,10 @@ static int run_large_k(knn_ctx* ctx, const double* dQ, int64_t m, int W, int met
   ctx->last_kmetric = -1;
   launch_large_k(metric, t, dQ, m, W, ctx->class_cnt, (unsigned char*)ctx->lk.p, per, (int)nwg,
                  sink, s);
-  if (sink.tie_mask)
+  if (sink.tie_mode)
     launch_tie_order(metric, t, dQ, sink.tie_q, sink.tie_cnt, ctx->class_cnt,
-                     (unsigned char*)ctx->tie_ws.p, tie_per, tie_nwg, sink, s);
+                     (unsigned char*)ctx->tie_ws.p, tie_per, tie_nwg, sink,
+                     (unsigned long long*)ctx->totals.p + 2, s);
   launch_fill_i32(ctx->d_counts, 2, 0, s);  // exact path: no query fails certification
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(ctx->done_ev, s));
@@ -994,6 +998,19 @@ int knn_rescan_totals(knn_ctx* ctx, int64_t out[2], int reset) {
   out[1] = (int64_t)v[1];
   if (reset) HIP_TRY(hipMemset(ctx->totals.p, 0, sizeof v));
   auto_check(ctx);
+  return KNN_OK;
+}
+
+int knn_tie_totals(knn_ctx* ctx, int64_t* out, int reset) {
+  int rc;
+  if ((rc = device_guard(ctx))) return rc;
+  if (!out) return knn_fail(KNN_ERR_ARG, "null output");
+  unsigned long long v = 0;
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  HIP_TRY(hipEventSynchronize(ctx->done_ev));
+  HIP_TRY(hipMemcpy(&v, (unsigned long long*)ctx->totals.p + 2, sizeof v, hipMemcpyDeviceToHost));
+  *out = (int64_t)v;
+  if (reset) HIP_TRY(hipMemset((unsigned long long*)ctx->totals.p + 2, 0, sizeof v));
   return KNN_OK;
 }
 

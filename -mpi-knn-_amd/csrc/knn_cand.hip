@@ -222,6 +222,19 @@ cand_stream_kernel(const float* __restrict__ X32, const float* __restrict__ xini
 #ifndef KNN_S3_NB
 #define KNN_S3_NB 4
 #endif
+// Q16: A-fragment ring depth (LDS reads in flight behind the MFMAs) and
+// whether the MFMA / read interleave is pinned with sched_group_barrier
+#ifndef KNN_S3_RING
+#define KNN_S3_RING 4
+#endif
+#ifndef KNN_S3_SCHED
+#define KNN_S3_SCHED 1
+#endif
+// one 8-wave workgroup per CU (the 4-deep LDS ring takes 132 KiB): 2 waves
+// per SIMD, so up to 256 registers each for fragments in flight
+#ifndef KNN_S3_WPE
+#define KNN_S3_WPE 2
+#endif
 // s_waitcnt vmcnt(n) + s_barrier with a run-time n (vmcnt takes an immediate)
 __device__ __forceinline__ void s3_wait_barrier(int n) {
   switch (n) {
@@ -272,7 +285,7 @@ __device__ __forceinline__ void s3_map(int b, int nwg, int n_qt, int gq, int& qt
 // than 32x32x16 for the same cycles per FLOP (MI355X_MICROARCH.md, DVFS
 // give-back item 7).
 template <int R, bool F16, bool Q16>
-__global__ void __launch_bounds__(512)
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(KNN_S3_WPE, KNN_S3_WPE)))
 cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* QT, int nch,
                int n_tiles, int S, int n_qt, float* __restrict__ out_v, int* __restrict__ out_i,
                int abl, int gq, uint32_t* gthr, int gk) {
@@ -419,11 +432,30 @@ cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* 
       }
       const f16x8 b0 = *(const f16x8*)(buf + BLK + off_q + off_16);
       const f16x8 b1 = *(const f16x8*)(buf + BLK + off_q + 16 * 64 + off_16);
+      // A fragments through a ring of KNN_S3_RING registers: the read of row
+      // block rb + RING is issued as block rb's two MFMAs go out, so RING - 1
+      // reads are in flight behind the MFMAs instead of the one or two the
+      // compiler's own schedule keeps (its just-in-time reads left each wave
+      // waiting on LDS latency every two MFMAs, with only two waves per SIMD
+      // to cover it)
+      constexpr int RING = KNN_S3_RING;
+      f16x8 ar[RING];
+#pragma unroll
+      for (int i = 0; i < RING; ++i) ar[i] = *(const f16x8*)(buf + i * 16 * 64 + off_16);
+#if KNN_S3_SCHED
+      __builtin_amdgcn_sched_group_barrier(0x100, RING + 2, 0);  // B pair + ring fill first
+#endif
 #pragma unroll
       for (int rb = 0; rb < 16; ++rb) {
-        const f16x8 a = *(const f16x8*)(buf + rb * 16 * 64 + off_16);
+        const f16x8 a = ar[rb % RING];
         aq[rb][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b0, aq[rb][0], 0, 0, 0);
         aq[rb][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b1, aq[rb][1], 0, 0, 0);
+        if (rb + RING < 16) ar[rb % RING] = *(const f16x8*)(buf + (rb + RING) * 16 * 64 + off_16);
+#if KNN_S3_SCHED
+        // pin the order: 2 MFMAs, then the ring refill
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+#endif
       }
       if (c == nch - 1) {
         if (!(abl & 2)) {

@@ -34,6 +34,11 @@ static_assert(KNN_RES_TPB * knnk::kTR == knnk::kResTileRows || KNN_RES_TPB != 2,
 #ifndef KNN_M4_PIPE
 #define KNN_M4_PIPE 1
 #endif
+// fp16 kernel: A-fragment reads kept KNN_M4_SCHED ahead of the MFMAs by
+// sched_group_barrier (0: the compiler's own schedule)
+#ifndef KNN_M4_SCHED
+#define KNN_M4_SCHED 0
+#endif
 
 namespace knnk {
 
@@ -403,6 +408,11 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
         // lane's chunk 4ks + g16 sits at 4ks + (g16 ^ xh_swz(row)) (rows of a
         // sub-tile start at multiples of 32, so row & 15 = c16)
         const int g16s = g16 ^ (xsw ? xh_swz(c16) : 0);
+#if KNN_M4_SCHED
+        // the seed reads and the first KNN_M4_SCHED A fragments first, then
+        // each fragment's two MFMAs followed by the next fragment's read
+        __builtin_amdgcn_sched_group_barrier(0x100, KNN_M4_SCHED + 2, 0);
+#endif
 #pragma unroll
         for (int ks = 0; ks < DP / 32; ++ks) {
 #pragma unroll
@@ -414,6 +424,11 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
               const f16x8 b = __builtin_bit_cast(f16x8, qf[qb * (DP / 32) + ks]);
               acc[rb][qb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, acc[rb][qb], 0, 0, 0);
             }
+#if KNN_M4_SCHED
+            __builtin_amdgcn_sched_group_barrier(0x008, QB, 0);
+            if (2 * ks + rb + KNN_M4_SCHED < DP / 16)
+              __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+#endif
           }
         }
       } else {

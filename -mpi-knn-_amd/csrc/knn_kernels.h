@@ -29,10 +29,10 @@ struct Sink {
   double* dist;          // single: [m*k] (nullable); partial: [m*w]
   int32_t* flags;        // single: [m] (nullable)
   int32_t* plab;         // partial: [m*w]
-  // single: queries whose tie bits (KNN_FLAG_TIE_*) intersect tie_mask are
-  // appended to tie_q (count in tie_cnt[0]) for the reference-order pass
-  // (launch_tie_order); tie_mask 0 = off
-  int tie_mask;
+  // single: tied queries appended to tie_q (count in tie_cnt[0]) for the
+  // reference-order pass (launch_tie_order): tie_mode 0 none, 1 those whose
+  // label the reference's tie order could change, 2 every tied query
+  int tie_mode;
   int* tie_q;
   int* tie_cnt;
 };
@@ -199,9 +199,10 @@ void launch_fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t s);
 // reach the first k positions.  Per workgroup scratch: tie_scratch_bytes.
 constexpr int kFlagTieRef = 32;  // KNN_FLAG_TIE_REF: order resolved as the reference's
 int64_t tie_scratch_bytes(int64_t n, int class_cnt);
+// totals: device running count of the queries re-ordered (nullable)
 void launch_tie_order(int metric, const TrainDev& t, const double* Q64, const int* tie_q,
                       const int* tie_cnt, int class_cnt, unsigned char* scratch, int64_t per_wg,
-                      int nwg, const Sink& sink, hipStream_t s);
+                      int nwg, const Sink& sink, unsigned long long* totals, hipStream_t s);
 // fp64 rows -> [hi(DP) | lo(DP)] bf16 rows of scale*x (candidate metric 2 = L2 via bf16x3)
 // rows of `out` are row_shorts 16-bit words; xl2/xl1 (train only, else null)
 // fill the padded row's seed floats after the 2*DP bf16 payload

@@ -26,18 +26,42 @@ __device__ void finish_single(int64_t q, const double* dk, const int* di, const 
   }
   const int M = wave_max_i(bc);
   const int tmin = wave_min_i(bc == M ? bt : INT_MAX);
+  const int winner = k > 0 ? ls[tmin] : -1;
   int tie = 0;
   for (int t = lane; t + 1 < k; t += 64)
     if (dk[t] == dk[t + 1]) tie |= ls[t] != ls[t + 1] ? 4 : 8;  // TIE_VOTE / TIE_ORDER
   tie = wave_or_i(tie);
+  const bool bnd = k > 0 && k < cnt && dk[k - 1] == dk[k];  // KNN_FLAG_TIE_BOUNDARY
+  bool queue = false;
+  if (sink.tie_mode == 1 && (bnd || (tie & 4))) {
+    // could the reference's tie order give another label?  The runner-up
+    // count m2 (classes other than the winner) and gin, the top-k entries in
+    // a tie across the k-th place: the order among equal distances only
+    // decides between classes sharing the top count, and the membership of
+    // that tie group moves at most gin entries from one class to another
+    int m2 = 0, gin = 0;
+    for (int t = lane; t < k; t += 64) {
+      const int lt = ls[t];
+      if (lt != winner) {
+        int c = 0;
+        for (int s2 = 0; s2 < k; ++s2) c += (ls[s2] == lt);
+        m2 = max(m2, c);
+      }
+      gin += bnd && dk[t] == dk[k - 1];
+    }
+    m2 = wave_max_i(m2);
+    gin = wave_sum_i(gin);
+    queue = (bnd && M - m2 <= 2 * gin) || ((tie & 4) && m2 == M);
+  } else if (sink.tie_mode == 2) {
+    queue = bnd || tie;
+  }
   if (lane == 0) {
-    sink.labels[q] = k > 0 ? ls[tmin] : -1;
-    int f = flag0 | tie;
-    if (k > 0 && k < cnt && dk[k - 1] == dk[k]) f |= 2;  // KNN_FLAG_TIE_BOUNDARY
+    sink.labels[q] = winner;
+    const int f = flag0 | tie | (bnd ? 2 : 0);
     if (sink.flags) sink.flags[q] = f;
     // the order among exactly equal distances is the reference's std::sort's:
     // queue the query for the reference-order pass (tie_order_kernel)
-    if (f & sink.tie_mask) sink.tie_q[atomicAdd(sink.tie_cnt, 1)] = (int)q;
+    if (queue) sink.tie_q[atomicAdd(sink.tie_cnt, 1)] = (int)q;
   }
   for (int t = lane; t < k; t += 64) {
     if (sink.idx) sink.idx[q * k + t] = (int64_t)di[t] + idx_off;
@@ -1182,10 +1206,12 @@ template <int METRIC>
 __global__ void __launch_bounds__(kTieThreads)
 tie_order_kernel(TrainDev t, const double* __restrict__ Q64, const int* __restrict__ tie_q,
                  const int* __restrict__ tie_cnt, int class_cnt, unsigned char* __restrict__ scratch,
-                 int64_t per_wg, Sink sink) {
+                 int64_t per_wg, Sink sink, unsigned long long* totals) {
   __shared__ double tiles[kTieThreads / 64][64 * (kFullDC + 1)];
   __shared__ RefSortShared s;
   const int count = *tie_cnt;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && totals && count)
+    atomicAdd(totals, (unsigned long long)count);  // running count of re-ordered queries
   const int64_t n = t.n;
   unsigned char* base = scratch + (int64_t)blockIdx.x * per_wg;
   double* D = (double*)base;
@@ -1205,14 +1231,14 @@ tie_order_kernel(TrainDev t, const double* __restrict__ Q64, const int* __restri
 
 void launch_tie_order(int metric, const TrainDev& t, const double* Q64, const int* tie_q,
                       const int* tie_cnt, int class_cnt, unsigned char* scratch, int64_t per_wg,
-                      int nwg, const Sink& sink, hipStream_t s) {
+                      int nwg, const Sink& sink, unsigned long long* totals, hipStream_t s) {
   if (nwg <= 0) return;
   if (metric == 0)
     hipLaunchKernelGGL(tie_order_kernel<0>, dim3(nwg), dim3(kTieThreads), 0, s, t, Q64, tie_q,
-                       tie_cnt, class_cnt, scratch, per_wg, sink);
+                       tie_cnt, class_cnt, scratch, per_wg, sink, totals);
   else
     hipLaunchKernelGGL(tie_order_kernel<1>, dim3(nwg), dim3(kTieThreads), 0, s, t, Q64, tie_q,
-                       tie_cnt, class_cnt, scratch, per_wg, sink);
+                       tie_cnt, class_cnt, scratch, per_wg, sink, totals);
 }
 
 // ------------------------------------------------ large k (k > kMaxK)
@@ -1354,6 +1380,10 @@ large_k_kernel(TrainDev t, const double* __restrict__ Q64, int64_t m, int W, int
           if (c > best) { best = c; lab = ol[i]; }
         }
         sink.labels[q] = lab;
+        int m2 = 0;  // runner-up count (see finish_single)
+        for (int c = 0; c < class_cnt; ++c)
+          if (c != lab) m2 = max(m2, cnt[c]);
+        s_rank = best - m2;  // (s_rank is free here)
       }
       int tie = 0;
       for (int i = tid; i + 1 < k; i += kLkThreads)
@@ -1362,16 +1392,22 @@ large_k_kernel(TrainDev t, const double* __restrict__ Q64, int64_t m, int W, int
       __syncthreads();
       if (tid == 0) {
         int f = s_bad;
-        if (k < W && od[k - 1] == od[k]) f |= 2;  // KNN_FLAG_TIE_BOUNDARY
+        const bool bnd = k < W && od[k - 1] == od[k];
+        if (bnd) f |= 2;  // KNN_FLAG_TIE_BOUNDARY
         if (sink.flags) sink.flags[q] = f;
-        s_flags = f;
+        int gin = 0;
+        for (int i = k - 1; bnd && i >= 0 && od[i] == od[k - 1]; --i) ++gin;
+        // queue for the reference-order pass: the rule of finish_single
+        s_flags = sink.tie_mode == 2 ? (f & 14) != 0
+                : sink.tie_mode == 1 ? (bnd && s_rank <= 2 * gin) || ((f & 4) && s_rank == 0)
+                                     : 0;
       }
       for (int i = tid; i < k; i += kLkThreads) {
         if (sink.idx) sink.idx[q * k + i] = (int64_t)oi[i] + sink.idx_off;
         if (sink.dist) sink.dist[q * k + i] = od[i];
       }
       // exact ties: queued for the reference-order pass (tie_order_kernel)
-      if (tid == 0 && (s_flags & sink.tie_mask)) sink.tie_q[atomicAdd(sink.tie_cnt, 1)] = (int)q;
+      if (tid == 0 && s_flags) sink.tie_q[atomicAdd(sink.tie_cnt, 1)] = (int)q;
     } else {
       for (int i = tid; i < sink.w; i += kLkThreads) {
         const bool ok = i < W;

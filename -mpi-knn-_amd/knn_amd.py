@@ -36,7 +36,7 @@ EXPORTED = (
     "knn_group_last_compute_seconds", "knn_set_timing", "knn_last_phase_ms",
     "knn_last_geometry", "knn_set_precision", "knn_last_candidate_path", "knn_set_tuning",
     "knn_minmax_device", "knn_normalize_device", "knn_normalize", "knn_group_normalize",
-    "knn_timing_totals", "knn_rescan_totals", "knn_last_kernel_name",
+    "knn_timing_totals", "knn_rescan_totals", "knn_last_kernel_name", "knn_tie_totals",
 )
 PRECISION_AUTO, PRECISION_FP32, PRECISION_BF16X3, PRECISION_FP16 = 0, 1, 2, 3
 PHASE_PREP, PHASE_CANDIDATE, PHASE_RERANK, PHASE_RESCAN = 0, 1, 2, 3
@@ -121,6 +121,7 @@ def lib():
                               ctypes.c_int),
         "knn_rescan_totals": ([P, ctypes.POINTER(i64), ctypes.c_int], ctypes.c_int),
         "knn_last_kernel_name": ([P], ctypes.c_char_p),
+        "knn_tie_totals": ([P, ctypes.POINTER(i64), ctypes.c_int], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -244,6 +245,13 @@ class Classifier:
         out = (ctypes.c_int64 * 2)()
         _check(lib().knn_rescan_totals(self._h, out, int(bool(reset))))
         return int(out[0]), int(out[1])
+
+    def tie_totals(self, reset=False):
+        """Queries re-ordered as the reference's std::sort orders them
+        (KNN_FLAG_TIE_REF), summed over calls since the last reset."""
+        out = ctypes.c_int64()
+        _check(lib().knn_tie_totals(self._h, ctypes.byref(out), int(bool(reset))))
+        return int(out.value)
 
     def timing_totals(self, reset=False):
         """(per-phase ms summed over timed calls since the last reset, calls)."""

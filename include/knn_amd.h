@@ -229,6 +229,10 @@ int64_t knn_last_rescan_count(knn_ctx* ctx);
  * that failed certification, out[1] = of those, queries finished by the full
  * exact scan.  Waits for the context's work; reset != 0 zeroes the sums. */
 int knn_rescan_totals(knn_ctx* ctx, int64_t out[2], int reset);
+/* Queries re-ordered as the reference's std::sort orders them
+ * (KNN_FLAG_TIE_REF) summed over calls since the last reset.  Waits for the
+ * context's work; reset != 0 zeroes the sum. */
+int knn_tie_totals(knn_ctx* ctx, int64_t* out, int reset);
 
 /* ---- single-process multi-GPU group over RCCL (xGMI) ---------------------
  * mode 0 = query-sharded: the train set is RCCL-broadcast from device

@@ -38,8 +38,9 @@ def pytest_terminal_summary(terminalreporter):
         return
     terminalreporter.write_line(
         "tie-vote parity: %d cases, %d queries, %d with an exact-tie vote, %d of those with a "
-        "label other than the oracle's std::sort order" %
-        (tv["cases"], tv["queries"], tv["tie_vote"], tv["tie_vote_label_differs"]))
+        "label other than the oracle's std::sort order; %d re-ordered as the reference's "
+        "std::sort" % (tv["cases"], tv["queries"], tv["tie_vote"], tv["tie_vote_label_differs"],
+                       tv.get("reordered", 0)))
     try:
         import json
         out = os.path.join(ROOT, "gpurun_out")
