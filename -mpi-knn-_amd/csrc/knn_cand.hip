@@ -225,7 +225,7 @@ cand_stream_kernel(const float* __restrict__ X32, const float* __restrict__ xini
 // Q16: A-fragment ring depth (LDS reads in flight behind the MFMAs) and
 // whether the MFMA / read interleave is pinned with sched_group_barrier
 #ifndef KNN_S3_RING
-#define KNN_S3_RING 4
+#define KNN_S3_RING 3
 #endif
 #ifndef KNN_S3_SCHED
 #define KNN_S3_SCHED 1
@@ -385,7 +385,9 @@ cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* 
       if (abl & 1) n = 0;
       if (x_age >= 0) ++x_age;
       if (x_age >= 1 && x_age <= PD) n += x_ops;
-      s3_wait_barrier(n);
+      // (wave-uniform: scalar branches to the right immediate, not an
+      // exec-masked tree -- the divergence analysis cannot prove it)
+      s3_wait_barrier(__builtin_amdgcn_readfirstlane(n));
     }
     __builtin_amdgcn_sched_barrier(0);
     if (st + PD < total && !(abl & 1)) issue();

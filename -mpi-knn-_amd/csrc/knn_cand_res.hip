@@ -39,6 +39,10 @@ static_assert(KNN_RES_TPB * knnk::kTR == knnk::kResTileRows || KNN_RES_TPB != 2,
 #ifndef KNN_M4_SCHED
 #define KNN_M4_SCHED 0
 #endif
+#ifndef KNN_RFL
+#define KNN_RFL 1
+#endif
+
 
 namespace knnk {
 
@@ -295,7 +299,12 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       // not order memory) and no vmcnt(0) drains the in-flight tiles.
       const int ahead = min(PD - 1, my_nt - 1 - it);
       if (x_age >= 0) ++x_age;
+      // (wave-uniform; readfirstlane keeps the dispatch below on scalar branches)
+#if KNN_RFL
+      const int extra = __builtin_amdgcn_readfirstlane((x_age >= 1 && x_age <= PD - 1) ? x_ops : 0);
+#else
       const int extra = (x_age >= 1 && x_age <= PD - 1) ? x_ops : 0;
+#endif
       if (abl & 16) {
         // timing-only ablation: this wave's own waits, no workgroup barrier
         // (other waves' pieces may not have landed: results invalid)
