@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cfloat>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -134,6 +135,45 @@ int knn_destroy(knn_ctx* ctx) {
 
 }  // extern "C"
 
+// Integer-coded train sets (knn_prep.hip, int8 images): every value x =
+// (c_i + k) / 2^s with an integer code k in [-128, 127] per dimension -- the
+// 8-bit grid of SIFT-like byte features, or of the reference's CSVs of
+// k/256 values.  s = the largest number of fractional bits of any value; the
+// centre c_i is the middle of dimension i's code range.  Sets ctx->i8_ok.
+static int detect_i8(knn_ctx* ctx, const double* dX, int64_t n, int d) {
+  ctx->i8_ok = false;
+  if (pad_dim_i8(d) <= 0) return KNN_OK;
+  int rc;
+  if ((rc = ctx->i8_gs.ensure((size_t)(col_mean_blocks(n) * 2 + 2) * d * sizeof(double) + 16)))
+    return rc;
+  double* part = (double*)ctx->i8_gs.p;
+  double* out = part + (size_t)col_mean_blocks(n) * 2 * d;
+  unsigned* frac = (unsigned*)(out + 2 * d);
+  HIP_TRY(hipMemsetAsync(frac, 0, sizeof(unsigned), ctx->stream));
+  launch_grid_stats(dX, n, d, part, out, frac, ctx->stream);
+  HIP_TRY(hipGetLastError());
+  std::string buf((size_t)2 * d * sizeof(double) + sizeof(unsigned), '\0');
+  HIP_TRY(hipMemcpyAsync(&buf[0], out, buf.size(), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  const double* lohi = (const double*)buf.data();
+  unsigned s;
+  memcpy(&s, buf.data() + 2 * d * sizeof(double), sizeof s);
+  if (s > 30) return KNN_OK;
+  std::string cent((size_t)2 * d * sizeof(double), '\0');
+  double* c = (double*)&cent[0];
+  for (int i = 0; i < d; ++i) {
+    const double lo = std::ldexp(lohi[i], (int)s), hi = std::ldexp(lohi[d + i], (int)s);
+    if (!(hi - lo <= 255.0) || !(std::fabs(lo) < 0x1p50) || !(std::fabs(hi) < 0x1p50)) return KNN_OK;
+    c[i] = std::floor((lo + hi + 1.0) / 2.0);        // codes x 2^s - c in [-128, 127]
+    c[d + i] = std::ldexp(c[i], -(int)s);            // the same centre in value units
+  }
+  if ((rc = ctx->i8_cent.ensure((size_t)2 * d * sizeof(double)))) return rc;
+  HIP_TRY(hipMemcpy(ctx->i8_cent.p, c, (size_t)2 * d * sizeof(double), hipMemcpyHostToDevice));
+  ctx->i8_s = (int)s;
+  ctx->i8_ok = true;
+  return KNN_OK;
+}
+
 // Builds the fp32 candidate copy + seeds + norm stats from fp64 rows that
 // already sit on the device.
 static int build_train(knn_ctx* ctx, const double* dX, const int32_t* dlab, int64_t n, int d,
@@ -169,6 +209,7 @@ static int build_train(knn_ctx* ctx, const double* dX, const int32_t* dlab, int6
     return knn_fail(KNN_ERR_ARG, std::to_string(ctx->h_stats[5]) +
                                      " train labels outside [0, class_cnt)");
   memcpy(&ctx->xamax, &ctx->h_stats[2], 8);
+  if ((rc = detect_i8(ctx, dX, n, d))) return rc;
   int e = 0;
   if (ctx->xamax > 0.0) (void)std::frexp(ctx->xamax, &e);  // xamax < 2^e
   // |x - mu| up to 2^400 (beyond, fp32 operands could overflow); tiny data
@@ -209,6 +250,8 @@ static int build_train(knn_ctx* ctx, const double* dX, const int32_t* dlab, int6
   ctx->DPb = 0;  // bf16x3 / fp16 copies are rebuilt lazily for the new train set
   ctx->DPh = 0;
   ctx->DPs = 0;
+  ctx->DPi = 0;
+  ctx->i8_off = false;
   ctx->fp16_off = false;
   ctx->auto_pending = false;
   ctx->trained = true;
@@ -268,6 +311,29 @@ static int ensure_fp16(knn_ctx* ctx, hipStream_t s) {
   return KNN_OK;
 }
 
+// The int8 image for kernel metric 5 (knn_prep.hip): codes x 2^s - c of
+// every row (16-B chunks swizzled as the fp16 image) + the accumulator seeds
+// -ceil(||k||^2 / 2); rows of DP + 16 bytes, n_pad rows.
+static int ensure_i8(knn_ctx* ctx, hipStream_t s) {
+  const TrainDev& t = ctx->train;
+  const int DPi = pad_dim_i8(t.d);
+  if (!ctx->i8_ok || DPi <= 0) return knn_fail(KNN_ERR_ARG, "train set not integer-coded (int8 pass)");
+  if (ctx->DPi == DPi) return KNN_OK;
+  int rc;
+  if ((rc = ctx->XI.ensure((size_t)t.n_pad * (DPi + 16) + 1024))) return rc;
+  unsigned* cmax = (unsigned*)((unsigned long long*)ctx->stats.p + 3);
+  HIP_TRY(hipMemsetAsync(cmax, 0, 8, s));
+  launch_prep_i8_train(t.X64, (const double*)ctx->i8_cent.p, t.n, t.d, DPi, t.n_pad, ctx->i8_s,
+                       (signed char*)ctx->XI.p, cmax, s);
+  HIP_TRY(hipGetLastError());
+  unsigned cm = 0;
+  HIP_TRY(hipMemcpyAsync(&cm, cmax, sizeof cm, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  ctx->i8_x2max = std::ldexp((double)cm, -2 * ctx->i8_s);
+  ctx->DPi = DPi;
+  return KNN_OK;
+}
+
 // The fp16 S3 image (d > 256, cand_s3_kernel<R, true>): 2^jx (x - mu) in
 // fp16 tile-chunk images + the L2 seeds; the representation error measured
 // as for the resident copy.
@@ -309,6 +375,18 @@ static bool use_fp16(const knn_ctx* ctx, int metric, int64_t m, int W) {
   if (ctx->precision == KNN_PRECISION_FP16) return true;
   if (ctx->precision != KNN_PRECISION_AUTO || ctx->fp16_off) return false;
   return streamed || (m >= 4096 && W <= kQuadMaxW);
+}
+
+// int8 candidate pass (kernel metric 5): integer-coded train sets (detect_i8)
+// at d <= 256 for batches of >= 4096 queries, in AUTO and FP16 modes, until a
+// batch sends more than 1/16 of its queries to the rescan (queries off the
+// train set's grid).  Tuning key "i8": -1 auto, 0 off, 1 on (where possible).
+static bool use_i8(const knn_ctx* ctx, int metric, int64_t m, int W) {
+  if (metric != KNN_METRIC_L2 || !ctx->i8_ok || pad_dim_i8(ctx->train.d) <= 0) return false;
+  if (ctx->tune_i8 >= 0) return ctx->tune_i8 > 0;
+  if (ctx->tune_fp16 >= 0) return false;  // an explicit fp16 request
+  if (ctx->precision != KNN_PRECISION_AUTO || ctx->i8_off) return false;
+  return m >= 4096 && W <= kQuadMaxW;
 }
 
 static bool use_bf16x3(const knn_ctx* ctx, int metric) {
@@ -369,7 +447,7 @@ static void choose_geometry(knn_ctx* ctx, int metric, bool streamed, int DP, int
                             int64_t n_tiles, int W, int C, bool s3q, int& S_out, int& R_out) {
   int S_hi = (int)std::max<int64_t>(1, std::min<int64_t>(64, n_tiles));
   int bestS = 1, bestR = 8;
-  const bool quad = !streamed && (metric == 3 || metric == 4);  // 16x16 layouts
+  const bool quad = !streamed && metric >= 3;  // 16x16 layouts (bf16x3, fp16, int8)
   const int lps = quad || s3q ? 4 : 2;  // lists per query per split
   // S3 on 16x16x32 (s3q): R = 8 quad lists, 4 * S * 8 <= kMaxUnion entries
   if (s3q) S_hi = std::min(S_hi, kMaxUnion / (4 * 8));
@@ -497,7 +575,10 @@ static void auto_check(knn_ctx* ctx) {
   // AUTO retires the fp16 pass for this train set when a batch leaves more
   // than 1/16 of its queries to the rescan (data whose neighbour gaps are
   // too fine for fp16 operands): later batches take bf16x3
-  if ((int64_t)ctx->h_counts[0] * 16 > ctx->auto_m) ctx->fp16_off = true;
+  if ((int64_t)ctx->h_counts[0] * 16 > ctx->auto_m) {
+    if (ctx->auto_kind == 5) ctx->i8_off = true;
+    else ctx->fp16_off = true;
+  }
   ctx->auto_pending = false;
 }
 
@@ -537,7 +618,12 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   int kmetric = metric, DP = t.DP;
   const float* Xk = t.X32;
   bool s3h = false;  // fp16 on the S3 stream kernel (d > 256)
-  if (use_fp16(ctx, metric, m, W)) {
+  if (use_i8(ctx, metric, m, W)) {
+    if ((rc = ensure_i8(ctx, s))) return rc;
+    kmetric = 5;
+    DP = ctx->DPi;
+    Xk = (const float*)ctx->XI.p;
+  } else if (use_fp16(ctx, metric, m, W)) {
     kmetric = 4;
     if (pad_dim_fp16(t.d) > 0) {
       if ((rc = ensure_fp16(ctx, s))) return rc;
@@ -565,7 +651,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   if (kmetric == 2 && !s3 && m16 && DP % 32 == 0) kmetric = 3;
   int nw = 4;
   if (DP <= 256 && kmetric != 1) nw = ctx->tune_nw ? std::min(ctx->tune_nw, 8) : (m >= 4096 ? 8 : 4);
-  if (kmetric >= 3) nw = 8;
+  if (kmetric >= 3) nw = 8;  // (the 16x16 layouts: fp16, bf16x3, int8)
   if (kmetric == 4 && !s3 && ctx->tune_nw) nw = ctx->tune_nw;  // 4, 8 or 16
   if (s3) nw = 8;
   const int qpb = s3 ? kS3Rows : (DP <= 256 ? 32 * nw : kQPB);
@@ -585,7 +671,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   const bool s3q = s3h && ctx->tune_s3q != 0 && s3q_S <= kMaxUnion / 32 && s3q_S <= n_tiles;
   choose_geometry(ctx, kmetric, s3, DP, nw, n_qt, n_tiles, W, C, s3q, S, R);
   // 16x16 layouts: 4 lists per query per split
-  const bool quad_lists = (!s3 && (kmetric == 3 || kmetric == 4)) || s3q;
+  const bool quad_lists = (!s3 && kmetric >= 3) || s3q;
   if (quad_lists && !s3q) R = 4;
   const int NL = (quad_lists ? 4 : 2) * S;
   C = std::min(C, NL * R);
@@ -645,8 +731,12 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   const double qscale = metric == KNN_METRIC_L2 ? -2.0 : 1.0;
   float* qvalid = (float*)ctx->qvalid.p;
   launch_query_check(dQ, t.mu, m, t.d, m_pad, qscale, t.jx,
-                     kmetric == 4 ? 65000.0 : std::ldexp(1.0, 100), qvalid, s);
-  if (s3h)
+                     kmetric == 5 ? DBL_MAX : kmetric == 4 ? 65000.0 : std::ldexp(1.0, 100), qvalid,
+                     s);
+  if (kmetric == 5)  // codes of the train set's grid; a query off it: valid 0 (rescan)
+    launch_prep_i8_queries(dQ, (const double*)ctx->i8_cent.p, m, t.d, DP, m_pad, ctx->i8_s,
+                           (signed char*)ctx->Q32.p, qvalid, s);
+  else if (s3h)
     launch_prep_half_tiled(dQ, t.mu, m, t.d, DP, m_pad, t.jx, -2.0, (unsigned short*)ctx->Q32.p,
                            nullptr, nullptr, qvalid, nullptr, s);
   else if (s3)
@@ -677,7 +767,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   cl.nw = nw;
   cl.gthr = use_gthr ? (uint32_t*)ctx->gthr.p : nullptr;
   cl.gk = gk;
-  cl.xsw = ctx->xh_swz;
+  cl.xsw = kmetric == 5 ? 1 : ctx->xh_swz;  // the int8 image is always swizzled
   // slots of groups without a split stay 0 (never the max)
   if (use_gthr) launch_fill_gthr(cl.gthr, m_pad, std::min(S, gk ? 8 : 4), s);
   if (s3h)
@@ -693,12 +783,30 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   HIP_TRY(hipGetLastError());
   if (tc) HIP_TRY(hipEventRecord(tc->ev[2], s));
   HIP_TRY(hipMemsetAsync(ctx->rescan_cnt.p, 0, 4 * sizeof(int), s));
-  launch_merge_rerank(metric, (const float*)ctx->cand_v.p, (const int*)ctx->cand_i.p, NL, R, t, dQ,
-                      m, W, C, err_factor(kmetric, DP),
-                      kmetric == 4 ? ProxyScale{qvalid, 0x1p-14, 0x1p-28, true}
-                                   : ProxyScale{qvalid, 0x1p-125, 0x1p-124},
-                      cl.gthr, sink, (int*)ctx->rescan_q.p,
-                      (double*)ctx->rescan_tau.p, (int*)ctx->rescan_cnt.p, s);
+  if (kmetric == 5) {
+    // int8 proxies are exact up to +1 (the odd-norm half of the seed): the
+    // merge sees the pass's own centre and scale (codes (x - cent/2^s) 2^s),
+    // an absolute error of one code unit (DP x up / DP) and each query's
+    // own coding error (off the grid / beyond the code range), measured
+    TrainDev t8 = t;
+    t8.mu = (const double*)ctx->i8_cent.p + t.d;
+    t8.jx = ctx->i8_s;
+    t8.x2max = ctx->i8_x2max;
+    t8.DP = DP;
+    launch_merge_rerank(metric, (const float*)ctx->cand_v.p, (const int*)ctx->cand_i.p, NL, R, t8,
+                        dQ, m, W, C, 0.0,
+                        ProxyScale{qvalid, 0.0, 1.0 / DP, false, (const double*)ctx->i8_cent.p},
+                        cl.gthr, sink,
+                        (int*)ctx->rescan_q.p, (double*)ctx->rescan_tau.p, (int*)ctx->rescan_cnt.p,
+                        s);
+  } else {
+    launch_merge_rerank(metric, (const float*)ctx->cand_v.p, (const int*)ctx->cand_i.p, NL, R, t,
+                        dQ, m, W, C, err_factor(kmetric, DP),
+                        kmetric == 4 ? ProxyScale{qvalid, 0x1p-14, 0x1p-28, true}
+                                     : ProxyScale{qvalid, 0x1p-125, 0x1p-124},
+                        cl.gthr, sink, (int*)ctx->rescan_q.p, (double*)ctx->rescan_tau.p,
+                        (int*)ctx->rescan_cnt.p, s);
+  }
   HIP_TRY(hipGetLastError());
   if (tc) HIP_TRY(hipEventRecord(tc->ev[3], s));
   // rescan of uncertified queries, sized on the device (knn_select.hip)
@@ -730,8 +838,10 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   // the deferred AUTO decision reads done_ev and h_counts, which belong to
   // the LAST call: it is armed by an fp16 call and dropped by any other
   // (a later fp16 call re-arms it with its own count)
-  ctx->auto_pending =
-      kmetric == 4 && ctx->precision == KNN_PRECISION_AUTO && ctx->tune_fp16 < 0 && !abl;
+  ctx->auto_pending = !abl && ((kmetric == 4 && ctx->precision == KNN_PRECISION_AUTO &&
+                                ctx->tune_fp16 < 0) ||
+                               (kmetric == 5 && ctx->tune_i8 < 0));
+  ctx->auto_kind = kmetric;
   ctx->auto_m = m;
   return KNN_OK;
 }
@@ -1053,6 +1163,9 @@ int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value) {
   } else if (!strcmp(key, "xhswz")) {
     if (value < 0 || value > 1) return knn_fail(KNN_ERR_ARG, "xhswz must be 0 or 1");
     ctx->tune_xhswz = (int)value;
+  } else if (!strcmp(key, "i8")) {
+    if (value < -1 || value > 1) return knn_fail(KNN_ERR_ARG, "i8 must be -1, 0 or 1");
+    ctx->tune_i8 = (int)value;
   } else if (!strcmp(key, "ties")) {
     if (value < 0 || value > 2) return knn_fail(KNN_ERR_ARG, "ties must be 0, 1 or 2");
     ctx->tune_ties = (int)value;

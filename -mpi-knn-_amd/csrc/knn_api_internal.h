@@ -38,6 +38,14 @@ struct knn_ctx {
   int xh_swz = 0;        // the fp16 copy's chunks are swizzled (xh_swz)
   int DPs = 0;           // padded dim of the fp16 S3 image (0 = not built)
   double xamax = 0.0;    // max |x_i - mu_i| over the train set
+  // int8 candidate pass (kernel metric 5): the train values are integer codes
+  // x = (cent_i + k) / 2^i8_s, k in [-128, 127] (i8_ok, set at set_train)
+  bool i8_ok = false;
+  int i8_s = 0;
+  int DPi = 0;           // padded dim of the int8 image (0 = not built)
+  double i8_x2max = 0.0; // max ||k||^2 / 2^(2 s) of the image
+  bool i8_off = false;   // AUTO: int8 pass retired for this train set
+  int auto_kind = 0;     // the pass the pending AUTO decision is about (4 fp16, 5 int8)
   bool fp16_off = false; // AUTO: fp16 candidate pass retired for this train set
                          // (a batch certified too few queries, see knn_run_search)
   // the last call, for the deferred AUTO decision: its completion event,
@@ -52,6 +60,7 @@ struct knn_ctx {
   int tune_gk = -1;            // what the lists publish into gthr (-1 auto, 0 list R-th, 1..16)
   int tune_xhswz = 1;          // fp16 train image chunk swizzle (xh_swz): 1 on, 0 off (A/B)
   int tune_fp16 = -1;          // fp16 candidate pass: -1 auto, 0 off, 1 on
+  int tune_i8 = -1;            // int8 candidate pass: -1 auto, 0 off, 1 on (where the data allow)
   int tune_ties = 1;           // reference tie order: 0 off, 1 vote-affecting ties, 2 all ties
   int tune_m16 = -1;           // bf16x3 on the 16x16x32 MFMA layout: -1 auto, 0 off, 1 on
   int last_nw = 0;
@@ -66,6 +75,9 @@ struct knn_ctx {
   int64_t geom[4] = {0, 0, 0, 0};
   // train-side HBM
   DevBuf X64_own, lab_own, X32, xl2, xl1, stats, XB, XS, XH, XT16, XS16, mu, mu_part;
+  // int8 image: codes [n_pad][DP + 16 B]; per-dim centres [code units d |
+  // value units d] (the latter the merge's mu for this pass); grid stats scratch
+  DevBuf XI, i8_cent, i8_gs;
   // per-classify workspace
   DevBuf Q64, Q32, qvalid, cand_v, cand_i, gthr, rescan_q, rescan_tau, rescan_cnt, fr_cnt, fr_buf,
       fr_q, fr_thr, slow_q, totals, lk;
@@ -78,7 +90,7 @@ struct knn_ctx {
   // normalisation: per-thread partial max/min, bounds, host-API staging
   DevBuf nrm_part, nrm_mm, nrm_X;
   std::vector<DevBuf*> all_bufs() {
-    return {&X64_own, &lab_own, &X32,   &xl2,   &xl1,    &stats,  &XB,       &XS,
+    return {&X64_own, &lab_own, &X32,   &xl2,   &xl1,    &stats,  &XB,       &XS, &XI, &i8_cent, &i8_gs,
             &XH,      &XT16,    &XS16,  &mu,      &mu_part, &Q64, &Q32,    &qvalid, &cand_v,   &cand_i,
             &gthr,    &rescan_q, &rescan_tau, &rescan_cnt, &fr_cnt, &fr_buf, &fr_q, &fr_thr,
             &slow_q,  &totals,  &lk, &mrg, &tie_q, &tie_ws, &o_lab, &o_idx, &o_dist, &o_flags, &nrm_part, &nrm_mm, &nrm_X};

@@ -573,6 +573,12 @@ int pad_dim_fp16(int d) {
   return (DP <= 256 && DP % 32 == 0) ? DP : -1;
 }
 
+// int8 path: the resident 16x16x64 kernel, DP a multiple of 64, <= 256
+int pad_dim_i8(int d) {
+  const int DP = (d + 63) / 64 * 64;
+  return DP <= 256 ? DP : -1;
+}
+
 // fp16 S3 kernel above 256 dims: any multiple of 32
 int pad_dim_fp16_s3(int d) {
   const int DP = (d + 31) / 32 * 32;

@@ -42,6 +42,15 @@ static_assert(KNN_RES_TPB * knnk::kTR == knnk::kResTileRows || KNN_RES_TPB != 2,
 #ifndef KNN_RFL
 #define KNN_RFL 1
 #endif
+// int8 kernel: 32-row sub-tiles per staged tile (8: 256-row tiles, half the
+// barriers per MFMA of 128-row tiles; n_pad is a multiple of kRowAlign = 256)
+#ifndef KNN_I8_TPB
+#define KNN_I8_TPB 4
+#endif
+// int8 kernel: all A-fragment reads of a sub-tile issued before its MFMAs
+#ifndef KNN_I8_SCHED
+#define KNN_I8_SCHED 1
+#endif
 
 
 namespace knnk {
@@ -75,7 +84,7 @@ __device__ __forceinline__ bool exchange_tile(int it) {
 
 template <int METRIC>
 constexpr int res_tpb() {
-  return METRIC == 4 ? KNN_M4_TPB : KNN_RES_TPB;
+  return METRIC == 5 ? KNN_I8_TPB : METRIC == 4 ? KNN_M4_TPB : KNN_RES_TPB;
 }
 
 // Train rows in HBM (X32 for fp32/L1, XB for bf16x3) share one padded row
@@ -112,7 +121,7 @@ constexpr int res_tpb() {
 // (not for R = 16 lists or DP > 160, whose registers do not fit: spills).
 template <int DP, int R, int METRIC, int NW>
 __global__ void __launch_bounds__(NW * 64)
-__attribute__((amdgpu_waves_per_eu((METRIC == 4 ? DP / 2 : DP) <= 160 && R <= 8 ? 4 : 1)))
+__attribute__((amdgpu_waves_per_eu((METRIC == 5 ? DP / 4 : METRIC == 4 ? DP / 2 : DP) <= 160 && R <= 8 ? 4 : 1)))
 cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
             int n_qt, float* __restrict__ out_v, int* __restrict__ out_i, int abl,
             uint32_t* gthr, int gk, int xsw) {
@@ -128,10 +137,12 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   // after the first tiles, bit1 = no selection epilogue, bit3 = staging
   // pieces always of an L2-resident tile, bit4 = no workgroup barrier (own
   // vmcnt wait only).  0 in production.
-  // fp16 operands: METRIC 4 on the 16x16x32 layout
+  // fp16 operands: METRIC 4 on the 16x16x32 layout; int8 codes: METRIC 5 on
+  // v_mfma_i32_16x16x64_i8, the same fragment layout with 64 dims per MFMA
   constexpr bool F16 = METRIC == 4;
-  constexpr bool TEC = METRIC == 4 && KNN_M4_TE_CACHE;
-  constexpr int DPF = F16 ? DP / 2 : DP;    // payload floats per row
+  constexpr bool I8 = METRIC == 5;
+  constexpr bool TEC = (F16 || I8) && KNN_M4_TE_CACHE;
+  constexpr int DPF = I8 ? DP / 4 : (F16 ? DP / 2 : DP);  // payload floats per row
   constexpr int RSF = DPF + 4;              // row stride (floats), HBM and LDS
   constexpr int TPB = res_tpb<METRIC>();    // 32-row sub-tiles per staged tile
   constexpr int TBY = kTR * TPB * RSF * 4;  // tile bytes
@@ -152,7 +163,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   // METRIC 3 (bf16x3 on 16x16x32) and 4 (fp16 on 16x16x32): lane l holds
   // queries wv*32 + qb*16 + (l&15), qb = 0, 1, against rows 4*(l>>4) + i of
   // each 16-row block
-  constexpr bool M16 = METRIC == 3 || METRIC == 4;
+  constexpr bool M16 = METRIC == 3 || METRIC == 4 || I8;
   constexpr int QB = 2;                    // 16-query blocks per wave (M16)
   constexpr int QW = M16 ? 16 * QB : 32;   // queries per wave
   const int c16 = lane & 15, g16 = lane >> 4;
@@ -164,7 +175,8 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   // qh dims 16t+8h..16t+8h+7, float4 DP/16+t the same dims of ql.
   // METRIC 4: fp16 -2q (the train set's power-of-two scale), float4 qb*(DP/32)+ks
   // = dims 32ks + 8*g16 .. +7 of query block qb.
-  constexpr int NQF = METRIC == 1 ? 1 : (F16 ? QB * DP / 32 : DP / 8);
+  // METRIC 5: int8 codes, float4 qb*(DP/64)+ks = dims 64ks + 16*g16 .. +15
+  constexpr int NQF = METRIC == 1 ? 1 : (I8 ? QB * DP / 64 : (F16 ? QB * DP / 32 : DP / 8));
   float4 qf[NQF];
   if constexpr (METRIC != 1) {
     // Loaded with inline asm (loads + their vmcnt(0) in one statement): with
@@ -178,7 +190,10 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int c = c0 + u < NQF ? c0 + u : c0;
-        if constexpr (F16) {
+        if constexpr (I8) {
+          const int ks = c % (DP / 64), qb = c / (DP / 64);
+          p[u] = Q32 + (qb0 + 16 * qb) * (DP / 4) + 16 * ks + 4 * g16;
+        } else if constexpr (F16) {
           const int ks = c % (DP / 32), qb = c / (DP / 32);
           p[u] = Q32 + (qb0 + 16 * qb) * (DP / 2) + 16 * ks + 4 * g16;
         } else if constexpr (M16) {
@@ -251,14 +266,19 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
           : (uint32_t)(qg * (4 * kGthrSlots));
   const uint32_t* gslot = gthr + (gk ? (split & 7) : (split & 3));
   float tq[NQL], te[NQL];
+  int tn[NQL];  // int8: i8_neg_half(te), the filter on the accumulators
 #pragma unroll
-  for (int b = 0; b < NQL; ++b) tq[b] = te[b] = KNN_INF_F;
+  for (int b = 0; b < NQL; ++b) {
+    tq[b] = te[b] = KNN_INF_F;
+    tn[b] = INT_MIN;
+  }
   uint32_t last_pub = kKeyInf;
   int x_ops = 0, x_age = -1;  // ops of the pending exchange, tiles since it
 
   const int my_nt = split < n_tiles ? (n_tiles - split + S - 1) / S : 0;
   constexpr bool PIPE = TEC && KNN_M4_PIPE && DP <= 192;  // DP 256: no registers to spare
-  f32x4 accp[2][QB];  // PIPE: the previous sub-tile's accumulators
+  using AccT = std::conditional_t<I8, i32x4, f32x4>;
+  AccT accp[2][QB];  // PIPE: the previous sub-tile's accumulators
   int rowp = 0;
   bool havep = false;
 
@@ -385,13 +405,78 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       // the quad's shared filter, refreshed once per staged tile (a stale,
       // larger value only admits more insertions)
 #pragma unroll
-      for (int b = 0; b < NQL; ++b) te[b] = __builtin_fminf(quad_min(thr[b]), tq[b]);
+      for (int b = 0; b < NQL; ++b) {
+        te[b] = __builtin_fminf(quad_min(thr[b]), tq[b]);
+        if constexpr (I8) tn[b] = i8_neg_half(te[b]);
+      }
     }
 #pragma unroll
     for (int sub = 0; sub < TPB; ++sub) {
     const float* base = lds + cur * BUFF + sub * kTR * RSF;
 
-    if constexpr (M16) {
+    if constexpr (I8) {
+      // int8 codes on v_mfma_i32_16x16x64_i8, exact: the accumulators start
+      // at -ceil(||k||^2 / 2) (the pad of row 4g carries rows 4g .. 4g+3)
+      // and end at q.k - ceil(||k||^2 / 2); one MFMA per 64 dims
+      i32x4 acc[2][QB];
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        const i32x4 sd = __builtin_bit_cast(i32x4, *(const float4*)(base + (rb * 16 + 4 * g16) * RSF + SEED));
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) acc[rb][qb] = sd;
+      }
+      const int g16s = g16 ^ (xsw ? xh_swz(c16) : 0);
+      // every A fragment of the sub-tile (DP / 32 reads) is read before its
+      // MFMAs, fenced (KNN_I8_SCHED): the registers are there (the query
+      // image is half the fp16 one), and the compiler's own schedule would
+      // wait on each read just before its two MFMAs
+      i32x4 af[DP / 64][2];
+#pragma unroll
+      for (int ks = 0; ks < DP / 64; ++ks)
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+          af[ks][rb] = __builtin_bit_cast(
+              i32x4, *(const float4*)(base + (rb * 16 + c16) * RSF + 16 * ks + 4 * g16s));
+#if KNN_I8_SCHED
+      __builtin_amdgcn_sched_barrier(0);
+#endif
+#pragma unroll
+      for (int ks = 0; ks < DP / 64; ++ks) {
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          const i32x4 a = af[ks][rb];
+#pragma unroll
+          for (int qb = 0; qb < QB; ++qb) {
+            const i32x4 b = __builtin_bit_cast(i32x4, qf[qb * (DP / 64) + ks]);
+            acc[rb][qb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, acc[rb][qb], 0, 0, 0);
+          }
+        }
+      }
+      const int row0 = (t * TPB + sub) * kTR + 4 * g16;
+      if constexpr (PIPE) {
+        if (!(abl & 2)) {
+          if (havep) {
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb)
+              select_quad_i8<R>(accp[0][qb], accp[1][qb], rowp, L[qb], I[qb], te[qb], tn[qb]);
+          }
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb) accp[rb][qb] = acc[rb][qb];
+          rowp = row0;
+          havep = true;
+        } else if (acc[0][0][0] == 12345 && acc[1][1][3] == 12345) {
+          thr[0] = (float)acc[0][1][2];  // keep the accumulators live
+        }
+      } else if (!(abl & 2)) {
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb)
+          select_quad_i8<R>(acc[0][qb], acc[1][qb], row0, L[qb], I[qb], te[qb], tn[qb]);
+      } else if (acc[0][0][0] == 12345 && acc[1][1][3] == 12345) {
+        thr[0] = (float)acc[0][1][2];  // keep the accumulators live
+      }
+    } else if constexpr (M16) {
       // bf16x3 on v_mfma_f32_16x16x32_bf16: 2 row blocks x 2 query blocks of
       // 16; lane l: A = row rb*16 + (l&15), B = query qb*16 + (l&15), k-group
       // l>>4; D = rows rb*16 + 4(l>>4) + i, column l&15
@@ -550,8 +635,12 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   if constexpr (PIPE) {
     if (havep) {
 #pragma unroll
-      for (int qb = 0; qb < QB; ++qb)
-        select_quad_te<R>(accp[0][qb], accp[1][qb], rowp, L[qb], I[qb], te[qb]);
+      for (int qb = 0; qb < QB; ++qb) {
+        if constexpr (I8)
+          select_quad_i8<R>(accp[0][qb], accp[1][qb], rowp, L[qb], I[qb], te[qb], tn[qb]);
+        else
+          select_quad_te<R>(accp[0][qb], accp[1][qb], rowp, L[qb], I[qb], te[qb]);
+      }
     }
   }
 
@@ -587,7 +676,8 @@ static void with_M(int M, F f) {
   else if (M == 1) f(std::integral_constant<int, 1>{});
   else if (M == 2) f(std::integral_constant<int, 2>{});
   else if (M == 3) f(std::integral_constant<int, 3>{});
-  else f(std::integral_constant<int, 4>{});
+  else if (M == 4) f(std::integral_constant<int, 4>{});
+  else f(std::integral_constant<int, 5>{});
 }
 
 template <int DP, int R, int METRIC, int NW>
@@ -599,13 +689,15 @@ static void launch_res(const CandLaunch& c, hipStream_t s) {
 }
 
 // Instantiated variants: R in {4, 8, 16}; METRIC 0/2 with NW in {4, 8};
-// METRIC 4 also with NW = 16 (512 queries share each staged tile);
+// METRIC 4 also with NW = 16 (512 queries share each staged tile); METRIC 5
+// (int8) with R = 4, NW = 8 at DP % 64 == 0;
 // METRIC 1 (L1, not perf-graded) with NW = 4 and R in {8, 16}; METRIC 2
 // needs DP % 16 == 0.
 template <int DP, int R, int M, int NW>
 constexpr bool res_variant() {
   return (M != 2 || DP % 16 == 0) && (M != 1 || (NW == 4 && R != 4)) &&
-         (M < 3 || (DP % 32 == 0 && R == 4 && (NW == 8 || M == 4))) && (NW != 16 || M == 4);
+         (M < 3 || (DP % 32 == 0 && R == 4 && (NW == 8 || M == 4))) && (NW != 16 || M == 4) &&
+         (M != 5 || (DP % 64 == 0 && NW == 8));
 }
 
 template <int DP>

@@ -430,6 +430,38 @@ __device__ __forceinline__ void select_quad_te(const f32x4& a, const f32x4& b, i
   }
 }
 
+// int8 kernel (metric 5): the accumulators hold acc = q.k - ceil(||k||^2 / 2)
+// (exact int32), the proxy is -2 acc = ||k||^2 - 2 q.k (+1 for an odd
+// ||k||^2): a row beats the quad filter te (an even integer or +inf) iff
+// acc > -te / 2, so the filter runs on the accumulators as they stand (a
+// max-tree, no per-value conversion); only an insertion forms the proxy.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ int i8_neg_half(float te) {
+  // -te/2 as an int (te: even integers, +inf -> INT_MIN: every row passes)
+  return te > 3.0e38f ? INT_MIN : (int)(-0.5f * te);
+}
+// tn = i8_neg_half(te), kept by the caller (refreshed with te per tile):
+// the no-insertion case is 4 v_max3 + 1 compare per call.
+template <int R>
+__device__ __forceinline__ void select_quad_i8(const i32x4& a, const i32x4& b, int row0,
+                                               float (&L)[R], int (&I)[R], float& te, int& tn) {
+  const int m1 = max(max(a[0], a[1]), a[2]);
+  const int m2 = max(max(a[3], b[0]), b[1]);
+  const int m3 = max(max(b[2], b[3]), m1);
+  const int mx = max(m2, m3);
+  if (mx > tn) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int v = i < 4 ? a[i] : b[i - 4];
+      if (v > tn) {
+        list_insert<R>(L, I, (float)(-2 * v), row_at(row0, i < 4 ? i : 16 + i - 4));
+        te = __builtin_fminf(te, L[R - 1]);
+        tn = i8_neg_half(te);
+      }
+    }
+  }
+}
+
 // Lists are stored [query][split][half][R] so a query's 2S lists are contiguous.
 template <int R>
 __device__ __forceinline__ void write_lists(float* __restrict__ out_v, int* __restrict__ out_i,

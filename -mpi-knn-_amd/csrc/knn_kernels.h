@@ -13,7 +13,7 @@ constexpr int kMaxUnion = 1024;  // max candidates kept per query across all lis
 constexpr int kSortN = 2048;     // rows per exact-rescan chunk / reduce block
 constexpr int kMaxK = 1000;      // largest k served (k+1 <= kMaxUnion)
 constexpr int kStreamDC = 32;    // dims per LDS chunk in the large-d kernel
-constexpr int kRowAlign = 128;   // train rows are padded to a multiple of this
+constexpr int kRowAlign = 256;   // train rows are padded to a multiple of this (<= one staged tile)
 
 enum { MODE_SINGLE = 0, MODE_PARTIAL = 1 };
 
@@ -147,6 +147,9 @@ struct ProxyScale {
   const float* valid;
   double ue, up;
   bool f16 = false;
+  // int8 pass: the per-dimension code centres (queries are coded
+  // clamp(rint(q 2^s - cent), -128, 127); the merge measures the rounding)
+  const double* i8c = nullptr;
 };
 void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int R,
                          const TrainDev& t, const double* Q64, int64_t m, int W, int C,
@@ -193,6 +196,18 @@ void launch_large_k(int metric, const TrainDev& t, const double* Q64, int64_t m,
                     int class_cnt, unsigned char* scratch, int64_t per_wg, int nwg,
                     const Sink& sink, hipStream_t s);
 void launch_fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t s);
+// int8 images (kernel metric 5, knn_prep.hip): train values x = (cent_i + k) /
+// 2^s with integer codes k in [-128, 127].  grid_stats: per-dim min | max
+// (out[2d]) and the largest fractional bit count (frac, atomicMax) of the
+// train values; partial holds col_mean_blocks(n) x 2d doubles.
+void launch_grid_stats(const double* X64, int64_t n, int d, double* partial, double* out,
+                       unsigned* frac, hipStream_t s);
+void launch_prep_i8_train(const double* X64, const double* cent, int64_t n, int d, int DP,
+                          int64_t n_pad, int s, signed char* out, unsigned* codes_max,
+                          hipStream_t st);
+void launch_prep_i8_queries(const double* Q64, const double* cent, int64_t m, int d, int DP,
+                            int64_t m_pad, int s, signed char* out, float* valid, hipStream_t st);
+int pad_dim_i8(int d);  // padded dim of the int8 kernel (a multiple of 64, <= 256), -1 if none
 // The reference's exact neighbour order on exact distance ties (knn_select.hip,
 // "reference tie order"): libstdc++ std::sort (introsort) emulated over all
 // n exact distances of each listed query, restricted to the ranges that

@@ -343,6 +343,145 @@ void launch_prep_half_queries(const double* Q64, const double* mu, int64_t m, in
                      d, DP, m_pad, jx, out, valid);
 }
 
+// ---------------------------------- int8 images (kernel metric 5, d <= 256)
+// Integer-coded data (e.g. SIFT-like byte features scaled by a power of two,
+// the reference's CSV of k/256 values): every train value is x = (c_i + k) /
+// 2^s with an integer code k in [-128, 127] per dimension i.  Then q.x on
+// v_mfma_i32_16x16x64_i8 is exact (int32 accumulation), twice the fp16 MFMA
+// rate per element.
+//
+// grid_stats: per-dim min / max (fp64) and the largest number of fractional
+// bits of any value (x = odd * 2^lsb -> max(0, -lsb)); two stages.
+__device__ __forceinline__ int frac_bits(double v) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const int e = (int)((b >> 52) & 0x7FF);
+  const unsigned long long mant = (b & 0xFFFFFFFFFFFFFull) | (e ? (1ull << 52) : 0ull);
+  if (mant == 0) return 0;                        // +-0
+  if (e == 0x7FF) return 4096;                    // non-finite (refused elsewhere)
+  const int lsb = (e ? e : 1) - 1075 + __builtin_ctzll(mant);
+  return lsb < 0 ? -lsb : 0;
+}
+
+__global__ void __launch_bounds__(256)
+grid_stats_kernel(const double* __restrict__ X64, int64_t n, int d, int64_t rpb,
+                  double* __restrict__ partial, unsigned* __restrict__ frac) {
+  // partial: [nb][2][d] (min | max)
+  const int64_t r0 = (int64_t)blockIdx.x * rpb;
+  const int64_t r1 = r0 + rpb < n ? r0 + rpb : n;
+  int fb = 0;
+  for (int c = threadIdx.x; c < d; c += 256) {
+    double lo = KNN_INF_D, hi = -KNN_INF_D;
+    for (int64_t r = r0; r < r1; ++r) {
+      const double x = X64[r * d + c];
+      lo = fmin(lo, x);
+      hi = fmax(hi, x);
+      fb = max(fb, frac_bits(x));
+    }
+    partial[((int64_t)blockIdx.x * 2) * d + c] = lo;
+    partial[((int64_t)blockIdx.x * 2 + 1) * d + c] = hi;
+  }
+  fb = wave_max_i(fb);
+  if ((threadIdx.x & 63) == 0 && fb) atomicMax(frac, (unsigned)fb);
+}
+
+__global__ void grid_stats_final_kernel(const double* __restrict__ partial, int nb, int d,
+                                        double* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= d) return;
+  double lo = KNN_INF_D, hi = -KNN_INF_D;
+  for (int b = 0; b < nb; ++b) {
+    lo = fmin(lo, partial[(int64_t)(2 * b) * d + c]);
+    hi = fmax(hi, partial[(int64_t)(2 * b + 1) * d + c]);
+  }
+  out[c] = lo;
+  out[d + c] = hi;
+}
+
+void launch_grid_stats(const double* X64, int64_t n, int d, double* partial, double* out,
+                       unsigned* frac, hipStream_t s) {
+  const int nb = col_mean_blocks(n);
+  const int64_t rpb = (n + nb - 1) / nb;
+  hipLaunchKernelGGL(grid_stats_kernel, dim3(nb), dim3(256), 0, s, X64, n, d, rpb, partial, frac);
+  hipLaunchKernelGGL(grid_stats_final_kernel, dim3((d + 255) / 256), dim3(256), 0, s, partial, nb,
+                     d, out);
+}
+
+// Train rows: [int8 codes (DP bytes, 16-B chunks at (c >> 4) ^ xh_swz(row)) |
+// 4 int32], codes k = x 2^s - c_i; the int32 of row 4g + j (in the pad of
+// row 4g, j = 0..3) is -ceil(||k||^2 / 2), the accumulator seed: the kernel
+// ends at dot(q, k) - ceil(||k||^2 / 2) = -(proxy + (||k||^2 & 1)) / 2 with
+// proxy = ||k||^2 - 2 q.k, i.e. it ranks by proxy + (0 or 1).  Pad rows:
+// INT_MIN (never selected).  codes_max receives max ||k||^2.
+__global__ void __launch_bounds__(256)
+prep_i8_train_kernel(const double* __restrict__ X64, const double* __restrict__ cent, int64_t n,
+                     int d, int DP, int64_t n_pad, int s, signed char* __restrict__ out,
+                     unsigned* __restrict__ codes_max) {
+  const int row_bytes = DP + 16;
+  const int lane = threadIdx.x & 63;
+  const int64_t wstride = (int64_t)gridDim.x * 4;
+  unsigned mx = 0;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n_pad; row += wstride) {
+    int q2 = 0;
+    const int cx = xh_swz((int)(row & 15)) << 4;
+    for (int c = lane; c < DP; c += 64) {
+      int k = 0;
+      if (row < n && c < d) {
+        k = (int)__builtin_rint(__builtin_ldexp(X64[row * d + c], s) - cent[c]);
+        q2 += k * k;
+      }
+      out[row * row_bytes + (c ^ cx)] = (signed char)k;
+    }
+    q2 = wave_sum_i(q2);
+    mx = max(mx, (unsigned)q2);
+    const int seed = row < n ? -((q2 + 1) >> 1) : INT_MIN;
+    // seeds of rows 4g .. 4g+3 in the pad of row 4g (n_pad % 4 == 0): every
+    // row writes its own slot of its group leader's pad
+    if (lane == 0) ((int*)(out + (row & ~3ll) * row_bytes + DP))[row & 3] = seed;
+  }
+  if (lane == 0 && mx) atomicMax(codes_max, mx);
+}
+
+void launch_prep_i8_train(const double* X64, const double* cent, int64_t n, int d, int DP,
+                          int64_t n_pad, int s, signed char* out, unsigned* codes_max,
+                          hipStream_t st) {
+  int64_t blocks = (n_pad + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(prep_i8_train_kernel, dim3((unsigned)blocks), dim3(256), 0, st, X64, cent, n,
+                     d, DP, n_pad, s, out, codes_max);
+}
+
+// Query rows: int8 codes clamp(rint(q 2^s - c_i), -128, 127) (DP bytes,
+// plain row-major).  A value off the train set's grid or beyond the code
+// range is rounded / saturated; the merge rebuilds the same code, measures
+// the query's coding error and widens its bound by it (merge_rerank_kernel).
+// Rows launch_query_check marked invalid get zero operands.
+__global__ void __launch_bounds__(256)
+prep_i8_queries_kernel(const double* __restrict__ Q64, const double* __restrict__ cent, int64_t m,
+                       int d, int DP, int64_t m_pad, int s, signed char* __restrict__ out,
+                       float* __restrict__ valid) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wstride = (int64_t)gridDim.x * 4;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < m_pad; row += wstride) {
+    const bool use = row < m && valid[row] > 0.0f;
+    for (int c = lane; c < DP; c += 64) {
+      int k = 0;
+      if (use && c < d) {
+        const double y = __builtin_ldexp(Q64[row * d + c], s) - cent[c];
+        k = (int)__builtin_fmin(__builtin_fmax(__builtin_rint(y), -128.0), 127.0);
+      }
+      out[row * DP + c] = (signed char)k;
+    }
+  }
+}
+
+void launch_prep_i8_queries(const double* Q64, const double* cent, int64_t m, int d, int DP,
+                            int64_t m_pad, int s, signed char* out, float* valid, hipStream_t st) {
+  int64_t blocks = (m_pad + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(prep_i8_queries_kernel, dim3((unsigned)blocks), dim3(256), 0, st, Q64, cent, m,
+                     d, DP, m_pad, s, out, valid);
+}
+
 __global__ void fill_i32_kernel(int32_t* p, int64_t n, int32_t v) {
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256)
     p[e] = v;

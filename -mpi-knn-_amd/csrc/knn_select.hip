@@ -262,6 +262,20 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
       E = f_err * (t.x2max + 2.0 * (qn + dq) * (xm + t.dxmax) * 1.001) + 3.01 * 0x1p-24 * t.x2max +
           2.0 * (qn * t.dxmax + dq * (xm + t.dxmax)) * 1.001 + 1e-300;
     }
+    if (METRIC == 0 && ps.i8c) {
+      // int8 codes: the query's code k_q = clamp(rint(Q), -128, 127) of
+      // Q = q 2^s - cent (rebuilt here exactly as prep_i8_queries_kernel
+      // does); with delta = Q - k_q, |qa + proxy - d^2| gains
+      // 2 |delta . k_x| 4^-s <= 2 ||delta|| 2^-s sqrt(x2max) (value units)
+      double dq2 = 0.0;
+      for (int c = lane; c < d; c += 64) {
+        const double y = __builtin_ldexp(qv[c], t.jx) - ps.i8c[c];
+        const double r = __builtin_fmin(__builtin_fmax(__builtin_rint(y), -128.0), 127.0);
+        dq2 += (y - r) * (y - r);
+      }
+      const double dq = __builtin_sqrt(wave_sum_d(dq2) * (1.0 + 1e-12)) * (1.0 + 1e-12);
+      E += 2.0 * __builtin_ldexp(dq, -t.jx) * __builtin_sqrt(t.x2max) * 1.001;
+    }
     // proxies are in scaled units (operands 2^jx (x - mu), knn_prep.hip):
     // unscale exactly; operand values outside the format's normal range add
     // absolute error terms (ue per element, up per product, scaled units)

@@ -185,14 +185,21 @@ int knn_last_geometry(knn_ctx* ctx, int64_t out[4]);
 
 /* Candidate-pass precision for L2 (the result is the exact fp64 top-k in
  * every mode; this only selects how candidates are found):
- *   AUTO (default): fp16 for batches of >= 4096 queries at d <= 256 (until
- *         a batch of this train set leaves > 1/16 of its queries to the
- *         rescan), else bf16x3 (d > 256 on the streamed kernel);
+ *   AUTO (default): for batches of >= 4096 queries at d <= 256, int8 when
+ *         the train set is integer-coded (every value c / 2^s with the
+ *         codes of each dimension spanning <= 255, e.g. byte features),
+ *         else fp16 (either until a batch of this train set leaves > 1/16
+ *         of its queries to the rescan); otherwise bf16x3 (d > 256 on the
+ *         streamed kernel);
  *   FP32: v_mfma_f32_32x32x2_f32 on fp32 copies;
  *   BF16X3: q.x as qh.xh + ql.xh + qh.xl on bf16 MFMA
  *           (hi/lo bf16 split of the fp64 values, ~2^-16 relative error);
  *   FP16: q.x on v_mfma_f32_16x16x32_f16 with both operands in fp16 under
  *         power-of-two scales (~2^-10 relative error), d <= 256.
+ * The int8 pass (kernel path 5) is exact: v_mfma_i32_16x16x64_i8 on the
+ * codes, centred per dimension; a query off the train set's grid or beyond
+ * the codes' range goes to the exact rescan.  It has no precision mode of
+ * its own (tuning key "i8").
  * Environment override at knn_create: KNN_PRECISION=fp32|bf16x3|fp16. */
 #define KNN_PRECISION_AUTO 0
 #define KNN_PRECISION_FP32 1
@@ -200,7 +207,8 @@ int knn_last_geometry(knn_ctx* ctx, int64_t out[4]);
 #define KNN_PRECISION_FP16 3
 int knn_set_precision(knn_ctx* ctx, int mode);
 /* Candidate kernel flavour of the last search: 0 fp32 L2, 1 fp32 L1, 2 bf16x3
- * L2 (32x32x16 MFMA), 3 bf16x3 L2 (16x16x32), 4 fp16 L2 (16x16x32). */
+ * L2 (32x32x16 MFMA), 3 bf16x3 L2 (16x16x32), 4 fp16 L2 (16x16x32), 5 int8
+ * L2 (16x16x64, exact integer dot products). */
 int knn_last_candidate_path(knn_ctx* ctx);
 /* Name of the last candidate kernel launched, as rocprofv3 reports it
  * without namespace, spaces and argument list (e.g. "cand_kernel<128,4,4,8>"). */
@@ -211,7 +219,8 @@ const char* knn_last_kernel_name(knn_ctx* ctx);
  * candidate workgroup (4 or 8; 32 queries per wave), "ablate" (bits 0/1:
  * timing-only kernel ablations, results invalid; bit 2: no per-query global
  * threshold exchange, results stay exact); -1 = auto for "fp16" (fp16
- * candidate pass: 0 off, 1 on), "mfma16" (bf16x3 on the 16x16x32 layout: 0
+ * candidate pass: 0 off, 1 on), "i8" (the int8 candidate pass where the
+ * train set is integer-coded: 0 off, 1 on at every batch size), "mfma16" (bf16x3 on the 16x16x32 layout: 0
  * off, 1 on), "s3q" (the fp16 d > 256 kernel on 16x16x32: 0 off, 1 on) and
  * "gk" (what the global threshold exchange publishes: 0 the lists' R-th
  * entries (resident kernel) / no exchange (S3), K = 1..16 the K-th smallest

@@ -161,13 +161,20 @@ def test_cfg2_full(knn):
     clf = knn.Classifier(0)
     clf.set_train_device(X.data_ptr(), lab.data_ptr(), n, d, C, keep=(X, lab))
     got, idx, dist, flags = classify(knn, clf, Q, k)
-    assert clf.last_candidate_path() == 4, "cfg2 should run the fp16 candidate pass"
+    # 8-bit grid data (bench.synth's byte features): the int8 pass, exact
+    assert clf.last_candidate_path() == 5, "cfg2 should run the int8 candidate pass"
+    assert clf.last_rescan_count() * 64 <= m
     lab_all = lab.cpu().numpy()
     check_properties(X, lab_all, Q, k, got, idx, dist, np.arange(m))
     check_oracle(X, lab_all, Q, k, got, idx, dist, np.arange(0, m, m // 32))
     check_optimal(X, Q, k, dist, np.arange(0, m, m // 512))
     check_tie_votes(knn, X, lab_all, Q, k, got, flags)
-    # the other candidate paths give the same exact answer
+    # the other candidate paths give the same exact answer: fp16, bf16x3, fp32
+    clf.set_tuning("i8", 0)
+    goth, _, disth, _ = classify(knn, clf, Q, k)
+    assert clf.last_candidate_path() == 4
+    np.testing.assert_array_equal(goth, got)
+    assert (disth.view(np.int64) == dist.view(np.int64)).all()
     clf.set_precision(knn.PRECISION_BF16X3)
     for m16, path in ((1, 3), (0, 2)):  # bf16x3 on 16x16x32, then on 32x32x16
         clf.set_tuning("mfma16", m16)

@@ -34,19 +34,23 @@ def knn():
     return mod
 
 
-@pytest.fixture(scope="module", params=["auto", "fp32", "m16", "fp16", "fp16w"])
+@pytest.fixture(scope="module", params=["auto", "fp32", "m16", "fp16", "fp16w", "i8"])
 def clf(knn, request):
-    """Every parity test runs with the default candidate path (AUTO: fp16 for
-    batches of >= 4096 queries at d <= 256, else bf16x3 on 32x32x16 for L2),
-    with the fp32 path forced, with bf16x3 on the 16x16x32 MFMA layout forced,
-    with the fp16 path forced (every batch size), and with the fp16 path's
-    alternative forms (fp16w: the S3 kernel on 32x32x16 above 256 dims, the
-    resident kernel publishing list thresholds, gk = 0)."""
+    """Every parity test runs with the default candidate path (AUTO: int8 for
+    integer-coded data and fp16 otherwise for batches of >= 4096 queries at
+    d <= 256, else bf16x3 on 32x32x16 for L2), with the fp32 path forced,
+    with bf16x3 on the 16x16x32 MFMA layout forced, with the fp16 path forced
+    (every batch size), with the fp16 path's alternative forms (fp16w: the S3
+    kernel on 32x32x16 above 256 dims, the resident kernel publishing list
+    thresholds, gk = 0), and with the int8 path forced wherever the data are
+    integer-coded (i8; other data take the AUTO path)."""
     c = knn.Classifier(0)
     c.set_precision({"auto": knn.PRECISION_AUTO, "fp32": knn.PRECISION_FP32,
                      "m16": knn.PRECISION_BF16X3, "fp16": knn.PRECISION_FP16,
-                     "fp16w": knn.PRECISION_FP16}[request.param])
+                     "fp16w": knn.PRECISION_FP16, "i8": knn.PRECISION_AUTO}[request.param])
     c.set_tuning("mfma16", 1 if request.param == "m16" else -1)
+    if request.param == "i8":
+        c.set_tuning("i8", 1)
     if request.param == "fp16w":
         c.set_tuning("s3q", 0)
         c.set_tuning("gk", 0)
@@ -254,6 +258,58 @@ def test_sorted_train_rows(clf, knn):
     tr, lab, te = _mix(rng, 12000, 256, 32, 3, spread=3.0)
     order = np.argsort(lab, kind="stable")
     run_case(clf, knn, np.ascontiguousarray(tr[order]), lab[order].copy(), te, 20, 0, 3)
+
+
+def _grid_codes(rng, n, m, d, classes, lo=0, hi=255, scale=256.0):
+    """SIFT-like byte features on the grid (code) / scale, codes in [lo, hi]."""
+    centres = rng.uniform(lo + 40, hi - 40, (classes, d))
+    lab = rng.integers(0, classes, n + m).astype(np.int32)
+    X = np.clip(np.rint(centres[lab] + 25 * rng.standard_normal((n + m, d))), lo, hi) / scale
+    return X[:n].copy(), lab[:n].copy(), X[n:].copy()
+
+
+@pytest.mark.parametrize("d", [32, 64, 96, 128, 200, 256])
+def test_int8_codes(knn, d):
+    """The int8 pass (v_mfma_i32_16x16x64_i8 on the data's integer codes,
+    exact) against the oracle on 8-bit grid data -- the full byte range
+    (codes 0..255, centre 128) -- forced and in AUTO at 4096+ queries; every
+    padded width (d = 96 and 200 pad to 128 / 256)."""
+    rng = np.random.default_rng(80 + d)
+    tr, lab, te = _grid_codes(rng, 9000, 4200, d, 7)
+    assert tr.min() == 0.0 and tr.max() == 255 / 256.0
+    for mode in ("forced", "auto"):
+        c = knn.Classifier(0)
+        if mode == "forced":
+            c.set_tuning("i8", 1)
+        run_case(c, knn, tr, lab, te, 10, 0, 7)
+        assert c.last_candidate_path() == 5, mode
+        assert c.last_kernel_name().startswith("cand_kernel<%d,4,5,8>" % ((d + 63) // 64 * 64))
+        assert c.last_rescan_count() * 16 <= te.shape[0]
+        c.close()
+
+
+def test_int8_off_grid_queries(knn):
+    """Queries the int8 codes cannot hold exactly -- off the train grid,
+    beyond the code range -- are coded rounded / saturated and their measured
+    coding error widens the bound (far-out ones fail certification and take
+    the exact rescan); integer data at scale 1 with negative values; k = 50.
+    Exact answers."""
+    rng = np.random.default_rng(91)
+    tr, lab, te = _grid_codes(rng, 6000, 300, 48, 5, lo=-100, hi=120, scale=1.0)
+    te[:5, 3] += 0.5          # off the integer grid
+    te[5:9, 7] = 121.0 + 200  # beyond the codes the centre leaves room for
+    c = knn.Classifier(0)
+    c.set_tuning("i8", 1)
+    got, want, flags = run_case(c, knn, tr, lab, te, 50, 0, 5)
+    assert c.last_candidate_path() == 5
+    assert (flags[5:9] & knn.FLAG_EXACT_RESCAN).all()
+    # a train set off any 8-bit grid: the int8 pass is not available, the
+    # forced request falls back to the other paths (still exact)
+    tr2 = tr.copy()
+    tr2[17, 2] += 1e-3
+    run_case(c, knn, tr2, lab, te, 10, 0, 5)
+    assert c.last_candidate_path() != 5
+    c.close()
 
 
 def test_k_zero_and_errors(clf, knn):
