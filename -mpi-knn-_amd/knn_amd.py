@@ -265,13 +265,14 @@ class Classifier:
         return lib().knn_last_kernel_name(self._h).decode()
 
     def set_precision(self, mode):
-        """PRECISION_AUTO (bf16x3 where supported), PRECISION_FP32, PRECISION_BF16X3.
+        """PRECISION_AUTO (int8 on integer-coded data, else fp16 / bf16x3 by
+        shape, knn_amd.h), PRECISION_FP32, PRECISION_BF16X3, PRECISION_FP16.
         Results are the exact fp64 top-k in every mode."""
         _check(lib().knn_set_precision(self._h, int(mode)))
 
     def set_tuning(self, key, value):
         """Experiment overrides (knn_amd.h): "R", "S", "nw", "ablate", "fp16",
-        "mfma16"; 0 (or -1 where stated) = automatic."""
+        "mfma16", "i8", "gk", "s3q", "xhswz"; 0 (or -1 where stated) = automatic."""
         _check(lib().knn_set_tuning(self._h, key.encode(), int(value)))
 
     def last_candidate_path(self):

@@ -83,6 +83,10 @@ def test_cfg4_100m_train_sharded(knn):
     for p in range(parts):
         r0, r1 = n * p // parts, n * (p + 1) // parts
         c = knn.Classifier(0)
+        # even shards: AUTO (the int8 pass on this 8-bit grid data); odd
+        # shards: the fp16 pass forced -- both candidate kernels at full size
+        if p % 2:
+            c.set_precision(knn.PRECISION_FP16)
         Xs, Ls = X[r0:r1], lab[r0:r1]
         c.set_train_device(Xs.data_ptr(), Ls.data_ptr(), r1 - r0, d, C, idx_offset=r0,
                            keep=(Xs, Ls))
@@ -91,7 +95,7 @@ def test_cfg4_100m_train_sharded(knn):
         c.sync()
         paths.append(c.last_candidate_path())
         c.close()
-    assert paths == [4] * parts, "cfg4 shards should run the fp16 candidate pass"
+    assert paths == [5, 4] * (parts // 2), "shards should run int8 (AUTO, grid data) / fp16 (forced)"
     ol = torch.empty(m, dtype=torch.int32, device=DEV)
     oi = torch.empty((m, k), dtype=torch.int64, device=DEV)
     od = torch.empty((m, k), dtype=torch.float64, device=DEV)
