@@ -653,8 +653,12 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   if (DP <= 256 && kmetric != 1) nw = ctx->tune_nw ? std::min(ctx->tune_nw, 8) : (m >= 4096 ? 8 : 4);
   if (kmetric >= 3) nw = 8;  // (the 16x16 layouts: fp16, bf16x3, int8)
   if (kmetric == 4 && !s3 && ctx->tune_nw) nw = ctx->tune_nw;  // 4, 8 or 16
+  // queries per wave of the resident kernel (int8: 16 x the build's query
+  // blocks); the int8 kernel with 64 queries per wave also runs 4 waves
+  const int qpw = !s3 && DP <= 256 ? cand_queries_per_wave(kmetric, DP) : 32;
+  if (kmetric == 5 && ctx->tune_nw && qpw > 32) nw = ctx->tune_nw;
   if (s3) nw = 8;
-  const int qpb = s3 ? kS3Rows : (DP <= 256 ? 32 * nw : kQPB);
+  const int qpb = s3 ? kS3Rows : (DP <= 256 ? qpw * nw : kQPB);
   const int n_qt = (int)((m + qpb - 1) / qpb);
   const int64_t m_pad = (int64_t)n_qt * qpb;
   const int64_t n_pad3 = (t.n + kS3Rows - 1) / kS3Rows * kS3Rows;
@@ -765,6 +769,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   cl.out_i = (int*)ctx->cand_i.p;
   cl.ablate = ctx->tune_ablate;
   cl.nw = nw;
+  cl.qpb = qpb;
   cl.gthr = use_gthr ? (uint32_t*)ctx->gthr.p : nullptr;
   cl.gk = gk;
   cl.xsw = kmetric == 5 ? 1 : ctx->xh_swz;  // the int8 image is always swizzled
@@ -822,7 +827,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   rb.counts = ctx->d_counts;
   rb.totals = (unsigned long long*)ctx->totals.p;
   // (timing-only ablations leave every query uncertified: no rescan then)
-  const bool abl = ctx->tune_ablate & 11;
+  const bool abl = ctx->tune_ablate & 27;
   launch_rescan(metric, t, dQ, rb, abl ? 0 : cap, W, err_factor(metric, t.DP), sink,
                 abl ? 0 : (int)std::min<int64_t>(m, ctx->cu_count), s);
   // (without the full-scan launch nothing writes this call's counts)

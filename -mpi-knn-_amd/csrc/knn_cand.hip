@@ -27,7 +27,8 @@ namespace knnk {
 
 #define KNN_DECL(v)                                          \
   bool launch_res_##v(const CandLaunch& c, hipStream_t s);   \
-  int blocks_res_##v(int R, int metric, int nw);
+  int blocks_res_##v(int R, int metric, int nw);             \
+  int qpw_res_##v(int metric);
 KNN_DP_LIST(KNN_DECL)
 #undef KNN_DECL
 
@@ -657,6 +658,15 @@ int cand_blocks_per_cu(int metric, int DP, int R, int nw) {
     out = occupancy_of(metric == 1 ? cand_stream_kernel<kStreamDC, 16, 1>
                                    : cand_stream_kernel<kStreamDC, 16, 0>, 256);
   return out;
+}
+
+// queries per wave of the resident kernel serving (metric, DP), from the
+// object that holds that kernel (a variant build's KNN_I8_QB)
+int cand_queries_per_wave(int metric, int DP) {
+#define KNN_CASE(v) if (DP == v) return qpw_res_##v(metric);
+  KNN_DP_LIST(KNN_CASE)
+#undef KNN_CASE
+  return 32;
 }
 
 int cand_tile_rows(int DP) { return DP <= 256 ? kResTileRows : 128; }

@@ -51,6 +51,21 @@ static_assert(KNN_RES_TPB * knnk::kTR == knnk::kResTileRows || KNN_RES_TPB != 2,
 #ifndef KNN_I8_SCHED
 #define KNN_I8_SCHED 1
 #endif
+// int8 kernel: 16-query blocks per wave (2: 32 queries per wave as the fp16
+// kernel; 4: 64 queries, each A fragment read from LDS feeds 4 MFMAs) and
+// the waves-per-SIMD target of the 4-block form (its registers exceed 128)
+// int8 kernel: LDS buffers (2: tile it+1 streams in behind tile it's
+// compute; 3: two tiles of lead -- the int8 tile's compute is half the
+// fp16 one's, too short to cover an HBM fetch)
+#ifndef KNN_I8_NB
+#define KNN_I8_NB 2
+#endif
+#ifndef KNN_I8_QB
+#define KNN_I8_QB 2
+#endif
+#ifndef KNN_I8_WPE
+#define KNN_I8_WPE 2
+#endif
 
 
 namespace knnk {
@@ -61,9 +76,10 @@ __device__ __forceinline__ void wait_barrier() {
 }
 
 // The wait count plus `extra` younger exchange ops (see cand_kernel).
-template <int BASE>
+template <int BASE, int XMAX = 2>
 __device__ __forceinline__ void wait_barrier_x(int extra) {
-  if (extra == 2) wait_barrier<BASE + 2>();
+  if (XMAX >= 3 && extra == 3) wait_barrier<BASE + 3>();
+  else if (extra == 2) wait_barrier<BASE + 2>();
   else if (extra == 1) wait_barrier<BASE + 1>();
   else wait_barrier<BASE>();
 }
@@ -80,6 +96,20 @@ constexpr int kPubEvery = 8;  // tiles between global-threshold exchanges
 __device__ __forceinline__ bool exchange_tile(int it) {
   if (KNN_EARLY_X && it < kPubEvery) return it == 0 || it == 1 || it == 2 || it == 4;
   return (it & (kPubEvery - 1)) == kPubEvery - 1;
+}
+
+// waves per SIMD the resident kernel is compiled for: 4 (<= 128 VGPRs, two
+// 8-wave workgroups per CU) where its registers fit
+template <int DP, int R, int METRIC>
+constexpr int res_wpe() {
+  if (METRIC == 5 && KNN_I8_QB > 2) return KNN_I8_WPE;
+  return (METRIC == 5 ? DP / 4 : METRIC == 4 ? DP / 2 : DP) <= 160 && R <= 8 ? 4 : 1;
+}
+
+// queries per wave: 16 per query block (the 16x16 layouts), 32 otherwise
+template <int METRIC>
+constexpr int res_qpw() {
+  return METRIC == 5 ? 16 * KNN_I8_QB : 32;
 }
 
 template <int METRIC>
@@ -121,7 +151,7 @@ constexpr int res_tpb() {
 // (not for R = 16 lists or DP > 160, whose registers do not fit: spills).
 template <int DP, int R, int METRIC, int NW>
 __global__ void __launch_bounds__(NW * 64)
-__attribute__((amdgpu_waves_per_eu((METRIC == 5 ? DP / 4 : METRIC == 4 ? DP / 2 : DP) <= 160 && R <= 8 ? 4 : 1)))
+__attribute__((amdgpu_waves_per_eu(res_wpe<DP, R, METRIC>())))
 cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
             int n_qt, float* __restrict__ out_v, int* __restrict__ out_i, int abl,
             uint32_t* gthr, int gk, int xsw) {
@@ -147,7 +177,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   constexpr int TPB = res_tpb<METRIC>();    // 32-row sub-tiles per staged tile
   constexpr int TBY = kTR * TPB * RSF * 4;  // tile bytes
   constexpr int NG = (TBY + 1023) / 1024;   // 1-KiB LDS-DMA pieces per tile
-  constexpr int NB = KNN_RES_NB;            // LDS buffers (prefetch distance NB - 1)
+  constexpr int NB = I8 ? KNN_I8_NB : KNN_RES_NB;  // LDS buffers (prefetch distance NB - 1)
   constexpr int BUFF = NG * 256;            // floats per buffer
   constexpr int SEED = METRIC == 1 ? DP + 1 : DPF;  // seed float within a row
   __shared__ __attribute__((aligned(16))) float lds[NB * BUFF];
@@ -164,8 +194,9 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   // queries wv*32 + qb*16 + (l&15), qb = 0, 1, against rows 4*(l>>4) + i of
   // each 16-row block
   constexpr bool M16 = METRIC == 3 || METRIC == 4 || I8;
-  constexpr int QB = 2;                    // 16-query blocks per wave (M16)
+  constexpr int QB = I8 ? KNN_I8_QB : 2;   // 16-query blocks per wave (M16)
   constexpr int QW = M16 ? 16 * QB : 32;   // queries per wave
+  static_assert(QW == res_qpw<METRIC>(), "queries per wave: kernel and host disagree");
   const int c16 = lane & 15, g16 = lane >> 4;
   const int64_t qb0 = (int64_t)qt * (NW * QW) + wv * QW + c16;  // query of block 0 (+16 qb: block qb)
 
@@ -251,9 +282,13 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   // wave's 1-KiB area of gls (16 B per lane); they are read after the next
   // barrier: a plain load into VGPRs would be consumed (or copied) by
   // compiler code before it lands.
-  __shared__ __attribute__((aligned(16))) u32x4 gls[NW * 64];
+  // (64 queries per wave: lane l fetches both halves of query l's slots,
+  // into this wave's 2-KiB area)
+  constexpr int GW = QW > 32 ? 128 : 64;  // gls entries per wave
+  constexpr int XMAX = GW == 128 ? 3 : 2;  // exchange ops in flight at most
+  __shared__ __attribute__((aligned(16))) u32x4 gls[NW * GW];
   const uint32_t gls_addr =
-      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) u32x4*)gls + wv * 1024;
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) u32x4*)gls + wv * GW * 16;
   // An exchange at tile e issues (after that tile's DMA pieces) an atomic
   // (only if some lane improved) and the slot fetch; the barriers of tiles
   // e+1 .. e+PD-1 leave those x ops in flight (counted wait + x), the
@@ -330,11 +365,11 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
         // (other waves' pieces may not have landed: results invalid)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       } else if (ahead >= 2 && PD >= 3) {
-        if (g_hi) wait_barrier_x<2 * G_HI>(extra); else wait_barrier_x<2 * G_LO>(extra);
+        if (g_hi) wait_barrier_x<2 * G_HI, XMAX>(extra); else wait_barrier_x<2 * G_LO, XMAX>(extra);
       } else if (ahead == 1) {
-        if (g_hi) wait_barrier_x<G_HI>(extra); else wait_barrier_x<G_LO>(extra);
+        if (g_hi) wait_barrier_x<G_HI, XMAX>(extra); else wait_barrier_x<G_LO, XMAX>(extra);
       } else {
-        wait_barrier_x<0>(extra);
+        wait_barrier_x<0, XMAX>(extra);
       }
       __builtin_amdgcn_sched_barrier(0);
       // (abl bit 3: the same pieces, always of the split's first tile -- DMA
@@ -346,7 +381,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
           for (int b = 0; b < NQL; ++b) {
             // slots 0-3 as fetched by lane qi, 4-7 by lane qi + 32
             const int qi = M16 ? 16 * b + c16 : j;
-            const u32x4 g0 = gls[wv * 64 + qi], g1 = gls[wv * 64 + qi + 32];
+            const u32x4 g0 = gls[wv * GW + qi], g1 = gls[wv * GW + qi + GW / 2];
             tq[b] = key2f(max(max(max(g0.x, g0.y), max(g0.z, g0.w)),
                               max(max(g1.x, g1.y), max(g1.z, g1.w))));
           }
@@ -358,21 +393,25 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
           uint32_t pk;
           bool pub;
           if constexpr (M16) {
-            float m0, m1;
+            // lane group g16 publishes for query block g16 (QB of the 4)
+            float mb[QB];
             if (gk) {
-              float u[4];
 #pragma unroll
-              for (int e = 0; e < 4; ++e) u[e] = L[0][e];
-              m0 = union_kth<4>(u, gk);
+              for (int b = 0; b < QB; ++b) {
+                float u[4];
 #pragma unroll
-              for (int e = 0; e < 4; ++e) u[e] = L[1][e];
-              m1 = union_kth<4>(u, gk);
+                for (int e = 0; e < 4; ++e) u[e] = L[b][e];
+                mb[b] = union_kth<4>(u, gk);
+              }
             } else {
-              m0 = quad_min(thr[0]);
-              m1 = quad_min(thr[1]);
+#pragma unroll
+              for (int b = 0; b < QB; ++b) mb[b] = quad_min(thr[b]);
             }
-            pk = f2key(g16 == 0 ? m0 : m1);
-            pub = g16 < 2 && pk < last_pub;
+            float mq = mb[QB - 1];
+#pragma unroll
+            for (int b = QB - 2; b >= 0; --b) mq = g16 == b ? mb[b] : mq;
+            pk = f2key(mq);
+            pub = g16 < QB && pk < last_pub;
           } else {
             float m;
             if (gk) {
@@ -396,7 +435,13 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
             x_ops = 2;
           }
           if (pub) last_pub = pk;
-          glds16((const char*)gthr + goff + 16 * h, gls_addr);
+          if constexpr (GW == 128) {
+            glds16((const char*)gthr + goff, gls_addr);
+            glds16((const char*)gthr + goff + 16, gls_addr + 1024);
+            ++x_ops;
+          } else {
+            glds16((const char*)gthr + goff + 16 * h, gls_addr);
+          }
           x_age = 0;
         }
       }
@@ -696,8 +741,8 @@ static void launch_res(const CandLaunch& c, hipStream_t s) {
 template <int DP, int R, int M, int NW>
 constexpr bool res_variant() {
   return (M != 2 || DP % 16 == 0) && (M != 1 || (NW == 4 && R != 4)) &&
-         (M < 3 || (DP % 32 == 0 && R == 4 && (NW == 8 || M == 4))) && (NW != 16 || M == 4) &&
-         (M != 5 || (DP % 64 == 0 && NW == 8));
+         (M < 3 || (DP % 32 == 0 && R == 4 && (NW == 8 || M >= 4))) && (NW != 16 || M == 4) &&
+         (M != 5 || (DP % 64 == 0 && (NW == 8 || (NW == 4 && KNN_I8_QB > 2))));
 }
 
 template <int DP>
@@ -725,6 +770,9 @@ static bool launch_res_dp(const CandLaunch& c, hipStream_t s) {
   bool launched = false;  // false: no instantiated variant (caller reports it)
   with_R(c.R, [&](auto Rc) {
     with_M(c.metric, [&](auto Mc) {
+      // the host's query tile must be this kernel's (nw x queries per
+      // wave): a mismatch would index queries past the operand buffers
+      if (c.qpb != c.nw * res_qpw<Mc.value>()) return;
       if (c.nw == 16) {
         if constexpr (res_variant<DP, Rc.value, Mc.value, 16>())
           launch_res<DP, Rc.value, Mc.value, 16>(c, s), launched = true;
@@ -754,7 +802,8 @@ static bool launch_res_dp(const CandLaunch& c, hipStream_t s) {
 
 #define KNN_DEF(v)                                                                 \
   bool launch_res_##v(const CandLaunch& c, hipStream_t s) { return launch_res_dp<v>(c, s); } \
-  int blocks_res_##v(int R, int metric, int nw) { return blocks_per_cu_res<v>(R, metric, nw); }
+  int blocks_res_##v(int R, int metric, int nw) { return blocks_per_cu_res<v>(R, metric, nw); } \
+  int qpw_res_##v(int metric) { return metric == 5 ? res_qpw<5>() : res_qpw<0>(); }
 KNN_GROUP_DPS(KNN_DEF)
 #undef KNN_DEF
 

@@ -91,6 +91,7 @@ void launch_prep_half_tiled(const double* X64, const double* mu, int64_t n, int 
 bool cand_supported(int DP);
 int cand_tile_rows(int DP);         // train rows per tile of the kernel serving DP
 int cand_blocks_per_cu(int metric, int DP, int R, int nw);  // resident workgroups per CU
+int cand_queries_per_wave(int metric, int DP);  // resident kernel: queries per wave
 
 // metric: 0 = L2 fp32 MFMA, 1 = L1 fp32 VALU, 2 = L2 bf16x3 MFMA (32x32x16),
 // 3 = L2 bf16x3 on 16x16x32, 4 = L2 fp16 on 16x16x32 (see knn_cand_res.hip)
@@ -103,7 +104,9 @@ struct CandLaunch {
   float* out_v;
   int* out_i;
   int ablate;   // timing-only ablation bits (0 in production)
-  int nw;       // resident kernel: waves (x32 queries) per workgroup, 4 or 8
+  int nw;       // resident kernel: waves per workgroup, 4, 8 or 16
+  int qpb;      // resident kernel: queries per workgroup the host laid out (nw x
+                // queries per wave; checked against the kernel before launch)
   uint32_t* gthr;  // resident kernel: per-query global thresholds [m_pad][kGthrSlots] (keys)
   int xsw;         // fp16 (metric 4): the train image's chunks are swizzled (xh_swz)
   int gk;          // what a list group publishes into gthr (see cand_kernel): 0 = the
