@@ -290,6 +290,9 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(KNN_S3
 cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* QT, int nch,
                int n_tiles, int S, int n_qt, float* __restrict__ out_v, int* __restrict__ out_i,
                int abl, int gq, uint32_t* gthr, int gk) {
+#if !KNN_ABLATIONS
+  abl = 0;  // (folds every ablation check below)
+#endif
   static_assert(F16 || !Q16, "the 16x16x32 S3 layout is fp16 only");
   // gthr / gk (Q16 only; null / 0: none): the per-query global threshold of
   // cand_kernel -- at tiles 0, 1, 2, 4 and every 4th tile each workgroup

@@ -43,9 +43,13 @@ static_assert(KNN_RES_TPB * knnk::kTR == knnk::kResTileRows || KNN_RES_TPB != 2,
 #define KNN_RFL 1
 #endif
 // int8 kernel: 32-row sub-tiles per staged tile (8: 256-row tiles, half the
-// barriers per MFMA of 128-row tiles; n_pad is a multiple of kRowAlign = 256)
+// barriers and per-tile work per MFMA of 128-row tiles, and a 256-row lead
+// for the streamed rows; n_pad is a multiple of kRowAlign = 256): cfg2
+// candidate pass 1.636 -> 1.50 ms against 4 (gpurun_out/r3c_ab_*.log), where
+// a third LDS buffer of 128-row tiles measured +4 % and 64 queries per wave
+// +12 %
 #ifndef KNN_I8_TPB
-#define KNN_I8_TPB 4
+#define KNN_I8_TPB 8
 #endif
 // int8 kernel: all A-fragment reads of a sub-tile issued before its MFMAs
 #ifndef KNN_I8_SCHED
@@ -70,6 +74,10 @@ static_assert(KNN_RES_TPB * knnk::kTR == knnk::kResTileRows || KNN_RES_TPB != 2,
 
 namespace knnk {
 
+#if KNN_COUNT_SEL
+__device__ unsigned long long knn_sel_cnt[4];
+#endif
+
 template <int N>
 __device__ __forceinline__ void wait_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
@@ -84,7 +92,10 @@ __device__ __forceinline__ void wait_barrier_x(int extra) {
   else wait_barrier<BASE>();
 }
 
-constexpr int kPubEvery = 8;  // tiles between global-threshold exchanges
+#ifndef KNN_PUB_EVERY
+#define KNN_PUB_EVERY 8
+#endif
+constexpr int kPubEvery = KNN_PUB_EVERY;  // tiles between global-threshold exchanges (power of 2)
 // Early exchanges (KNN_EARLY_X): also at tiles 0, 1, 2 and 4.  The fetch at
 // tile 0 hands a workgroup of a later grid round the thresholds the earlier
 // rounds already published, and the early publishes shorten every list's
@@ -94,7 +105,7 @@ constexpr int kPubEvery = 8;  // tiles between global-threshold exchanges
 #define KNN_EARLY_X 1
 #endif
 __device__ __forceinline__ bool exchange_tile(int it) {
-  if (KNN_EARLY_X && it < kPubEvery) return it == 0 || it == 1 || it == 2 || it == 4;
+  if (KNN_EARLY_X && it < 8 && kPubEvery >= 4) return it == 0 || it == 1 || it == 2 || it == 4;
   return (it & (kPubEvery - 1)) == kPubEvery - 1;
 }
 
@@ -155,6 +166,9 @@ __attribute__((amdgpu_waves_per_eu(res_wpe<DP, R, METRIC>())))
 cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
             int n_qt, float* __restrict__ out_v, int* __restrict__ out_i, int abl,
             uint32_t* gthr, int gk, int xsw) {
+#if !KNN_ABLATIONS
+  abl = 0;  // (folds every ablation check below)
+#endif
 #if KNN_SETPRIO
   // the second-dispatched half of the workgroup at priority 1 (MI355X_MICROARCH
   // "Two waves per SIMD", item 4)
@@ -313,9 +327,19 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   const int my_nt = split < n_tiles ? (n_tiles - split + S - 1) / S : 0;
   constexpr bool PIPE = TEC && KNN_M4_PIPE && DP <= 192;  // DP 256: no registers to spare
   using AccT = std::conditional_t<I8, i32x4, f32x4>;
-  AccT accp[2][QB];  // PIPE: the previous sub-tile's accumulators
+  // PIPE: the previous sub-tile's accumulators; before the first sub-tile
+  // they hold values no filter passes (int8: INT_MIN, fp16: +inf), so the
+  // pipelined selection needs no first-sub-tile check
+  AccT accp[2][QB];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb) {
+      if constexpr (I8) accp[rb][qb] = i32x4{INT_MIN, INT_MIN, INT_MIN, INT_MIN};
+      else accp[rb][qb] = f32x4{KNN_INF_F, KNN_INF_F, KNN_INF_F, KNN_INF_F};
+    }
   int rowp = 0;
-  bool havep = false;
+  SelCount selc;
 
   // ---- staging: this wave's LDS-DMA pieces i = wv, wv+NW, ... of tile t ->
   // buffer b.  The last piece may read past the tile (and past the last row:
@@ -500,24 +524,21 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       const int row0 = (t * TPB + sub) * kTR + 4 * g16;
       if constexpr (PIPE) {
         if (!(abl & 2)) {
-          if (havep) {
 #pragma unroll
-            for (int qb = 0; qb < QB; ++qb)
-              select_quad_i8<R>(accp[0][qb], accp[1][qb], rowp, L[qb], I[qb], te[qb], tn[qb]);
-          }
+          for (int qb = 0; qb < QB; ++qb)
+            select_quad_i8<R>(accp[0][qb], accp[1][qb], rowp, L[qb], I[qb], te[qb], tn[qb], selc);
 #pragma unroll
           for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
             for (int qb = 0; qb < QB; ++qb) accp[rb][qb] = acc[rb][qb];
           rowp = row0;
-          havep = true;
         } else if (acc[0][0][0] == 12345 && acc[1][1][3] == 12345) {
           thr[0] = (float)acc[0][1][2];  // keep the accumulators live
         }
       } else if (!(abl & 2)) {
 #pragma unroll
         for (int qb = 0; qb < QB; ++qb)
-          select_quad_i8<R>(acc[0][qb], acc[1][qb], row0, L[qb], I[qb], te[qb], tn[qb]);
+          select_quad_i8<R>(acc[0][qb], acc[1][qb], row0, L[qb], I[qb], te[qb], tn[qb], selc);
       } else if (acc[0][0][0] == 12345 && acc[1][1][3] == 12345) {
         thr[0] = (float)acc[0][1][2];  // keep the accumulators live
       }
@@ -592,17 +613,14 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       const int row0 = (t * TPB + sub) * kTR + 4 * g16;
       if constexpr (PIPE) {
         if (!(abl & 2)) {
-          if (havep) {
 #pragma unroll
-            for (int qb = 0; qb < QB; ++qb)
-              select_quad_te<R>(accp[0][qb], accp[1][qb], rowp, L[qb], I[qb], te[qb]);
-          }
+          for (int qb = 0; qb < QB; ++qb)
+            select_quad_te<R>(accp[0][qb], accp[1][qb], rowp, L[qb], I[qb], te[qb]);
 #pragma unroll
           for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
             for (int qb = 0; qb < QB; ++qb) accp[rb][qb] = acc[rb][qb];
           rowp = row0;
-          havep = true;
         } else if (acc[0][0][0] == 1234.5f && acc[1][1][3] == 1234.5f) {
           thr[0] = acc[0][1][2];  // keep the accumulators live
         }
@@ -678,17 +696,25 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if constexpr (PIPE) {
-    if (havep) {
+    if (!(abl & 2)) {
 #pragma unroll
       for (int qb = 0; qb < QB; ++qb) {
         if constexpr (I8)
-          select_quad_i8<R>(accp[0][qb], accp[1][qb], rowp, L[qb], I[qb], te[qb], tn[qb]);
+          select_quad_i8<R>(accp[0][qb], accp[1][qb], rowp, L[qb], I[qb], te[qb], tn[qb], selc);
         else
           select_quad_te<R>(accp[0][qb], accp[1][qb], rowp, L[qb], I[qb], te[qb]);
       }
     }
   }
 
+#if KNN_COUNT_SEL
+  if constexpr (I8) {
+    atomicAdd(&knn_sel_cnt[0], (unsigned long long)selc.calls);
+    atomicAdd(&knn_sel_cnt[1], (unsigned long long)selc.lane_pass);
+    if (lane == 0) atomicAdd(&knn_sel_cnt[2], (unsigned long long)selc.wave_pass);
+    atomicAdd(&knn_sel_cnt[3], (unsigned long long)selc.inserts);
+  }
+#endif
   if constexpr (M16) {
     // 4 lists per query per split (lane groups l>>4): [query][4S][R]
 #pragma unroll
@@ -806,5 +832,24 @@ static bool launch_res_dp(const CandLaunch& c, hipStream_t s) {
   int qpw_res_##v(int metric) { return metric == 5 ? res_qpw<5>() : res_qpw<0>(); }
 KNN_GROUP_DPS(KNN_DEF)
 #undef KNN_DEF
+
+#if KNN_GROUP == 1
+// Experiment hook (no C-ABI entry; tools call it by its symbol): the int8
+// selection counts of a KNN_COUNT_SEL build (DP 96 / 128), zeros otherwise.
+int res_sel_counters(unsigned long long* out, int reset) {
+#if KNN_COUNT_SEL
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(knn_sel_cnt), 4 * sizeof(unsigned long long)) != hipSuccess)
+    return -1;
+  if (reset) {
+    const unsigned long long z[4] = {0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(knn_sel_cnt), z, sizeof z) != hipSuccess) return -1;
+  }
+#else
+  (void)reset;
+  for (int i = 0; i < 4; ++i) out[i] = 0;
+#endif
+  return 0;
+}
+#endif
 
 }  // namespace knnk

@@ -22,6 +22,12 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 #define KNN_INF_F __builtin_inff()
+// Timing-only kernel ablations (tuning key "ablate", bits 0/1/3/4) are
+// compiled in only with -DKNN_ABLATIONS=1 (tools/build_variant.sh): in the
+// production build the candidate kernels carry no per-tile checks for them.
+#ifndef KNN_ABLATIONS
+#define KNN_ABLATIONS 0
+#endif
 #define KNN_INF_D __builtin_inf()
 
 // ---------------------------------------------------------------- helpers
@@ -442,18 +448,47 @@ __device__ __forceinline__ int i8_neg_half(float te) {
 }
 // tn = i8_neg_half(te), kept by the caller (refreshed with te per tile):
 // the no-insertion case is 4 v_max3 + 1 compare per call.
+// KNN_I8_UBR: the no-candidate test as a wave-uniform branch (v_cmp into an
+// SGPR pair + s_cbranch_vccz) instead of an exec-masked region (cfg2
+// candidate pass -1.3 %, gpurun_out/r3d_ab_*.log)
+#ifndef KNN_I8_UBR
+#define KNN_I8_UBR 1
+#endif
+// KNN_COUNT_SEL (experiment builds only): per-lane counts of the int8
+// selection -- calls whose lane passes the filter, calls where some lane of
+// the wave does (the slow path runs), values inserted -- summed into
+// knn_sel_cnt at the end of cand_kernel (knn_cand_res.hip)
+#ifndef KNN_COUNT_SEL
+#define KNN_COUNT_SEL 0
+#endif
+struct SelCount {
+  unsigned calls = 0, lane_pass = 0, wave_pass = 0, inserts = 0;
+};
 template <int R>
 __device__ __forceinline__ void select_quad_i8(const i32x4& a, const i32x4& b, int row0,
-                                               float (&L)[R], int (&I)[R], float& te, int& tn) {
+                                               float (&L)[R], int (&I)[R], float& te, int& tn,
+                                               SelCount& sc) {
   const int m1 = max(max(a[0], a[1]), a[2]);
   const int m2 = max(max(a[3], b[0]), b[1]);
   const int m3 = max(max(b[2], b[3]), m1);
   const int mx = max(m2, m3);
+#if KNN_COUNT_SEL
+  sc.calls++;
+  sc.lane_pass += mx > tn;
+  sc.wave_pass += __builtin_amdgcn_ballot_w64(mx > tn) != 0;
+#endif
+#if KNN_I8_UBR
+  if (__builtin_amdgcn_ballot_w64(mx > tn)) {
+#else
   if (mx > tn) {
+#endif
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int v = i < 4 ? a[i] : b[i - 4];
       if (v > tn) {
+#if KNN_COUNT_SEL
+        sc.inserts++;
+#endif
         list_insert<R>(L, I, (float)(-2 * v), row_at(row0, i < 4 ? i : 16 + i - 4));
         te = __builtin_fminf(te, L[R - 1]);
         tn = i8_neg_half(te);

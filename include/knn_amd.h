@@ -32,9 +32,10 @@
  *     re-orders those too);
  *   - label = first label whose running count strictly exceeds the running
  *     maximum while scanning the k nearest in order; -1 when k == 0.
- *   - the GPU computes a certified candidate set on MFMA (by default fp16
- *     operands on v_mfma_f32_16x16x32_f16; bf16x3 or fp32 by precision mode,
- *     see knn_set_precision) and re-ranks it in fp64; queries whose
+ *   - the GPU computes a certified candidate set on MFMA (by default exact
+ *     int8 codes on v_mfma_i32_16x16x64_i8 for integer-coded train sets,
+ *     else fp16 operands on v_mfma_f32_16x16x32_f16; bf16x3 or fp32 by
+ *     precision mode, see knn_set_precision) and re-ranks it in fp64; queries whose
  *     candidate set cannot be certified are re-run exactly (fp64 over all
  *     rows).  No CPU fallback exists: without a usable HIP device every call
  *     fails with KNN_ERR_DEVICE.
@@ -216,9 +217,10 @@ const char* knn_last_kernel_name(knn_ctx* ctx);
 
 /* Tuning overrides for experiments (0 = automatic): "R" list entries per
  * lane (4, 8, 16), "S" train splits per query tile (1..64), "nw" waves per
- * candidate workgroup (4 or 8; 32 queries per wave), "ablate" (bits 0/1:
- * timing-only kernel ablations, results invalid; bit 2: no per-query global
- * threshold exchange, results stay exact); -1 = auto for "fp16" (fp16
+ * candidate workgroup (4, 8 or 16 where the kernel has the variant), "ablate"
+ * (bits 0/1/3/4: timing-only kernel ablations -- no staging, no selection,
+ * L2-resident staging, no workgroup barrier -- results invalid; bit 2: no
+ * per-query global threshold exchange, results stay exact); -1 = auto for "fp16" (fp16
  * candidate pass: 0 off, 1 on), "i8" (the int8 candidate pass where the
  * train set is integer-coded: 0 off, 1 on at every batch size), "mfma16" (bf16x3 on the 16x16x32 layout: 0
  * off, 1 on), "s3q" (the fp16 d > 256 kernel on 16x16x32: 0 off, 1 on) and

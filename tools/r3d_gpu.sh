@@ -1,13 +1,12 @@
 #!/bin/bash
-# round-3 session: cfg2 split-count sweep (in-process A/B), its HBM fetch per
-# variant (one FETCH_SIZE pass over the same sweep), then the default bench.
+# round 3: int8 256-row tiles as default -- GPU suite, ablations (abl build),
+# exchange-period / uniform-branch A/B, default bench
 cd "$GRAFT_REPO_ROOT" || exit 1
-export TMPDIR=/tmp
-O=gpurun_out
-stop() { echo "step $1 rc=$2"; exit $2; }
-V="fp16:0:0 fp16:0:24 fp16:0:32 fp16:0:40 fp16:0:48 fp16:0:64"
-timeout -k 10 200 python3 -u tools/tune.py --rounds 5 $V > $O/r3d_tune_S.log 2>&1 || stop tune $?
-timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/r3d_fetch -o run \
-  --output-format csv -- python3 tools/tune.py --rounds 1 $V > $O/r3d_fetch.log 2>&1 || stop fetch $?
-timeout -k 10 600 python3 -u bench.py > $O/r3d_bench.json 2> $O/r3d_bench.log || stop bench $?
-echo ok
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -q -p no:cacheprovider -x --timeout 300 \
+  --timeout-method thread > gpurun_out/r3d_tests.log 2>&1 || exit $?
+KNN_AMD_VARIANT=abl timeout -k 10 240 python -u tools/tune.py --rounds 5 "auto:0:0" "auto:0:0:1" \
+  "auto:0:0:2" "auto:0:0:3" "auto:0:0:8" "auto:0:0:16" > gpurun_out/r3d_abl.log 2>&1 || exit $?
+AB_TAG=r3d_ab AB_ARGS="--rounds 5 auto:0:0" AB_VARIANTS="base x4 x2 ubr" REPS=2 \
+  bash tools/ab_variants_gpu.sh || exit $?
+timeout -k 10 300 python -u bench.py > gpurun_out/r3d_bench.log 2>&1

@@ -1,17 +1,14 @@
 #!/bin/bash
-# GPU tests, then cfg5 / cfg2 candidate-kernel A/B, then the default bench.
-# Any step ending by a signal / time limit ends the script.
+# round 3: int8 selection counts, ablations, parity subset, profiles of the new default
 cd "$GRAFT_REPO_ROOT" || exit 1
-export TMPDIR=/tmp
-O=gpurun_out
-step() {  # step <name> <limit> <cmd...>: stop on signals/timeouts (rc >= 124)
-  local n=$1 lim=$2; shift 2
-  timeout -k 10 "$lim" "$@" > $O/$n.log 2>&1
-  local rc=$?
-  echo "$n rc=$rc"
-  [ $rc -lt 124 ] || exit $rc
-}
-step r3e_tests 900 python -u -m pytest tests -m gpu -v --maxfail=8 --timeout 300 --timeout-method thread
-step r3e_cfg5 200 python3 -u tools/tune.py --n 1000000 --m 10000 --d 960 --k 100 --rounds 4 fp16:0:0
-step r3e_cfg2S 200 python3 -u tools/tune.py --rounds 5 fp16:0:0 fp16:0:24 fp16:0:32 fp16:0:40 fp16:0:48 fp16:0:64
-step r3e_bench 600 python3 -u bench.py
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -x -p no:cacheprovider \
+  --timeout 120 --timeout-method thread -k "i8 or int8 or golden or global" \
+  > gpurun_out/r3e_parity.log 2>&1 || exit $?
+KNN_AMD_VARIANT=cnt timeout -k 10 200 python -u tools/tune.py --rounds 3 "auto:0:0" \
+  > gpurun_out/r3e_cnt.log 2>&1 || exit $?
+KNN_AMD_VARIANT=cnt timeout -k 10 200 python -u tools/tune.py --rounds 2 --m 100000 "auto:0:0" \
+  > gpurun_out/r3e_cnt_m100k.log 2>&1 || exit $?
+KNN_AMD_VARIANT=abl timeout -k 10 240 python -u tools/tune.py --rounds 5 "auto:0:0" \
+  "auto:0:0:2" "auto:0:0:3" "auto:0:0:8" "auto:0:0:16" > gpurun_out/r3e_abl.log 2>&1 || exit $?
+TAG=r3e bash tools/profile_all.sh stats pmc cfg4 cfg5

@@ -10,6 +10,7 @@ nw = waves per candidate workgroup, 0 auto / 4 / 8)
 Extra tuning keys after a comma, e.g. "fp16:0:0,mfma16=1" (keys listed in
 `defaults` and not named by a variant are reset to automatic)."""
 import argparse
+import ctypes
 import os
 import sys
 
@@ -43,6 +44,13 @@ def main():
     tot = {}
     ph = {}
     info = {}
+    # int8 selection counts of a KNN_COUNT_SEL build (knn_cand_res.hip), per variant
+    try:
+        cnt_fn = getattr(knn.lib(), "_ZN4knnk16res_sel_countersEPyi")
+    except AttributeError:
+        cnt_fn = None
+    selc = {}
+    cbuf = (ctypes.c_ulonglong * 4)()
     prec = {"auto": knn.PRECISION_AUTO, "fp32": knn.PRECISION_FP32, "bf16x3": knn.PRECISION_BF16X3,
             "m16": knn.PRECISION_BF16X3, "fp16": knn.PRECISION_FP16}
     defaults = {"gk": -1, "s3q": -1, "xhswz": 1, "i8": -1}
@@ -65,8 +73,14 @@ def main():
             clf.set_tuning("R", int(R))
             clf.set_tuning("S", int(S))
             clf.set_tuning("ablate", abl)
+            if cnt_fn is not None:
+                cnt_fn(cbuf, 1)
             clf.classify_device(Q.data_ptr(), a.m, a.k, knn.L2, out.data_ptr())
             clf.sync()
+            if cnt_fn is not None and r > 0:
+                cnt_fn(cbuf, 1)
+                if any(cbuf):
+                    selc[v] = list(cbuf)
             if r == 0:
                 if ref is None:
                     ref = out.clone()
@@ -77,6 +91,11 @@ def main():
             ph.setdefault(v, []).append([clf.last_phase_ms(p) for p in range(4)])
     flops = 2.0 * a.n * a.d * a.m
     for v in a.variants:
+        if v in selc:
+            c = selc[v]
+            print("%-14s int8 selection per launch: calls %d, lane passes %.4f, wave passes %.4f, "
+                  "inserts per lane-call %.4f" % (v, c[0], c[1] / max(1, c[0]), c[2] * 64 / max(1, c[0]),
+                                                 c[3] / max(1, c[0])))
         ms = np.median(res[v])
         print("%-14s cand %8.3f ms (min %8.3f)  %7.1f TF/s  all phases %8.3f ms  %s rescans=%d "
               "same_labels=%s" % (v, ms, np.min(res[v]), flops / ms / 1e9, np.median(tot[v]),
