@@ -455,7 +455,9 @@ static void choose_geometry(knn_ctx* ctx, int metric, bool streamed, int DP, int
     if (s3q && R != 8) continue;
     // kernel metrics 3, 4 (16x16x32 layout) have R = 4 only; elsewhere R = 4
     // only on request (resident kernel; tuning experiments)
-    if (quad ? R != 4 : (ctx->tune_R ? R != ctx->tune_R : R == 4)) continue;
+    // (int8: R = 8 quad lists on request, tuning key "R")
+    const bool q8 = quad && metric == 5 && ctx->tune_R == 8;
+    if (quad ? R != (q8 ? 8 : 4) : (ctx->tune_R ? R != ctx->tune_R : R == 4)) continue;
     if (R == 4 && (DP > 256 || metric == 1)) continue;
     const int64_t slots =
         (int64_t)(s3q ? s3q_blocks_per_cu() : cand_blocks_per_cu(metric, DP, R, nw)) * ctx->cu_count;
@@ -471,7 +473,10 @@ static void choose_geometry(knn_ctx* ctx, int metric, bool streamed, int DP, int
     // batches of >= 128K queries, whose many workgroup rounds make the longer
     // walks of fewer splits worth nothing (cfg3: candidate +0.8 %, rescan
     // phase 11.9 -> 1.8 ms); at least S >= W
-    if (quad) {
+    if (q8) {
+      S_lo = std::max(S_lo, W);  // an 8-entry list holding 8 of the top W: negligible
+      S_hi = std::min(S_hi, kMaxUnion / (4 * 8));
+    } else if (quad) {
       const int mult = n_qt >= 512 ? 4 : 2;
       S_lo = std::max(S_lo, std::max<int>(W, (int)std::min<int64_t>(mult * W, n_tiles / 32)));
     }
@@ -662,7 +667,8 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   const int n_qt = (int)((m + qpb - 1) / qpb);
   const int64_t m_pad = (int64_t)n_qt * qpb;
   const int64_t n_pad3 = (t.n + kS3Rows - 1) / kS3Rows * kS3Rows;
-  const int64_t n_tiles = s3 ? n_pad3 / kS3Rows : t.n_pad / cand_tile_rows(DP);
+  const int64_t trows = cand_tile_rows(kmetric, DP);  // rows per tile of the launched kernel
+  const int64_t n_tiles = s3 ? n_pad3 / kS3Rows : t.n_pad / trows;
   int C = (int)std::min<int64_t>(t.n, std::max(2 * W, W + 16));
   C = std::min(C, kMaxUnion);
   int S = 1, R = 8;
@@ -676,7 +682,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   choose_geometry(ctx, kmetric, s3, DP, nw, n_qt, n_tiles, W, C, s3q, S, R);
   // 16x16 layouts: 4 lists per query per split
   const bool quad_lists = (!s3 && kmetric >= 3) || s3q;
-  if (quad_lists && !s3q) R = 4;
+  if (quad_lists && !s3q && !(kmetric == 5 && R == 8)) R = 4;
   const int NL = (quad_lists ? 4 : 2) * S;
   C = std::min(C, NL * R);
   // rescan workspace: the fast path serves the first `cap` failed queries
@@ -711,6 +717,8 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   if ((rc = ctx->fr_q.ensure((size_t)cap * t.DP * sizeof(float) + 16))) return rc;
   if ((rc = ctx->fr_thr.ensure((size_t)cap * sizeof(float) + 16))) return rc;
   if ((rc = ctx->slow_q.ensure((size_t)m * sizeof(int) + 16))) return rc;
+  if ((rc = ctx->rescan_mask.ensure((size_t)m * sizeof(unsigned long long) + 16))) return rc;
+  if ((rc = ctx->rescan_nkeep.ensure((size_t)cap * sizeof(int) + 16))) return rc;
 
   ctx->last_kmetric = kmetric;
   ctx->geom[0] = (int64_t)n_qt * S;
@@ -774,7 +782,11 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   cl.gk = gk;
   cl.xsw = kmetric == 5 ? 1 : ctx->xh_swz;  // the int8 image is always swizzled
   // slots of groups without a split stay 0 (never the max)
-  if (use_gthr) launch_fill_gthr(cl.gthr, m_pad, std::min(S, gk ? 8 : 4), s);
+  // (experiment, tuning "ablate" bit 5: keep the previous call's final
+  // thresholds -- valid only for a repeat of the same queries; measures what
+  // perfectly seeded thresholds would save)
+  if (use_gthr && !(ctx->tune_ablate & 32))
+    launch_fill_gthr(cl.gthr, m_pad, std::min(S, gk ? 8 : 4), s);
   if (s3h)
     launch_cand_s3h((const unsigned short*)ctx->XT16.p, (const float*)ctx->XS16.p,
                     (const unsigned short*)ctx->Q32.p, DP, n_pad3, R, S, n_qt, cl.out_v, cl.out_i,
@@ -788,6 +800,16 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   HIP_TRY(hipGetLastError());
   if (tc) HIP_TRY(hipEventRecord(tc->ev[2], s));
   HIP_TRY(hipMemsetAsync(ctx->rescan_cnt.p, 0, 4 * sizeof(int), s));
+  // per-split certification: a query failing only through some splits'
+  // lists rescans just those splits' rows (knn_select.hip)
+  SplitMap sm;
+  sm.S = S <= 64 ? S : 0;
+  sm.lps = quad_lists ? 4 : 2;
+  sm.trows = trows;
+  sm.cap = cap;
+  sm.mask = (unsigned long long*)ctx->rescan_mask.p;
+  sm.nkeep = (int*)ctx->rescan_nkeep.p;
+  sm.keep = (int*)ctx->fr_buf.p;
   if (kmetric == 5) {
     // int8 proxies are exact up to +1 (the odd-norm half of the seed): the
     // merge sees the pass's own centre and scale (codes (x - cent/2^s) 2^s),
@@ -803,14 +825,14 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
                         ProxyScale{qvalid, 0.0, 1.0 / DP, false, (const double*)ctx->i8_cent.p},
                         cl.gthr, sink,
                         (int*)ctx->rescan_q.p, (double*)ctx->rescan_tau.p, (int*)ctx->rescan_cnt.p,
-                        s);
+                        sm, s);
   } else {
     launch_merge_rerank(metric, (const float*)ctx->cand_v.p, (const int*)ctx->cand_i.p, NL, R, t,
                         dQ, m, W, C, err_factor(kmetric, DP),
                         kmetric == 4 ? ProxyScale{qvalid, 0x1p-14, 0x1p-28, true}
                                      : ProxyScale{qvalid, 0x1p-125, 0x1p-124},
                         cl.gthr, sink, (int*)ctx->rescan_q.p, (double*)ctx->rescan_tau.p,
-                        (int*)ctx->rescan_cnt.p, s);
+                        (int*)ctx->rescan_cnt.p, sm, s);
   }
   HIP_TRY(hipGetLastError());
   if (tc) HIP_TRY(hipEventRecord(tc->ev[3], s));
@@ -826,6 +848,10 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   rb.slow_q = (int*)ctx->slow_q.p;
   rb.counts = ctx->d_counts;
   rb.totals = (unsigned long long*)ctx->totals.p;
+  rb.mask = sm.mask;
+  rb.nkeep = sm.nkeep;
+  rb.S = sm.S;
+  rb.trows = sm.trows;
   // (timing-only ablations leave every query uncertified: no rescan then)
   const bool abl = ctx->tune_ablate & 27;
   launch_rescan(metric, t, dQ, rb, abl ? 0 : cap, W, err_factor(metric, t.DP), sink,

@@ -80,7 +80,7 @@ struct knn_ctx {
   DevBuf XI, i8_cent, i8_gs;
   // per-classify workspace
   DevBuf Q64, Q32, qvalid, cand_v, cand_i, gthr, rescan_q, rescan_tau, rescan_cnt, fr_cnt, fr_buf,
-      fr_q, fr_thr, slow_q, totals, lk;
+      fr_q, fr_thr, slow_q, totals, lk, rescan_mask, rescan_nkeep;
   // train-sharded merge of unions beyond 4096 entries (rank merge scratch)
   DevBuf mrg;
   // reference tie order pass: queued queries, per-workgroup scratch

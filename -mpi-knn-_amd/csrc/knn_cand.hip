@@ -28,7 +28,8 @@ namespace knnk {
 #define KNN_DECL(v)                                          \
   bool launch_res_##v(const CandLaunch& c, hipStream_t s);   \
   int blocks_res_##v(int R, int metric, int nw);             \
-  int qpw_res_##v(int metric);
+  int qpw_res_##v(int metric);                               \
+  int trows_res_##v(int metric);
 KNN_DP_LIST(KNN_DECL)
 #undef KNN_DECL
 
@@ -672,7 +673,13 @@ int cand_queries_per_wave(int metric, int DP) {
   return 32;
 }
 
-int cand_tile_rows(int DP) { return DP <= 256 ? kResTileRows : 128; }
+int cand_tile_rows(int metric, int DP) {
+  if ((metric == 2 && bf16x3_streamed(DP)) || (metric == 4 && DP > 256)) return kS3R;
+#define KNN_CASE(v) if (DP == v) return trows_res_##v(metric);
+  KNN_DP_LIST(KNN_CASE)
+#undef KNN_CASE
+  return 128;  // cand_stream_kernel
+}
 
 bool launch_cand(const CandLaunch& c, hipStream_t s) {
 #define KNN_CASE(v) \

@@ -347,6 +347,15 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   constexpr int G_HI = (NG + NW - 1) / NW, G_LO = NG / NW;
   constexpr int PD = NB - 1;  // prefetch distance in tiles
   static_assert(G_HI * (PD - 1) <= 63, "vmcnt range");
+  // tiles an exchange's ops stay in flight (the slots are read after the
+  // barrier of tile e + XPD); KNN_XPD_MIN = 2 lets them pass the barrier of
+  // tile e + 1 even at PD = 1 (counted as younger than its pieces), but the
+  // thresholds then arrive a tile later: int8 cfg2 candidate +2.5 %
+  // (gpurun_out/r3e_ab_*.log), so the default waits at tile e + 1
+#ifndef KNN_XPD_MIN
+#define KNN_XPD_MIN 1
+#endif
+  constexpr int XPD = PD < KNN_XPD_MIN ? KNN_XPD_MIN : PD;
   // LDS byte address of the staging array (wave-uniform)
   const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)lds;
 #define KNN_ISSUE(t_, b_)                                                              \
@@ -380,9 +389,9 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       if (x_age >= 0) ++x_age;
       // (wave-uniform; readfirstlane keeps the dispatch below on scalar branches)
 #if KNN_RFL
-      const int extra = __builtin_amdgcn_readfirstlane((x_age >= 1 && x_age <= PD - 1) ? x_ops : 0);
+      const int extra = __builtin_amdgcn_readfirstlane((x_age >= 1 && x_age <= XPD - 1) ? x_ops : 0);
 #else
-      const int extra = (x_age >= 1 && x_age <= PD - 1) ? x_ops : 0;
+      const int extra = (x_age >= 1 && x_age <= XPD - 1) ? x_ops : 0;
 #endif
       if (abl & 16) {
         // timing-only ablation: this wave's own waits, no workgroup barrier
@@ -400,7 +409,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       // issue cost without the data stream; timing only)
       if (it + PD < my_nt && !(abl & 1)) KNN_ISSUE((abl & 8) ? split : t + PD * S, nxt);
       if (gthr) {
-        if (x_age == PD) {
+        if (x_age == XPD) {
 #pragma unroll
           for (int b = 0; b < NQL; ++b) {
             // slots 0-3 as fetched by lane qi, 4-7 by lane qi + 32
@@ -411,7 +420,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
           }
           x_age = -1;
         }
-        if (x_age < 0 && exchange_tile(it) && it + PD < my_nt) {
+        if (x_age < 0 && exchange_tile(it) && it + XPD < my_nt) {
           // publish the best list threshold of the query's lanes in this wave
           // (one lane per query, only when it improved), fetch its 4 slots
           uint32_t pk;
@@ -767,7 +776,7 @@ static void launch_res(const CandLaunch& c, hipStream_t s) {
 template <int DP, int R, int M, int NW>
 constexpr bool res_variant() {
   return (M != 2 || DP % 16 == 0) && (M != 1 || (NW == 4 && R != 4)) &&
-         (M < 3 || (DP % 32 == 0 && R == 4 && (NW == 8 || M >= 4))) && (NW != 16 || M == 4) &&
+         (M < 3 || (DP % 32 == 0 && (R == 4 || (M == 5 && R == 8)) && (NW == 8 || M >= 4))) && (NW != 16 || M == 4) &&
          (M != 5 || (DP % 64 == 0 && (NW == 8 || (NW == 4 && KNN_I8_QB > 2))));
 }
 
@@ -829,7 +838,10 @@ static bool launch_res_dp(const CandLaunch& c, hipStream_t s) {
 #define KNN_DEF(v)                                                                 \
   bool launch_res_##v(const CandLaunch& c, hipStream_t s) { return launch_res_dp<v>(c, s); } \
   int blocks_res_##v(int R, int metric, int nw) { return blocks_per_cu_res<v>(R, metric, nw); } \
-  int qpw_res_##v(int metric) { return metric == 5 ? res_qpw<5>() : res_qpw<0>(); }
+  int qpw_res_##v(int metric) { return metric == 5 ? res_qpw<5>() : res_qpw<0>(); } \
+  int trows_res_##v(int metric) {                                                        \
+    return kTR * (metric == 5 ? res_tpb<5>() : metric == 4 ? res_tpb<4>() : res_tpb<0>()); \
+  }
 KNN_GROUP_DPS(KNN_DEF)
 #undef KNN_DEF
 

@@ -89,7 +89,9 @@ void launch_prep_half_tiled(const double* X64, const double* mu, int64_t n, int 
                             const float* seed_src, float* seed_out, const float* valid,
                             unsigned long long* dx2max, hipStream_t s);
 bool cand_supported(int DP);
-int cand_tile_rows(int DP);         // train rows per tile of the kernel serving DP
+// train rows per tile of the candidate kernel serving (kernel metric, DP):
+// split s of a launch walks tiles s, s + S, ... (rows (r / tile) % S == s)
+int cand_tile_rows(int metric, int DP);
 int cand_blocks_per_cu(int metric, int DP, int R, int nw);  // resident workgroups per CU
 int cand_queries_per_wave(int metric, int DP);  // resident kernel: queries per wave
 
@@ -154,10 +156,23 @@ struct ProxyScale {
   // clamp(rint(q 2^s - cent), -128, 127); the merge measures the rounding)
   const double* i8c = nullptr;
 };
+// Per-split certification (merge) and the targeted rescan: a query whose
+// bound fails only through some splits' lists (a list holding R of its top
+// W, its R-th entry inside the top W) rescans just those splits' rows.
+struct SplitMap {
+  int S = 0;                  // splits of the candidate launch (0: whole-set rescans only)
+  int lps = 0;                // lists per query per split (4 quad, 2 otherwise)
+  int64_t trows = 0;          // train rows per tile
+  int cap = 0;                // failed queries the fast rescan serves
+  unsigned long long* mask = nullptr;  // [m] splits each failed query rescans (~0: all rows)
+  int* nkeep = nullptr;       // [cap] re-ranked rows of the other splits handed to the rescan
+  int* keep = nullptr;        // [cap][kRescanCap] (the fast rescan's row buffer)
+};
 void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int R,
                          const TrainDev& t, const double* Q64, int64_t m, int W, int C,
                          double f_err, ProxyScale ps, const uint32_t* gthr, const Sink& sink,
-                         int* rescan_q, double* rescan_tau, int* rescan_cnt, hipStream_t s);
+                         int* rescan_q, double* rescan_tau, int* rescan_cnt, const SplitMap& sm,
+                         hipStream_t s);
 constexpr int kRescanCap = 1024;        // rows a fast rescan may append per query
 constexpr int kRescanStageMaxDP = 256;  // fast rescan stages rows in LDS up to this DP
 constexpr int kRescanFastQueries = 65536;  // failed queries per call the fast path serves
@@ -174,6 +189,10 @@ struct RescanBufs {
   int* slow_q;               // [m] queries for the full scan
   int* counts;               // host-mapped {cnt[0], full scans} of the call (nullable)
   unsigned long long* totals;  // device running sums of the same (nullable)
+  const unsigned long long* mask;  // [m] splits to scan per failed query (null: all rows)
+  const int* nkeep;          // [cap] rows the merge already put in buf (null: none)
+  int S;                     // splits / tile rows of the candidate launch (mask bits)
+  int64_t trows;
 };
 // Enqueues the whole rescan path (prep, filter, exact finish, full scan);
 // every kernel reads the counts on the device.  f_err: the fp32 candidate

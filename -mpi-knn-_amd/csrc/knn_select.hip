@@ -202,16 +202,26 @@ __device__ void exact_sorted(const TrainDev& t, const double* qv, int* di, doubl
   bitonic_sort_lds(dk, di, C2, tid, NT);
 }
 
+// The certification test: every row whose proxy is >= LB (unscaled) has an
+// exact distance beyond dw, the W-th exact distance re-ranked (rigorous error
+// bound E; +inf LB: no such row can be closer)
+template <int METRIC>
+__device__ __forceinline__ bool bound_ok(double LB, double dw, double qa, double E) {
+  if (METRIC == 0) return (LB + qa * (1.0 - 2e-12) - E) * (1.0 - 1e-12) > dw * dw * (1.0 + 1e-12);
+  return (LB - E) * (1.0 - 1e-12) > dw * (1.0 + 1e-12);
+}
+
 template <int METRIC, int NT, int EPL>
 __global__ void __launch_bounds__(NT)
 merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, int U, int R,
                     TrainDev t, const double* __restrict__ Q64, int W, int Cmax, int C2,
                     double f_err, ProxyScale ps, const uint32_t* __restrict__ gthr, Sink sink,
                     int* __restrict__ rescan_q, double* __restrict__ rescan_tau,
-                    int* __restrict__ rescan_cnt) {
+                    int* __restrict__ rescan_cnt, SplitMap sm) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int s_cn, s_cert;
-  __shared__ double s_lb, s_qa, s_e;
+  __shared__ double s_lb, s_lbr, s_qa, s_e, s_pinv;
+  __shared__ uint32_t s_bs[64];  // per split: min over its full lists' R-th entries (keys)
   const int d = t.d;
   // the query row is staged in LDS up to kMergeLdsDim dims, else read in place
   const bool q_in_lds = d <= kMergeLdsDim;
@@ -226,6 +236,7 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
   const double* qv = q_in_lds ? (const double*)smem : qrow;
   if (q_in_lds)
     for (int c = tid; c < d; c += NT) ((double*)smem)[c] = qrow[c];
+  if (tid < 64) s_bs[tid] = kKeyInf;
   __syncthreads();
 
   if (tid < 64) {
@@ -304,7 +315,10 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
       if (x < U) {
         v[e] = lv[x];
         id[e] = li[x];
-        if (x % R == R - 1) mlr = fminf(mlr, v[e]);
+        if (x % R == R - 1) {
+          mlr = fminf(mlr, v[e]);
+          if (sm.S && v[e] < KNN_INF_F) atomicMin(&s_bs[x / (sm.lps * R)], f2key(v[e]));
+        }
       }
       nv += __popcll(__ballot(v[e] < KNN_INF_F));
     }
@@ -382,6 +396,8 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
       // void proxies: exact rescan below; non-finite query: no neighbours
       s_cn = nonfinite ? -1 : (void_q ? Cmax + 1 : cn);
       s_lb = (double)fminf(fminf(lbx, mlr), tq) * pinv;
+      s_lbr = (double)fminf(lbx, tq) * pinv;  // the bound without the lists' R-th entries
+      s_pinv = pinv;
       s_qa = qa;
       s_e = E;
     }
@@ -397,6 +413,10 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
       const int f = atomicAdd(rescan_cnt, 1);
       rescan_q[f] = (int)q;
       rescan_tau[f] = KNN_INF_D;
+      if (sm.mask) {
+        sm.mask[f] = ~0ull;
+        if (f < sm.cap) sm.nkeep[f] = 0;
+      }
     }
     return;
   }
@@ -415,14 +435,7 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
       // threshold): not certified, the rescan decides
       cert = false;
     } else {
-      const double dw = dk[W - 1], qa = s_qa, E = s_e;
-      if (METRIC == 0) {
-        const double bound = (LB + qa * (1.0 - 2e-12) - E) * (1.0 - 1e-12);
-        cert = bound > dw * dw * (1.0 + 1e-12);
-      } else {
-        const double bound = (LB - E) * (1.0 - 1e-12);
-        cert = bound > dw * (1.0 + 1e-12);
-      }
+      cert = bound_ok<METRIC>(LB, dk[W - 1], s_qa, s_e);
     }
     s_cert = cert;
     if (!cert) {
@@ -431,6 +444,37 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
       const int f = atomicAdd(rescan_cnt, 1);
       rescan_q[f] = (int)q;
       rescan_tau[f] = cn >= W ? dk[W - 1] : KNN_INF_D;
+      if (sm.mask) {
+        // Per split: rows a split dropped have proxy >= min(its lists' final
+        // R-th entries, the final global threshold) -- its quad filter and
+        // the lists only tighten.  When the bound holds without the lists'
+        // R-th entries, only the splits whose own bound fails can hold a row
+        // of the top W outside the re-ranked set: the rescan scans those
+        // splits' rows, and the re-ranked rows of the other splits within
+        // tau go along (every other row of theirs is beyond tau).
+        unsigned long long mk = ~0ull;
+        if (sm.S && cn >= W && bound_ok<METRIC>(s_lbr, dk[W - 1], s_qa, s_e)) {
+          mk = 0;
+          for (int sp = 0; sp < sm.S; ++sp) {
+            const double b = (double)key2f(s_bs[sp]) * s_pinv;
+            if (!bound_ok<METRIC>(b, dk[W - 1], s_qa, s_e)) mk |= 1ull << sp;
+          }
+          if (mk == 0) mk = ~0ull;
+        }
+        sm.mask[f] = mk;
+        if (f < sm.cap) {
+          int nk = 0;
+          if (mk != ~0ull) {
+            const double tau = dk[W - 1];
+            for (int i = 0; i < cn; ++i) {
+              const int r = di[i];
+              const int sp = (int)(((int64_t)r / sm.trows) % sm.S);
+              if (dk[i] <= tau && !((mk >> sp) & 1)) sm.keep[(int64_t)f * kRescanCap + nk++] = r;
+            }
+          }
+          sm.nkeep[f] = nk;
+        }
+      }
     }
   }
   __syncthreads();
@@ -451,26 +495,29 @@ template <int METRIC, int NT, int EPL>
 static void launch_mr(const float* cv, const int* ci, int U, int R, const TrainDev& t,
                       const double* Q64, int64_t m, int W, int Cmax, int C2, double f_err,
                       ProxyScale ps, const uint32_t* gthr, const Sink& sink, int* rescan_q,
-                      double* rescan_tau, int* rescan_cnt, hipStream_t s) {
+                      double* rescan_tau, int* rescan_cnt, const SplitMap& sm, hipStream_t s) {
   const size_t lds = (size_t)(t.d <= kMergeLdsDim ? t.d : 0) * 8 + (size_t)C2 * 8 +
                      (size_t)NT * 17 * 8 + (size_t)C2 * 8;
   hipLaunchKernelGGL((merge_rerank_kernel<METRIC, NT, EPL>), dim3((unsigned)m), dim3(NT), lds, s,
                      cv, ci, U, R, t, Q64, W, Cmax, C2, f_err, ps, gthr, sink, rescan_q, rescan_tau,
-                     rescan_cnt);
+                     rescan_cnt, sm);
 }
 
 void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int R,
                          const TrainDev& t, const double* Q64, int64_t m, int W, int C,
                          double f_err, ProxyScale ps, const uint32_t* gthr, const Sink& sink,
-                         int* rescan_q, double* rescan_tau, int* rescan_cnt, hipStream_t s) {
+                         int* rescan_q, double* rescan_tau, int* rescan_cnt, const SplitMap& sm_in,
+                         hipStream_t s) {
   if (m <= 0) return;
+  SplitMap sm = sm_in;
+  if (sm.S > 64 || sm.trows <= 0) sm.S = 0;  // per-split bounds need S <= 64 mask bits
   const int U = NL * R;  // <= 2 * 64 * 16 (choose_geometry bounds S and R)
   int C2 = 1;
   while (C2 < C) C2 <<= 1;
   const bool big = C2 > 64, wide = U > 1024;
 #define KNN_MR(M_, NT_, EPL_) \
   launch_mr<M_, NT_, EPL_>(cv, ci, U, R, t, Q64, m, W, C, C2, f_err, ps, gthr, sink, rescan_q, \
-                           rescan_tau, rescan_cnt, s)
+                           rescan_tau, rescan_cnt, sm, s)
   // fewer entries per lane when the union is small (cfg2: 152 lists x 4 =
   // 608 entries -> 10 per lane): every radix-select step and the selection
   // loops run over EPL unrolled entries
@@ -515,7 +562,7 @@ __global__ void __launch_bounds__(64)
 rescan_prep_kernel(TrainDev t, const double* __restrict__ Q64, const int* __restrict__ rescan_q,
                    const double* __restrict__ tau, const int* __restrict__ cnt, int cap,
                    double f_err, float* __restrict__ qf, float* __restrict__ thr,
-                   int* __restrict__ fcnt) {
+                   int* __restrict__ fcnt, const int* __restrict__ nkeep) {
   const int nf = min(cnt[0], cap);
   const int lane = threadIdx.x, d = t.d, DP = t.DP;
   for (int s = blockIdx.x; s < nf; s += gridDim.x) {
@@ -552,7 +599,7 @@ rescan_prep_kernel(TrainDev t, const double* __restrict__ Q64, const int* __rest
       float tf = (float)T;
       if ((double)tf < T && tf < KNN_INF_F) tf = key2f(f2key(tf) + 1u);
       thr[s] = tq < KNN_INF_D ? tf : -KNN_INF_F;  // unknown tau: nothing passes, full scan
-      fcnt[s] = 0;
+      fcnt[s] = nkeep ? nkeep[s] : 0;  // the merge's re-ranked rows of the certified splits
     }
   }
 }
@@ -574,7 +621,8 @@ template <int METRIC, int FQ>
 __global__ void __launch_bounds__(256)
 rescan_filter_kernel(TrainDev t, const float* __restrict__ qf, const float* __restrict__ thr,
                      const int* __restrict__ cnt, int cap, int* __restrict__ fcnt,
-                     int* __restrict__ buf) {
+                     int* __restrict__ buf, const unsigned long long* __restrict__ mask, int S,
+                     int64_t trows) {
   const int nf = min(cnt[0], cap);
   if (nf == 0) return;
   extern __shared__ __attribute__((aligned(16))) float fsm[];
@@ -583,10 +631,35 @@ rescan_filter_kernel(TrainDev t, const float* __restrict__ qf, const float* __re
   float* qs = fsm;                          // [FQ][DP] centred queries (x -2 for L2)
   float* thr_s = qs + FQ * DP;              // [FQ] proxy thresholds
   float* rows = thr_s + FQ;                 // [NWB][64][RSF]
+  __shared__ unsigned long long mask_s[FQ];  // splits each query of the group scans
+  __shared__ unsigned long long s_u;         // union of the failed queries' splits
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t row0 = ((int64_t)blockIdx.x * NWB + wv) * 64;
+  if (tid == 0) {
+    unsigned long long u = ~0ull;
+    if (mask && nf <= 64) {
+      u = 0;
+      for (int f = 0; f < nf; ++f) u |= mask[f];
+    }
+    s_u = u;
+  }
+  __syncthreads();
+  const unsigned long long need = s_u;
+  // grid-stride over blocks of NWB x 64 rows; a row block none of whose rows
+  // lies in a split some failed query scans is skipped before its rows load
+  // (a targeted rescan reads only the flagged splits' rows)
+  const int64_t nrb = (t.n_pad + NWB * 64 - 1) / (NWB * 64);
+  for (int64_t rbk = blockIdx.x; rbk < nrb; rbk += gridDim.x) {
+  const int64_t row0 = (rbk * NWB + wv) * 64;
   const bool active = row0 < t.n_pad;
+  // split of this wave's 64 rows (64 | trows)
+  const int wsp = mask ? (int)((row0 / trows) % S) : 0;
+  if (mask && need != ~0ull) {
+    unsigned long long bits = 0;  // (block-uniform)
+    for (int w = 0; w < NWB; ++w) bits |= 1ull << (int)((((rbk * NWB + w) * 64) / trows) % S);
+    if (!(bits & need)) continue;
+  }
+  __syncthreads();  // every wave is done with the previous row block's group loop
 
   float* my_rows = rows + (size_t)wv * 64 * RSF;
   if (active) {  // X32 carries 1 KiB of slack past the last row
@@ -603,7 +676,10 @@ rescan_filter_kernel(TrainDev t, const float* __restrict__ qf, const float* __re
       const int qi = e / DP;
       qs[e] = qi < nfg ? qf[(int64_t)g0 * DP + e] : 0.0f;
     }
-    if (tid < FQ) thr_s[tid] = tid < nfg ? thr[g0 + tid] : -KNN_INF_F;  // absent: no row passes
+    if (tid < FQ) {
+      thr_s[tid] = tid < nfg ? thr[g0 + tid] : -KNN_INF_F;  // absent: no row passes
+      mask_s[tid] = tid < nfg && mask ? mask[g0 + tid] : ~0ull;
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (active) {
@@ -634,9 +710,11 @@ rescan_filter_kernel(TrainDev t, const float* __restrict__ qf, const float* __re
       }
 #pragma unroll
       for (int qi = 0; qi < FQ; ++qi)
-        if (qi < nfg) rescan_append(acc[qi], thr_s[qi], g0 + qi, row0 + lane, fcnt, buf);
+        if (qi < nfg && ((mask_s[qi] >> wsp) & 1))
+          rescan_append(acc[qi], thr_s[qi], g0 + qi, row0 + lane, fcnt, buf);
     }
   }
+  }  // row blocks
 }
 
 // DP > 256 (rows too long to stage 64 per wave): 4 lanes per train row, 16
@@ -649,16 +727,34 @@ template <int METRIC, int FQ>
 __global__ void __launch_bounds__(256)
 rescan_filter_wide_kernel(TrainDev t, const float* __restrict__ qf, const float* __restrict__ thr,
                           const int* __restrict__ cnt, int cap, int* __restrict__ fcnt,
-                          int* __restrict__ buf) {
+                          int* __restrict__ buf, const unsigned long long* __restrict__ mask,
+                          int S, int64_t trows) {
   const int nf = min(cnt[0], cap);
   if (nf == 0) return;
   extern __shared__ __attribute__((aligned(16))) float fsm[];
   const int DP = t.DP, RSF = DP + 4;
   float* qs = fsm;             // [FQ][DP]
   float* thr_s = qs + FQ * DP; // [FQ]
+  __shared__ unsigned long long mask_s[FQ];
+  __shared__ unsigned long long s_u;
   const int tid = threadIdx.x, lane = tid & 63, part = lane & 3;
-  const int64_t row = ((int64_t)blockIdx.x * 4 + (tid >> 6)) * 16 + (lane >> 2);
+  if (tid == 0) {
+    unsigned long long u = ~0ull;
+    if (mask && nf <= 64) {
+      u = 0;
+      for (int f = 0; f < nf; ++f) u |= mask[f];
+    }
+    s_u = u;
+  }
+  __syncthreads();
+  const unsigned long long need = s_u;
+  const int64_t nrb = (t.n_pad + 63) / 64;
+  for (int64_t rbk = blockIdx.x; rbk < nrb; rbk += gridDim.x) {
+  const int64_t row = (rbk * 4 + (tid >> 6)) * 16 + (lane >> 2);
   const bool active = row < t.n_pad;
+  // the block's 64 rows lie in one tile (64 | trows): its split
+  const int bsp = mask ? (int)(((rbk * 64) / trows) % S) : 0;
+  if (mask && !((need >> bsp) & 1)) continue;  // (block-uniform)
   const float* xr = t.X32 + (active ? row : 0) * RSF;
   for (int g0 = 0; g0 < nf; g0 += FQ) {
     const int nfg = min(FQ, nf - g0);
@@ -667,7 +763,10 @@ rescan_filter_wide_kernel(TrainDev t, const float* __restrict__ qf, const float*
       const int qi = e / DP;
       qs[e] = qi < nfg ? qf[(int64_t)g0 * DP + e] : 0.0f;
     }
-    if (tid < FQ) thr_s[tid] = tid < nfg ? thr[g0 + tid] : -KNN_INF_F;
+    if (tid < FQ) {
+      thr_s[tid] = tid < nfg ? thr[g0 + tid] : -KNN_INF_F;
+      mask_s[tid] = tid < nfg && mask ? mask[g0 + tid] : ~0ull;
+    }
     __syncthreads();
     float acc[FQ];
 #pragma unroll
@@ -705,9 +804,11 @@ rescan_filter_wide_kernel(TrainDev t, const float* __restrict__ qf, const float*
     if (active && part == 0) {
 #pragma unroll
       for (int qi = 0; qi < FQ; ++qi)
-        if (qi < nfg) rescan_append(acc[qi], thr_s[qi], g0 + qi, row, fcnt, buf);
+        if (qi < nfg && ((mask_s[qi] >> bsp) & 1))
+          rescan_append(acc[qi], thr_s[qi], g0 + qi, row, fcnt, buf);
     }
   }
+  }  // row blocks
 }
 
 // Exact re-rank of each fast-rescanned query's appended rows (a loop over
@@ -880,13 +981,17 @@ rescan_full_kernel(TrainDev t, const double* __restrict__ Q64, const int* __rest
 void launch_rescan(int metric, const TrainDev& t, const double* Q64, const RescanBufs& rb, int cap,
                    int W, double f_err, const Sink& sink, int full_blocks, hipStream_t s) {
   if (cap > 0) {
+    // per-split masks (targeted rescans) need the launch's split geometry
+    const unsigned long long* mk = rb.S > 0 && rb.S <= 64 && rb.trows > 0 ? rb.mask : nullptr;
+    const int mS = mk ? rb.S : 1;
+    const int64_t mT = mk ? rb.trows : 64;
     const int gp = std::min(cap, 256);
     if (metric == 0)
       hipLaunchKernelGGL(rescan_prep_kernel<0>, dim3(gp), dim3(64), 0, s, t, Q64, rb.q, rb.tau,
-                         rb.cnt, cap, f_err, rb.qf, rb.thr, rb.fcnt);
+                         rb.cnt, cap, f_err, rb.qf, rb.thr, rb.fcnt, rb.nkeep);
     else
       hipLaunchKernelGGL(rescan_prep_kernel<1>, dim3(gp), dim3(64), 0, s, t, Q64, rb.q, rb.tau,
-                         rb.cnt, cap, f_err, rb.qf, rb.thr, rb.fcnt);
+                         rb.cnt, cap, f_err, rb.qf, rb.thr, rb.fcnt, rb.nkeep);
     constexpr int FQ = 16;
     const size_t qbytes = (size_t)FQ * (t.DP + 1) * 4;
     if (t.DP <= kRescanStageMaxDP) {
@@ -894,27 +999,28 @@ void launch_rescan(int metric, const TrainDev& t, const double* Q64, const Resca
       const size_t tile = (size_t)64 * (t.DP + 4) * 4;
       const int nwb = (int)std::max<size_t>(1, std::min<size_t>(4, (150 * 1024 - qbytes) / tile));
       const int64_t rpb = 64 * nwb;
-      const dim3 fg((unsigned)((t.n_pad + rpb - 1) / rpb));
+      // (grid-stride over row blocks: a targeted rescan skips most of them)
+      const dim3 fg((unsigned)std::min<int64_t>((t.n_pad + rpb - 1) / rpb, 1024));
       const size_t flds = qbytes + nwb * tile;
       if (metric == 0)
         hipLaunchKernelGGL((rescan_filter_kernel<0, FQ>), fg, dim3(64 * nwb), flds, s, t, rb.qf,
-                           rb.thr, rb.cnt, cap, rb.fcnt, rb.buf);
+                           rb.thr, rb.cnt, cap, rb.fcnt, rb.buf, mk, mS, mT);
       else
         hipLaunchKernelGGL((rescan_filter_kernel<1, FQ>), fg, dim3(64 * nwb), flds, s, t, rb.qf,
-                           rb.thr, rb.cnt, cap, rb.fcnt, rb.buf);
+                           rb.thr, rb.cnt, cap, rb.fcnt, rb.buf, mk, mS, mT);
     } else {
       // 64 rows per 4-wave block; 8 queries per pass (a failed query is rare
       // at d > 256: the LDS of 8 query rows leaves room for 5 blocks per CU,
       // i.e. more row loads in flight than 2 blocks with 16 queries)
       constexpr int FQW = 8;
       const size_t qbw = (size_t)FQW * (t.DP + 1) * 4;
-      const dim3 fg((unsigned)((t.n_pad + 63) / 64));
+      const dim3 fg((unsigned)std::min<int64_t>((t.n_pad + 63) / 64, 4096));
       if (metric == 0)
         hipLaunchKernelGGL((rescan_filter_wide_kernel<0, FQW>), fg, dim3(256), qbw, s, t, rb.qf,
-                           rb.thr, rb.cnt, cap, rb.fcnt, rb.buf);
+                           rb.thr, rb.cnt, cap, rb.fcnt, rb.buf, mk, mS, mT);
       else
         hipLaunchKernelGGL((rescan_filter_wide_kernel<1, FQW>), fg, dim3(256), qbw, s, t, rb.qf,
-                           rb.thr, rb.cnt, cap, rb.fcnt, rb.buf);
+                           rb.thr, rb.cnt, cap, rb.fcnt, rb.buf, mk, mS, mT);
     }
     const size_t lds = (size_t)(t.d <= 1024 ? t.d : 0) * 8 + (size_t)kRescanCap * 8 +
                        (size_t)256 * 17 * 8 + (size_t)kRescanCap * 8;

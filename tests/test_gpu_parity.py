@@ -312,6 +312,41 @@ def test_int8_off_grid_queries(knn):
     c.close()
 
 
+@pytest.mark.parametrize("path", ["i8", "fp16", "s3"])
+def test_targeted_rescan(knn, path):
+    """Per-split certification: with few splits (tuning S = 2, 3) a lane list
+    often holds R of a query's top W, so its bound fails; the merge then
+    flags only the splits whose own bound fails, hands the re-ranked rows of
+    the others to the rescan, and the rescan scans just the flagged splits'
+    rows (knn_select.hip).  Exact answers against the oracle on the int8
+    (grid data), fp16 (continuous data) and fp16 S3 (d = 300) paths."""
+    rng = np.random.default_rng(123)
+    if path == "i8":
+        tr, lab, te = _grid_codes(rng, 20000, 600, 64, 6)
+        k = 10
+    else:
+        d = 300 if path == "s3" else 64
+        k = 40 if path == "s3" else 10
+        cen = rng.uniform(-1, 1, (6, d))
+        lab_all = rng.integers(0, 6, 20600).astype(np.int32)
+        X = cen[lab_all] + 0.35 * rng.standard_normal((20600, d))
+        tr, te, lab = X[:20000].copy(), X[20000:].copy(), lab_all[:20000].copy()
+    rescans = 0
+    for S in (2, 3):
+        c = knn.Classifier(0)
+        if path == "i8":
+            c.set_tuning("i8", 1)
+        else:
+            c.set_precision(knn.PRECISION_FP16)
+        c.set_tuning("S", S)
+        run_case(c, knn, tr, lab, te, k, 0, 6)
+        assert c.last_candidate_path() == (5 if path == "i8" else 4)
+        assert c.last_geometry()["splits"] == S
+        rescans += c.last_rescan_count()
+        c.close()
+    assert rescans > 0, "expected certification failures with 2-3 splits"
+
+
 def test_k_zero_and_errors(clf, knn):
     rng = np.random.default_rng(3)
     tr, lab, te = _mix(rng, 500, 10, 8, 2)

@@ -12,3 +12,4 @@ KNN_AMD_VARIANT=cnt timeout -k 10 200 python -u tools/tune.py --rounds 2 --m 100
 KNN_AMD_VARIANT=abl timeout -k 10 240 python -u tools/tune.py --rounds 5 "auto:0:0" \
   "auto:0:0:2" "auto:0:0:3" "auto:0:0:8" "auto:0:0:16" > gpurun_out/r3e_abl.log 2>&1 || exit $?
 TAG=r3e bash tools/profile_all.sh stats pmc cfg4 cfg5
+AB_TAG=r3e_ab AB_ARGS="--rounds 5 auto:0:0" AB_VARIANTS="base xpd1" REPS=2 bash tools/ab_variants_gpu.sh

@@ -1,11 +1,10 @@
 #!/bin/bash
-# int8 candidate pass: parity, in-process A/B against fp16, default bench
+# round 3: per-split certification + targeted rescan -- GPU suite and the default bench
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu \
-  tests/test_gpu_parity.py -k "int8 or integer or golden" > gpurun_out/r3i_parity.log 2>&1 || exit $?
-timeout -k 10 240 python -u tools/tune.py --rounds 6 "auto:0:0,i8=0" "auto:0:0,i8=1" \
-  > gpurun_out/r3i_ab_cfg2.log 2>&1 || exit $?
-timeout -k 10 240 python -u tools/tune.py --rounds 4 --m 100000 "auto:0:0,i8=0" "auto:0:0,i8=1" \
-  > gpurun_out/r3i_ab_cfg2_100k.log 2>&1 || exit $?
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -x -p no:cacheprovider \
+  --timeout 120 --timeout-method thread -k "targeted or duplicates or rescan" \
+  > gpurun_out/r3i_targeted.log 2>&1 || exit $?
+timeout -k 10 600 python -u -m pytest tests -m gpu -q -p no:cacheprovider -x --timeout 300 \
+  --timeout-method thread > gpurun_out/r3i_tests.log 2>&1 || exit $?
 timeout -k 10 300 python -u bench.py > gpurun_out/r3i_bench.log 2>&1

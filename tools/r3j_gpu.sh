@@ -1,8 +1,11 @@
 #!/bin/bash
-# int8: phase breakdown at 1M queries (cfg3), kernel ablations at cfg2
+# round 3: grid-stride targeted rescan -- rescan tests, full suite, rescan phase time, bench
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-timeout -k 10 300 python -u tools/tune.py --rounds 2 --m 1000000 "auto:0:0,i8=0" "auto:0:0,i8=1" \
-  > gpurun_out/r3j_cfg3.log 2>&1 || exit $?
-timeout -k 10 240 python -u tools/tune.py --rounds 6 "auto:0:0,i8=1" "auto:0:0:1,i8=1" "auto:0:0:2,i8=1" \
-  "auto:0:0:3,i8=1" "auto:0:0:4,i8=1" > gpurun_out/r3j_abl_i8.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -x -p no:cacheprovider \
+  --timeout 120 --timeout-method thread -k "targeted or duplicates or rescan or large_d" \
+  > gpurun_out/r3j_targeted.log 2>&1 || exit $?
+timeout -k 10 600 python -u -m pytest tests -m gpu -q -p no:cacheprovider -x --timeout 300 \
+  --timeout-method thread > gpurun_out/r3j_tests.log 2>&1 || exit $?
+timeout -k 10 200 python -u tools/tune.py --rounds 5 "auto:0:0" > gpurun_out/r3j_tune.log 2>&1 || exit $?
+timeout -k 10 300 python -u bench.py > gpurun_out/r3j_bench.log 2>&1
