@@ -359,12 +359,6 @@ cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* 
     thr[b] = KNN_INF_F;
   }
 
-#pragma unroll
-  for (int p = 0; p < PD; ++p)
-    if (total > p) issue();
-
-  f32x16 acc[8];
-  f32x4 aq[16][2];  // Q16: [row block][query block]
   // Q16 global threshold state (see above); the exchange's ops stay in flight
   // across PD barriers (counted into their waits) and the slots are read
   // after the barrier that retires them
@@ -375,6 +369,19 @@ cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* 
   float tq[2] = {KNN_INF_F, KNN_INF_F};
   uint32_t last_pub = kKeyInf;
   int x_ops = 0, x_age = -1;
+  if (gx && KNN_X_START && total > 0) {
+    // the slots as they stand now (published by earlier grid rounds), fetched
+    // before step 0's pieces: step 0's wait retires them and they are read
+    // right after it (x_age = PD + 1 there, no extra count)
+    glds16((const char*)gthr + goff + 16 * h, gls_addr);
+    x_age = PD;
+  }
+#pragma unroll
+  for (int p = 0; p < PD; ++p)
+    if (total > p) issue();
+
+  f32x16 acc[8];
+  f32x4 aq[16][2];  // Q16: [row block][query block]
   int c = 0, t = split, cb = 0, ti = 0;
   for (int st = 0; st < total; ++st) {
     // own pieces of step st landed (those of st+1 may still be in flight),

@@ -365,6 +365,18 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
     for (int i_ = wv; i_ < NG; i_ += NW) glds16(g_ + i_ * 1024, l_ + (uint32_t)(i_ * 1024)); \
   } while (0)
 
+  if (gthr && KNN_X_START && my_nt > 0) {
+    // the slots as they stand now, fetched before tile 0's pieces: tile 0's
+    // wait retires them (x_age reaches XPD there, no extra count) and its
+    // selection filters with them
+    if constexpr (GW == 128) {
+      glds16((const char*)gthr + goff, gls_addr);
+      glds16((const char*)gthr + goff + 16, gls_addr + 1024);
+    } else {
+      glds16((const char*)gthr + goff + 16 * h, gls_addr);
+    }
+    x_age = XPD - 1;
+  }
 #pragma unroll
   for (int p = 0; p < PD; ++p)
     if (my_nt > p) KNN_ISSUE(split + p * S, p);

@@ -458,6 +458,13 @@ __device__ __forceinline__ int i8_neg_half(float te) {
 // selection -- calls whose lane passes the filter, calls where some lane of
 // the wave does (the slow path runs), values inserted -- summed into
 // knn_sel_cnt at the end of cand_kernel (knn_cand_res.hip)
+// Candidate kernels: fetch the per-query global thresholds once before the
+// first tile (what workgroups of earlier grid rounds published for these
+// queries), so the first tile's selection already filters with them instead
+// of inserting everything until the first exchange lands
+#ifndef KNN_X_START
+#define KNN_X_START 1
+#endif
 #ifndef KNN_COUNT_SEL
 #define KNN_COUNT_SEL 0
 #endif
