@@ -251,6 +251,7 @@ static int build_train(knn_ctx* ctx, const double* dX, const int32_t* dlab, int6
   ctx->DPh = 0;
   ctx->DPs = 0;
   ctx->DPi = 0;
+  ctx->smp_kind = 0;  // the seeding sample is rebuilt for the new train set
   ctx->i8_off = false;
   ctx->fp16_off = false;
   ctx->auto_pending = false;
@@ -357,6 +358,62 @@ static int ensure_fp16_s3(knn_ctx* ctx, hipStream_t s) {
   memcpy(&dx2, &ctx->h_stats[3], 8);
   ctx->train.dxmax = std::sqrt(dx2) * (1.0 + 1e-12) + 0x1p-50 * std::sqrt(t.x2max);
   ctx->DPs = DPs;
+  return KNN_OK;
+}
+
+// Seeded thresholds (resident fp16 / int8 kernels with the global threshold).
+// Workgroups of the first grid round start with no published threshold: every
+// lane inserts nearly every row of its first tiles (a 10K-query batch runs
+// ~3 rounds, so a third of its workgroups).  A pre-pass runs the same kernel
+// over a strided sample of the train rows (its own image, built once per
+// train set: identical operands and seeds for those rows, hence identical
+// proxies) and seeds every query's slots with the need-th smallest proxy of
+// its sample lists (launch_seed_gthr).  Measured a net loss at cfg2, one
+// setting per process (gpurun_out/r3o_*.log): int8 candidate phase 1.40-1.43
+// ms off, 1.42-1.45 with 8192 rows, 1.44-1.46 with 16384, 1.53 with 32768;
+// fp16 2.28 off vs 2.47 -- the sample pass runs cold itself (every lane
+// inserts) and a sample-rank threshold saves little next to the thresholds
+// the first round publishes within a tile or two.  Off by default; tuning
+// key "seed": 0 / -1 off, N = sample rows (experiments).
+
+static int64_t seed_rows(const knn_ctx* ctx) {
+  if (ctx->tune_seed <= 0) return 0;
+  const int64_t ns = std::min<int64_t>(ctx->tune_seed, ctx->train.n / 8) / 256 * 256;
+  return ns < 4096 ? 0 : ns;
+}
+
+static int ensure_sample(knn_ctx* ctx, int kmetric, int DP, int64_t ns, hipStream_t s) {
+  const TrainDev& t = ctx->train;
+  if (ctx->smp_kind == kmetric && ctx->smp_dp == DP && ctx->smp_n == ns &&
+      (kmetric == 5 || ctx->smp_swz == ctx->xh_swz))
+    return KNN_OK;
+  const int d = t.d;
+  const int64_t stride = t.n / ns;  // sample row i = train row i * stride
+  const size_t row_bytes = kmetric == 5 ? (size_t)DP + 16 : (size_t)(DP / 2 + 4) * 4;
+  int rc;
+  if ((rc = ctx->smp_x64.ensure((size_t)ns * d * sizeof(double)))) return rc;
+  if ((rc = ctx->smp_xl2.ensure((size_t)ns * sizeof(float)))) return rc;
+  if ((rc = ctx->smp_img.ensure((size_t)ns * row_bytes + 1024))) return rc;
+  if ((rc = ctx->smp_scr.ensure(16))) return rc;
+  HIP_TRY(hipMemcpy2DAsync(ctx->smp_x64.p, (size_t)d * 8, t.X64, (size_t)stride * d * 8,
+                           (size_t)d * 8, (size_t)ns, hipMemcpyDeviceToDevice, s));
+  HIP_TRY(hipMemsetAsync(ctx->smp_scr.p, 0, 16, s));
+  if (kmetric == 5) {
+    launch_prep_i8_train((const double*)ctx->smp_x64.p, (const double*)ctx->i8_cent.p, ns, d, DP, ns,
+                         ctx->i8_s, (signed char*)ctx->smp_img.p, (unsigned*)ctx->smp_scr.p, s);
+  } else {
+    // the fp16 image's seeds are the rows' fl32 ||x'||^2 of the main copy
+    HIP_TRY(hipMemcpy2DAsync(ctx->smp_xl2.p, 4, t.xinit_l2, (size_t)stride * 4, 4, (size_t)ns,
+                             hipMemcpyDeviceToDevice, s));
+    launch_prep_half_train((const double*)ctx->smp_x64.p, t.mu, ns, d, DP, ns, t.jx,
+                           (unsigned short*)ctx->smp_img.p, (const float*)ctx->smp_xl2.p,
+                           (unsigned long long*)ctx->smp_scr.p, ctx->xh_swz, s);
+  }
+  HIP_TRY(hipGetLastError());
+  ctx->smp_kind = kmetric;
+  ctx->smp_dp = DP;
+  ctx->smp_swz = ctx->xh_swz;
+  ctx->smp_n = ns;
   return KNN_OK;
 }
 
@@ -785,8 +842,33 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   // (experiment, tuning "ablate" bit 5: keep the previous call's final
   // thresholds -- valid only for a repeat of the same queries; measures what
   // perfectly seeded thresholds would save)
-  if (use_gthr && !(ctx->tune_ablate & 32))
-    launch_fill_gthr(cl.gthr, m_pad, std::min(S, gk ? 8 : 4), s);
+  if (use_gthr && !(ctx->tune_ablate & 32)) {
+    const int active = std::min(S, gk ? 8 : 4);
+    const int64_t ns = (kmetric == 4 || kmetric == 5) && !s3 ? seed_rows(ctx) : 0;
+    bool seeded = false;
+    if (ns > 0) {
+      // seeded thresholds (see seed_rows): the pre-pass over the sample
+      if ((rc = ensure_sample(ctx, kmetric, DP, ns, s))) return rc;
+      const int Ss = (int)std::max<int64_t>(1, std::min<int64_t>(16, ns / trows / 4));
+      const int Us = 4 * Ss * R;  // quad lists: 4 per query per split
+      if ((rc = ctx->smp_v.ensure((size_t)m_pad * Us * sizeof(float)))) return rc;
+      if ((rc = ctx->smp_i.ensure((size_t)m_pad * Us * sizeof(int)))) return rc;
+      CandLaunch cs = cl;
+      cs.X32 = (const float*)ctx->smp_img.p;
+      cs.n_pad = ns;
+      cs.S = Ss;
+      cs.out_v = (float*)ctx->smp_v.p;
+      cs.out_i = (int*)ctx->smp_i.p;
+      cs.gthr = nullptr;
+      cs.ablate = 0;
+      if (launch_cand(cs, s)) {
+        launch_seed_gthr((const float*)ctx->smp_v.p, m_pad, Us, gk ? kGthrSlots * gk : 4 * R, active,
+                         cl.gthr, s);
+        seeded = true;
+      }
+    }
+    if (!seeded) launch_fill_gthr(cl.gthr, m_pad, active, s);
+  }
   if (s3h)
     launch_cand_s3h((const unsigned short*)ctx->XT16.p, (const float*)ctx->XS16.p,
                     (const unsigned short*)ctx->Q32.p, DP, n_pad3, R, S, n_qt, cl.out_v, cl.out_i,
@@ -1197,6 +1279,9 @@ int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value) {
   } else if (!strcmp(key, "i8")) {
     if (value < -1 || value > 1) return knn_fail(KNN_ERR_ARG, "i8 must be -1, 0 or 1");
     ctx->tune_i8 = (int)value;
+  } else if (!strcmp(key, "seed")) {
+    if (value < -1) return knn_fail(KNN_ERR_ARG, "seed must be -1 (auto), 0 (off) or sample rows");
+    ctx->tune_seed = value;
   } else if (!strcmp(key, "ties")) {
     if (value < 0 || value > 2) return knn_fail(KNN_ERR_ARG, "ties must be 0, 1 or 2");
     ctx->tune_ties = (int)value;

@@ -63,6 +63,11 @@ struct knn_ctx {
   int tune_i8 = -1;            // int8 candidate pass: -1 auto, 0 off, 1 on (where the data allow)
   int tune_ties = 1;           // reference tie order: 0 off, 1 vote-affecting ties, 2 all ties
   int tune_m16 = -1;           // bf16x3 on the 16x16x32 MFMA layout: -1 auto, 0 off, 1 on
+  int64_t tune_seed = 0;       // seeded thresholds: 0 / -1 off, N sample rows (experiment)
+  // sample image of the seeding pre-pass (strided train rows in the image
+  // format of kernel metric smp_kind at width smp_dp; 0 = not built)
+  int smp_kind = 0, smp_dp = 0, smp_swz = -1;
+  int64_t smp_n = 0;
   int last_nw = 0;
   int last_kmetric = -1; // candidate kernel metric of the last search (knn_kernels.h)
   char last_kernel[96] = {0};  // name of the last candidate kernel launched
@@ -78,6 +83,7 @@ struct knn_ctx {
   // int8 image: codes [n_pad][DP + 16 B]; per-dim centres [code units d |
   // value units d] (the latter the merge's mu for this pass); grid stats scratch
   DevBuf XI, i8_cent, i8_gs;
+  DevBuf smp_x64, smp_xl2, smp_img, smp_scr, smp_v, smp_i;
   // per-classify workspace
   DevBuf Q64, Q32, qvalid, cand_v, cand_i, gthr, rescan_q, rescan_tau, rescan_cnt, fr_cnt, fr_buf,
       fr_q, fr_thr, slow_q, totals, lk, rescan_mask, rescan_nkeep;

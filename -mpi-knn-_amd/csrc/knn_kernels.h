@@ -119,6 +119,9 @@ constexpr uint32_t kGthrInit = 0xFF800000u;  // order-preserving key of +inf
 constexpr int kGthrSlots = 8;                // slots per query in gthr
 // gthr init: slots [0, active) = +inf keys, the rest 0 (never the max)
 void launch_fill_gthr(uint32_t* g, int64_t m_pad, int active, hipStream_t s);
+// seeded thresholds: the need-th smallest of each query's U pre-pass list entries
+void launch_seed_gthr(const float* v, int64_t m_pad, int U, int need, int active, uint32_t* g,
+                      hipStream_t s);
 
 // Candidate-pass operands are centred on the train column means mu (see knn_prep.hip).
 int col_mean_blocks(int64_t n);  // rows of the `partial` scratch (x d doubles)

@@ -497,6 +497,41 @@ __global__ void fill_gthr_kernel(uint32_t* g, int64_t n, int active) {
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256)
     g[e] = (int)(e % kGthrSlots) < active ? kGthrInit : 0u;
 }
+// Threshold seeding: per query, the need-th smallest proxy of the union of
+// its lists from the pre-pass over a strided sample of the train rows (U
+// entries; +inf entries are empty) into every active slot (0 elsewhere, as
+// the fill).  tq = max over the slots then has >= need distinct rows at or
+// below it whatever mix of this value and the main pass's publishes the
+// slots hold (knn_api.cpp, seeded thresholds).  One wave per query.
+__global__ void __launch_bounds__(256)
+seed_gthr_kernel(const float* __restrict__ v, int64_t m_pad, int U, int need, int active,
+                 uint32_t* __restrict__ g) {
+  const int lane = threadIdx.x & 63;
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= m_pad) return;
+  const float* lv = v + q * U;
+  int fin = 0;
+  for (int x = lane; x < U; x += 64) fin += f2key(lv[x]) < kKeyInf;
+  fin = wave_sum_i(fin);
+  uint32_t pre = kKeyInf;
+  if (fin >= need) {
+    pre = 0;  // radix select: key of the need-th smallest
+    for (int b = 31; b >= 0; --b) {
+      const uint32_t T = pre | ((1u << b) - 1u);
+      int cnt = 0;
+      for (int x = lane; x < U; x += 64) cnt += f2key(lv[x]) <= T;
+      if (wave_sum_i(cnt) < need) pre |= 1u << b;
+    }
+  }
+  if (lane < kGthrSlots) g[q * kGthrSlots + lane] = lane < active ? pre : 0u;
+}
+void launch_seed_gthr(const float* v, int64_t m_pad, int U, int need, int active, uint32_t* g,
+                      hipStream_t s) {
+  if (m_pad <= 0) return;
+  hipLaunchKernelGGL(seed_gthr_kernel, dim3((unsigned)((m_pad + 3) / 4)), dim3(256), 0, s, v, m_pad,
+                     U, need, active, g);
+}
+
 void launch_fill_gthr(uint32_t* g, int64_t m_pad, int active, hipStream_t s) {
   const int64_t n = m_pad * kGthrSlots;
   if (n <= 0) return;

@@ -228,7 +228,10 @@ const char* knn_last_kernel_name(knn_ctx* ctx);
  * entries (resident kernel) / no exchange (S3), K = 1..16 the K-th smallest
  * of a workgroup's union of a query's lists; results stay exact); "ties"
  * (the reference's std::sort order for tied queries: 0 off, 1 (default) the
- * queries whose label it can change, 2 every query with a tie in its top k). */
+ * queries whose label it can change, 2 every query with a tie in its top k);
+ * "seed" (experiment: seeded global thresholds of the fp16 / int8 resident
+ * kernels from a pre-pass over N strided train rows; 0 / -1 off, the
+ * default -- measured slower; results stay exact). */
 int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value);
 
 /* Synchronise the context's stream. */

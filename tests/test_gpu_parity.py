@@ -347,6 +347,34 @@ def test_targeted_rescan(knn, path):
     assert rescans > 0, "expected certification failures with 2-3 splits"
 
 
+@pytest.mark.parametrize("path", ["i8", "fp16"])
+def test_seeded_thresholds(knn, path):
+    """Seeded global thresholds (knn_api.cpp seed_rows / ensure_sample; an
+    experiment option, off by default): a pre-pass of the same candidate
+    kernel over a strided sample of the train rows seeds every query's slots
+    with the need-th smallest of its sample lists; exact answers with and
+    without it, and after a new train set (the sample image is rebuilt)."""
+    rng = np.random.default_rng(321)
+    if path == "i8":
+        tr, lab, te = _grid_codes(rng, 40000, 4500, 64, 6)
+    else:
+        cen = rng.uniform(-1, 1, (6, 64))
+        lab_all = rng.integers(0, 6, 44500).astype(np.int32)
+        X = cen[lab_all] + 0.35 * rng.standard_normal((44500, 64))
+        tr, te, lab = X[:40000].copy(), X[40000:].copy(), lab_all[:40000].copy()
+    for seed in (0, 8192, 32768):
+        c = knn.Classifier(0)
+        if path == "fp16":
+            c.set_precision(knn.PRECISION_FP16)
+        c.set_tuning("seed", seed)
+        run_case(c, knn, tr, lab, te, 10, 0, 6)
+        assert c.last_candidate_path() == (5 if path == "i8" else 4)
+        # a second train set through the same context: the sample is rebuilt
+        run_case(c, knn, tr[::-1].copy(), lab[::-1].copy(), te, 10, 0, 6)
+        assert c.last_candidate_path() == (5 if path == "i8" else 4)
+        c.close()
+
+
 def test_k_zero_and_errors(clf, knn):
     rng = np.random.default_rng(3)
     tr, lab, te = _mix(rng, 500, 10, 8, 2)
