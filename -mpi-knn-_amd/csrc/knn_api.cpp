@@ -934,6 +934,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   rb.nkeep = sm.nkeep;
   rb.S = sm.S;
   rb.trows = sm.trows;
+  rb.cus = ctx->cu_count;
   // (timing-only ablations leave every query uncertified: no rescan then)
   const bool abl = ctx->tune_ablate & 27;
   launch_rescan(metric, t, dQ, rb, abl ? 0 : cap, W, err_factor(metric, t.DP), sink,

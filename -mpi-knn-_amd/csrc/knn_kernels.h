@@ -196,6 +196,7 @@ struct RescanBufs {
   const int* nkeep;          // [cap] rows the merge already put in buf (null: none)
   int S;                     // splits / tile rows of the candidate launch (mask bits)
   int64_t trows;
+  int cus;                   // compute units (the staged filter's grid)
 };
 // Enqueues the whole rescan path (prep, filter, exact finish, full scan);
 // every kernel reads the counts on the device.  f_err: the fp32 candidate

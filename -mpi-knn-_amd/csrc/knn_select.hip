@@ -227,7 +227,8 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
   const bool q_in_lds = d <= kMergeLdsDim;
   double* dk = (double*)smem + (q_in_lds ? d : 0);
   double* tb = dk + C2;
-  int* di = (int*)(tb + NT * 17);
+  // (exact_sorted stages at most min(NT, C2) rows per batch: cn <= C2)
+  int* di = (int*)(tb + min(NT, C2) * 17);
   int* ls = di + C2;
   const int64_t q = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -496,8 +497,10 @@ static void launch_mr(const float* cv, const int* ci, int U, int R, const TrainD
                       const double* Q64, int64_t m, int W, int Cmax, int C2, double f_err,
                       ProxyScale ps, const uint32_t* gthr, const Sink& sink, int* rescan_q,
                       double* rescan_tau, int* rescan_cnt, const SplitMap& sm, hipStream_t s) {
+  // (the staging tile only as large as the candidate set: a smaller
+  // footprint keeps more of these latency-bound workgroups per CU)
   const size_t lds = (size_t)(t.d <= kMergeLdsDim ? t.d : 0) * 8 + (size_t)C2 * 8 +
-                     (size_t)NT * 17 * 8 + (size_t)C2 * 8;
+                     (size_t)std::min(NT, C2) * 17 * 8 + (size_t)C2 * 8;
   hipLaunchKernelGGL((merge_rerank_kernel<METRIC, NT, EPL>), dim3((unsigned)m), dim3(NT), lds, s,
                      cv, ci, U, R, t, Q64, W, Cmax, C2, f_err, ps, gthr, sink, rescan_q, rescan_tau,
                      rescan_cnt, sm);
@@ -999,8 +1002,9 @@ void launch_rescan(int metric, const TrainDev& t, const double* Q64, const Resca
       const size_t tile = (size_t)64 * (t.DP + 4) * 4;
       const int nwb = (int)std::max<size_t>(1, std::min<size_t>(4, (150 * 1024 - qbytes) / tile));
       const int64_t rpb = 64 * nwb;
-      // (grid-stride over row blocks: a targeted rescan skips most of them)
-      const dim3 fg((unsigned)std::min<int64_t>((t.n_pad + rpb - 1) / rpb, 1024));
+      // (grid-stride over row blocks: a targeted rescan skips most of them;
+      // one block per CU -- its ~150 KiB of LDS admits no second one)
+      const dim3 fg((unsigned)std::min<int64_t>((t.n_pad + rpb - 1) / rpb, std::max(1, rb.cus)));
       const size_t flds = qbytes + nwb * tile;
       if (metric == 0)
         hipLaunchKernelGGL((rescan_filter_kernel<0, FQ>), fg, dim3(64 * nwb), flds, s, t, rb.qf,
