@@ -134,17 +134,19 @@ __device__ __forceinline__ int lanes_below(unsigned long long mask) {
 // (The squared difference is formed from the same fp64 operands in the
 // same operation as before the prefetch: the result bits are unchanged.)
 // Pads [cn, C2) with (+inf, INT_MAX) and sorts (dist, idx) ascending.
-// All NT threads; tb holds NT x 17 doubles.
-template <int METRIC, int NT>
+// All NT threads; rows go in batches of RB = NT * EPT / 16 (tb holds RB x 17
+// doubles): EPT = 8 halves the prefetch registers where the candidate set
+// is at most NT / 2 rows.
+template <int METRIC, int NT, int EPT = 16>
 __device__ void exact_sorted(const TrainDev& t, const double* qv, int* di, double* dk, double* tb,
                              int cn, int C2, int tid) {
   const int d = t.d;
-  // the raw fp64 values of a 16-dim chunk, EPT per thread (nb * 16 <= NT * 16);
+  // the raw fp64 values of a 16-dim chunk, EPT per thread (nb * 16 <= NT * EPT);
   // two register sets in flight: chunk c+1's and c+2's loads overlap chunk c's
   // sums and barriers (rows of 7.7 KB at d = 960 make this an HBM stream)
-  constexpr int EPT = 16;
-  for (int b0 = 0; b0 < cn; b0 += NT) {
-    const int nb = min(NT, cn - b0);
+  constexpr int RB = NT * EPT / 16;
+  for (int b0 = 0; b0 < cn; b0 += RB) {
+    const int nb = min(RB, cn - b0);
     const int ne = nb * 16;
     auto fetch = [&](int c0, double (&o)[EPT]) {
 #pragma unroll
@@ -211,8 +213,9 @@ __device__ __forceinline__ bool bound_ok(double LB, double dw, double qa, double
   return (LB - E) * (1.0 - 1e-12) > dw * (1.0 + 1e-12);
 }
 
-template <int METRIC, int NT, int EPL>
+template <int METRIC, int NT, int EPL, int EPT = 16>
 __global__ void __launch_bounds__(NT)
+__attribute__((amdgpu_waves_per_eu(EPT == 8 ? 5 : 1)))
 merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, int U, int R,
                     TrainDev t, const double* __restrict__ Q64, int W, int Cmax, int C2,
                     double f_err, ProxyScale ps, const uint32_t* __restrict__ gthr, Sink sink,
@@ -422,7 +425,7 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
     return;
   }
 
-  exact_sorted<METRIC, NT>(t, qv, di, dk, tb, cn, C2, tid);
+  exact_sorted<METRIC, NT, EPT>(t, qv, di, dk, tb, cn, C2, tid);
 
   // certification: every row not re-ranked has proxy >= LB, hence exact
   // distance >= the bound below (rigorous error bound E)
@@ -492,7 +495,7 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
   }
 }
 
-template <int METRIC, int NT, int EPL>
+template <int METRIC, int NT, int EPL, int EPT = 16>
 static void launch_mr(const float* cv, const int* ci, int U, int R, const TrainDev& t,
                       const double* Q64, int64_t m, int W, int Cmax, int C2, double f_err,
                       ProxyScale ps, const uint32_t* gthr, const Sink& sink, int* rescan_q,
@@ -501,7 +504,7 @@ static void launch_mr(const float* cv, const int* ci, int U, int R, const TrainD
   // footprint keeps more of these latency-bound workgroups per CU)
   const size_t lds = (size_t)(t.d <= kMergeLdsDim ? t.d : 0) * 8 + (size_t)C2 * 8 +
                      (size_t)std::min(NT, C2) * 17 * 8 + (size_t)C2 * 8;
-  hipLaunchKernelGGL((merge_rerank_kernel<METRIC, NT, EPL>), dim3((unsigned)m), dim3(NT), lds, s,
+  hipLaunchKernelGGL((merge_rerank_kernel<METRIC, NT, EPL, EPT>), dim3((unsigned)m), dim3(NT), lds, s,
                      cv, ci, U, R, t, Q64, W, Cmax, C2, f_err, ps, gthr, sink, rescan_q, rescan_tau,
                      rescan_cnt, sm);
 }
@@ -518,21 +521,26 @@ void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int
   int C2 = 1;
   while (C2 < C) C2 <<= 1;
   const bool big = C2 > 64, wide = U > 1024;
-#define KNN_MR(M_, NT_, EPL_) \
-  launch_mr<M_, NT_, EPL_>(cv, ci, U, R, t, Q64, m, W, C, C2, f_err, ps, gthr, sink, rescan_q, \
-                           rescan_tau, rescan_cnt, sm, s)
+#define KNN_MR(M_, NT_, EPL_) KNN_MRE(M_, NT_, EPL_, 16)
+#define KNN_MRE(M_, NT_, EPL_, EPT_) \
+  launch_mr<M_, NT_, EPL_, EPT_>(cv, ci, U, R, t, Q64, m, W, C, C2, f_err, ps, gthr, sink,  \
+                                 rescan_q, rescan_tau, rescan_cnt, sm, s)
   // fewer entries per lane when the union is small (cfg2: 152 lists x 4 =
   // 608 entries -> 10 per lane): every radix-select step and the selection
   // loops run over EPL unrolled entries
   const bool narrow = U <= 640;
   if (metric == 0) {
     if (big) { if (wide) KNN_MR(0, 256, 32); else KNN_MR(0, 256, 16); }
-    else { if (wide) KNN_MR(0, 64, 32); else if (narrow) KNN_MR(0, 64, 10); else KNN_MR(0, 64, 16); }
+    // (candidate sets of <= 32 rows, cfg2's 27: half the prefetch registers,
+    // 4 waves per SIMD for this latency-bound kernel)
+    else { if (wide) KNN_MR(0, 64, 32); else if (narrow && C2 <= 32) KNN_MRE(0, 64, 10, 8);
+           else if (narrow) KNN_MR(0, 64, 10); else KNN_MR(0, 64, 16); }
   } else {
     if (big) { if (wide) KNN_MR(1, 256, 32); else KNN_MR(1, 256, 16); }
     else { if (wide) KNN_MR(1, 64, 32); else KNN_MR(1, 64, 16); }
   }
 #undef KNN_MR
+#undef KNN_MRE
 }
 
 // ------------------------------------------------- rescan (device-driven)
