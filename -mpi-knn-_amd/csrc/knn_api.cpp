@@ -435,13 +435,14 @@ static bool use_fp16(const knn_ctx* ctx, int metric, int64_t m, int W) {
 }
 
 // int8 candidate pass (kernel metric 5): integer-coded train sets (detect_i8)
-// at d <= 256 for batches of >= 4096 queries, in AUTO and FP16 modes, until a
+// at d <= 256 for batches of >= 4096 queries, in AUTO mode only, until a
 // batch sends more than 1/16 of its queries to the rescan (queries off the
-// train set's grid).  Tuning key "i8": -1 auto, 0 off, 1 on (where possible).
+// train set's grid).  Tuning key "i8": -1 auto, 0 off, 1 on (where possible);
+// "fp16" = 1 (an explicit fp16 request) turns it off, "fp16" = 0 does not.
 static bool use_i8(const knn_ctx* ctx, int metric, int64_t m, int W) {
   if (metric != KNN_METRIC_L2 || !ctx->i8_ok || pad_dim_i8(ctx->train.d) <= 0) return false;
   if (ctx->tune_i8 >= 0) return ctx->tune_i8 > 0;
-  if (ctx->tune_fp16 >= 0) return false;  // an explicit fp16 request
+  if (ctx->tune_fp16 == 1) return false;
   if (ctx->precision != KNN_PRECISION_AUTO || ctx->i8_off) return false;
   return m >= 4096 && W <= kQuadMaxW;
 }
@@ -653,9 +654,19 @@ static void auto_check(knn_ctx* ctx) {
 // across the k-th place within reach of the runner-up: finish_single),
 // 2 every query with equal distances in its top k (neighbour indices in the
 // reference's order too).
+// (Partial lists stay ordered by (dist, global idx): the reference's order
+// over the whole train set is restored after the merge, knn_tie_resolve_device.)
 static int tie_mask_of(const knn_ctx* ctx, const Sink& sink) {
-  if (sink.mode != MODE_SINGLE) return 0;  // partial lists: ordered by (dist, global idx)
+  if (sink.mode != MODE_SINGLE) return 0;
   return ctx->tune_ties;
+}
+
+// Scratch of the reference-order passes: tie_scratch_bytes per concurrent
+// workgroup, at most 32 workgroups and ~512 MB (at least one: n * 20 B); the
+// passes loop over their queued queries, which are rare.
+static int tie_workgroups(const knn_ctx* ctx, int64_t per) {
+  return (int)std::max<int64_t>(
+      1, std::min<int64_t>({(int64_t)32, (int64_t)ctx->cu_count, (512ll << 20) / per}));
 }
 
 int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
@@ -669,9 +680,9 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   int tie_nwg = 0;
   if (sink.tie_mode) {
     // scratch for the reference-order pass: every row's distance per
-    // workgroup, at most ~2 GB in all (tied queries are rare; the pass loops)
+    // workgroup (tied queries are rare; the pass loops over them)
     tie_per = tie_scratch_bytes(t.n, ctx->class_cnt);
-    tie_nwg = (int)std::max<int64_t>(1, std::min<int64_t>(ctx->cu_count, (2ll << 30) / tie_per));
+    tie_nwg = tie_workgroups(ctx, tie_per);
     if ((rc = ctx->tie_q.ensure((size_t)m * sizeof(int) + 16))) return rc;
     if ((rc = ctx->tie_ws.ensure((size_t)(tie_per * tie_nwg)))) return rc;
     sink.tie_q = (int*)ctx->tie_q.p;
@@ -972,7 +983,7 @@ static int run_large_k(knn_ctx* ctx, const double* dQ, int64_t m, int W, int met
   int tie_nwg = 0;
   if (sink.tie_mode) {  // tied queries: queued by large_k_kernel for the reference-order pass
     tie_per = tie_scratch_bytes(t.n, ctx->class_cnt);
-    tie_nwg = (int)std::max<int64_t>(1, std::min<int64_t>(ctx->cu_count, (2ll << 30) / tie_per));
+    tie_nwg = tie_workgroups(ctx, tie_per);
     if ((rc = ctx->tie_q.ensure((size_t)m * sizeof(int) + 16))) return rc;
     if ((rc = ctx->tie_ws.ensure((size_t)(tie_per * tie_nwg)))) return rc;
     if ((rc = ctx->rescan_cnt.ensure(4 * sizeof(int)))) return rc;
@@ -1119,8 +1130,62 @@ int knn_merge_vote_device(knn_ctx* ctx, const double* d_dist, const int64_t* d_i
   // unions beyond the LDS kernel's 4096 entries: rank merge through scratch
   if (const int64_t sb = merge_scratch_bytes(parts, w, k, mq))
     if ((rc = ctx->mrg.ensure((size_t)sb))) return rc;
+  MergeTies mt;
+  mt.mode = ctx->tune_ties;
   launch_merge_vote_partials(d_dist, d_idx, d_lab, parts, m, w, k, d_labels, d_out_idx,
-                             d_out_dist, d_flags, s, q0, mq, 0, ctx->mrg.p);
+                             d_out_dist, d_flags, s, q0, mq, 0, ctx->mrg.p, mt);
+  HIP_TRY(hipGetLastError());
+  return KNN_OK;
+}
+
+int knn_shard_distances_device(knn_ctx* ctx, const double* dQ, const int32_t* d_qsel,
+                               int32_t nsel, int32_t metric, double* d_out, void* stream) {
+  int rc;
+  if ((rc = device_guard(ctx))) return rc;
+  if (!ctx->trained) return knn_fail(KNN_ERR_STATE, "shard distances before set_train");
+  if (nsel < 0 || metric < 0 || metric > 1) return knn_fail(KNN_ERR_ARG, "bad shard distance arguments");
+  if (nsel == 0) return KNN_OK;
+  if (!dQ || !d_out) return knn_fail(KNN_ERR_ARG, "null pointer");
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  launch_shard_dist(metric, ctx->train, dQ, d_qsel, nsel, d_out, s);
+  HIP_TRY(hipGetLastError());
+  return KNN_OK;
+}
+
+int knn_tie_resolve_device(knn_ctx* ctx, const double* d_D, int32_t parts, const int64_t* rows,
+                           int32_t nsel, const int32_t* d_lab_all, const int32_t* d_orow,
+                           int32_t k, int32_t* d_labels, int64_t* d_idx, double* d_dist,
+                           int32_t* d_flags, void* stream) {
+  int rc;
+  if ((rc = device_guard(ctx))) return rc;
+  if (!ctx->trained) return knn_fail(KNN_ERR_STATE, "tie resolve before set_train");
+  if (parts <= 0 || parts > kMaxParts || nsel < 0 || !rows)
+    return knn_fail(KNN_ERR_ARG, "bad tie resolve geometry (1 <= parts <= 64)");
+  PartRows pr{};
+  pr.parts = parts;
+  for (int p = 0; p < parts; p++) {
+    if (rows[p] < 0) return knn_fail(KNN_ERR_ARG, "negative part rows");
+    pr.off[p + 1] = pr.off[p] + rows[p];
+  }
+  const int64_t n = pr.off[parts];
+  if (n <= 0 || n >= (int64_t)INT32_MAX) return knn_fail(KNN_ERR_ARG, "total rows must be in [1, 2^31)");
+  if (k <= 0 || k > n) return knn_fail(KNN_ERR_ARG, "k must be in [1, total rows]");
+  if (nsel == 0) return KNN_OK;
+  if (!d_D || !d_lab_all || !d_orow || !d_labels) return knn_fail(KNN_ERR_ARG, "null pointer");
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  const int64_t per = tie_scratch_bytes(n, ctx->class_cnt);
+  const int nwg = std::min<int>(tie_workgroups(ctx, per), nsel);
+  if ((rc = ctx->tie_ws.ensure((size_t)(per * nwg)))) return rc;
+  Sink sink{};
+  sink.mode = MODE_SINGLE;
+  sink.k = k;
+  sink.labels = d_labels;
+  sink.idx = d_idx;
+  sink.dist = d_dist;
+  sink.flags = d_flags;
+  launch_tie_resolve(d_D, pr, nsel, d_lab_all, d_orow, ctx->class_cnt,
+                     (unsigned char*)ctx->tie_ws.p, per, nwg, sink,
+                     (unsigned long long*)ctx->totals.p + 2, s);
   HIP_TRY(hipGetLastError());
   return KNN_OK;
 }
@@ -1281,7 +1346,7 @@ int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value) {
     if (value < -1 || value > 1) return knn_fail(KNN_ERR_ARG, "i8 must be -1, 0 or 1");
     ctx->tune_i8 = (int)value;
   } else if (!strcmp(key, "seed")) {
-    if (value < -1) return knn_fail(KNN_ERR_ARG, "seed must be -1 (auto), 0 (off) or sample rows");
+    if (value < -1) return knn_fail(KNN_ERR_ARG, "seed must be 0 / -1 (off) or N = sample rows");
     ctx->tune_seed = value;
   } else if (!strcmp(key, "ties")) {
     if (value < 0 || value > 2) return knn_fail(KNN_ERR_ARG, "ties must be 0, 1 or 2");

@@ -10,11 +10,22 @@
 //   mode 1, train-sharded: GPU g holds rows [n*g/G, n*(g+1)/G); queries are
 //     broadcast; each GPU computes its exact local top-(k+1) (with global
 //     indices and labels); ncclAllGather exchanges the lists; GPU g k-way
-//     merges and votes queries [m*g/G, m*(g+1)/G).
+//     merges and votes queries [m*g/G, m*(g+1)/G).  Queries whose label the
+//     reference's order among equal distances decides (its std::sort over
+//     the whole train set, cpp:366) are rare: their exact distances to every
+//     shard's rows go to the owner by ncclSend/ncclRecv, which re-sorts them
+//     as the reference does (knn_tie_resolve_device).
+// Transport (knn_group_transport): RCCL between distinct devices, also at
+// G = 1 on request (KNN_GROUP_RCCL: a one-rank communicator, every
+// collective of the path through RCCL); ranks sharing a device (repeated
+// entries in devs) exchange by stream-ordered device copies ("loopback"):
+// the whole G-rank decomposition, offsets and merges on fewer GPUs.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <string>
 #include <thread>
 #include <vector>
@@ -23,22 +34,29 @@
 #include "knn_api_internal.h"
 #include "knn_kernels.h"
 
+enum { XPORT_NONE = 0, XPORT_RCCL = 1, XPORT_LOOPBACK = 2 };
+
 struct knn_group {
   int ndev = 0;
   int mode = 0;
+  int transport = XPORT_NONE;
   std::vector<int> devs;
   std::vector<knn_ctx*> ctx;
   std::vector<ncclComm_t> comms;
   std::vector<DevBuf> X, lab;                  // per-device train rows (full or shard)
+  std::vector<DevBuf> labA;                    // mode 1: every train label (reference tie order)
   std::vector<DevBuf> Q, olab, oidx, odist, oflags;
   std::vector<DevBuf> pk, gk;                  // train-sharded packed partial / gathered lists
+  std::vector<DevBuf> tq, tcnt, tsel, trow, tsend, trecv;  // reference tie order exchange
   std::vector<DevBuf> nX, nmm;                 // normalisation shards / per-dim bounds
   std::vector<hipEvent_t> ev0, ev1;            // per device: around the last call's device work
+  std::vector<hipEvent_t> evx;                 // loopback: cross-rank stream ordering
   int64_t n = 0;
   int d = 0;
   int class_cnt = 0;
   bool trained = false;
   double last_compute = 0.0;
+  int64_t last_ties = 0;                       // mode 1: queries resolved by the exchange (last call)
 };
 
 #define HIP_G(expr)                                                                       \
@@ -72,16 +90,156 @@ static int for_each_dev(knn_group* g, F f) {
   return KNN_OK;
 }
 
+static hipStream_t stream_of(knn_group* g, int i) { return g->ctx[i]->stream; }
+
+// ---- collectives of the group (one call covers every rank)
+
+// loopback: every rank's stream waits for what every other rank's stream
+// has queued so far (before a copy: its sources are complete; after: no
+// rank overwrites a source another rank is still reading)
+static int lb_barrier(knn_group* g) {
+  for (int i = 0; i < g->ndev; i++) {
+    HIP_G(hipSetDevice(g->devs[i]));
+    HIP_G(hipEventRecord(g->evx[i], stream_of(g, i)));
+  }
+  for (int i = 0; i < g->ndev; i++) {
+    HIP_G(hipSetDevice(g->devs[i]));
+    for (int j = 0; j < g->ndev; j++)
+      if (j != i) HIP_G(hipStreamWaitEvent(stream_of(g, i), g->evx[j], 0));
+  }
+  return KNN_OK;
+}
+
+// buf[i] <- buf[root] for every rank i (count elements of `type`, esize B each)
+static int coll_bcast(knn_group* g, const std::vector<void*>& buf, size_t count,
+                      ncclDataType_t type, size_t esize, int root) {
+  if (g->transport == XPORT_RCCL) {
+    NCCL_G(ncclGroupStart());
+    for (int i = 0; i < g->ndev; i++)
+      NCCL_G(ncclBroadcast(buf[root], buf[i], count, type, root, g->comms[i], stream_of(g, i)));
+    NCCL_G(ncclGroupEnd());
+  } else if (g->transport == XPORT_LOOPBACK) {
+    int rc;
+    if ((rc = lb_barrier(g))) return rc;
+    for (int i = 0; i < g->ndev; i++) {
+      if (i == root) continue;
+      HIP_G(hipSetDevice(g->devs[i]));
+      HIP_G(hipMemcpyAsync(buf[i], buf[root], count * esize, hipMemcpyDeviceToDevice,
+                           stream_of(g, i)));
+    }
+    return lb_barrier(g);
+  }
+  return KNN_OK;
+}
+
+// recv[i][j * bytes ..] <- send[j] for every rank pair
+static int coll_allgather(knn_group* g, const std::vector<void*>& send,
+                          const std::vector<void*>& recv, size_t bytes) {
+  if (g->transport == XPORT_RCCL) {
+    NCCL_G(ncclGroupStart());
+    for (int i = 0; i < g->ndev; i++)
+      NCCL_G(ncclAllGather(send[i], recv[i], bytes, ncclUint8, g->comms[i], stream_of(g, i)));
+    NCCL_G(ncclGroupEnd());
+  } else if (g->transport == XPORT_LOOPBACK) {
+    int rc;
+    if ((rc = lb_barrier(g))) return rc;
+    for (int i = 0; i < g->ndev; i++) {
+      HIP_G(hipSetDevice(g->devs[i]));
+      for (int j = 0; j < g->ndev; j++)
+        HIP_G(hipMemcpyAsync((unsigned char*)recv[i] + j * bytes, send[j], bytes,
+                             hipMemcpyDeviceToDevice, stream_of(g, i)));
+    }
+    return lb_barrier(g);
+  }
+  return KNN_OK;
+}
+
+// mm[i] = [max | min] (2d doubles): MAX over ranks of the first d, MIN of the
+// rest (≙ the two MPI_Allreduce of cpp:276-277)
+static int coll_allreduce_maxmin(knn_group* g, const std::vector<double*>& mm, int d) {
+  if (g->transport == XPORT_RCCL) {
+    NCCL_G(ncclGroupStart());
+    for (int i = 0; i < g->ndev; i++) {
+      NCCL_G(ncclAllReduce(mm[i], mm[i], d, ncclFloat64, ncclMax, g->comms[i], stream_of(g, i)));
+      NCCL_G(ncclAllReduce(mm[i] + d, mm[i] + d, d, ncclFloat64, ncclMin, g->comms[i],
+                           stream_of(g, i)));
+    }
+    NCCL_G(ncclGroupEnd());
+  } else if (g->transport == XPORT_LOOPBACK) {
+    // (test transport) folded on the host in rank order with strict compares
+    std::vector<double> acc((size_t)2 * d), v((size_t)2 * d);
+    for (int i = 0; i < g->ndev; i++) {
+      HIP_G(hipSetDevice(g->devs[i]));
+      HIP_G(hipMemcpyAsync(v.data(), mm[i], v.size() * 8, hipMemcpyDeviceToHost, stream_of(g, i)));
+      HIP_G(hipStreamSynchronize(stream_of(g, i)));
+      for (int c = 0; c < 2 * d; c++)
+        if (i == 0 || (c < d ? v[c] > acc[c] : v[c] < acc[c])) acc[c] = v[c];
+    }
+    for (int i = 0; i < g->ndev; i++) {
+      HIP_G(hipSetDevice(g->devs[i]));
+      HIP_G(hipMemcpyAsync(mm[i], acc.data(), acc.size() * 8, hipMemcpyHostToDevice, stream_of(g, i)));
+      HIP_G(hipStreamSynchronize(stream_of(g, i)));
+    }
+  }
+  return KNN_OK;
+}
+
+// All-to-all of doubles: rank a sends cnt[a][b] doubles from send[a] + soff[a][b]
+// to rank b, which receives them at recv[b] + roff[b][a].
+static int coll_alltoallv(knn_group* g, const std::vector<double*>& send,
+                          const std::vector<double*>& recv,
+                          const std::vector<std::vector<int64_t>>& cnt,
+                          const std::vector<std::vector<int64_t>>& soff,
+                          const std::vector<std::vector<int64_t>>& roff) {
+  const int G = g->ndev;
+  if (g->transport == XPORT_LOOPBACK) {
+    int rc;
+    if ((rc = lb_barrier(g))) return rc;
+  }
+  // a rank's own block (and every block without a transport): a device copy
+  for (int a = 0; a < G; a++)
+    for (int b = 0; b < G; b++) {
+      if (cnt[a][b] <= 0 || (a != b && g->transport == XPORT_RCCL)) continue;
+      HIP_G(hipSetDevice(g->devs[b]));
+      HIP_G(hipMemcpyAsync(recv[b] + roff[b][a], send[a] + soff[a][b], cnt[a][b] * 8,
+                           hipMemcpyDeviceToDevice, stream_of(g, b)));
+    }
+  if (g->transport == XPORT_RCCL && G > 1) {
+    NCCL_G(ncclGroupStart());
+    for (int a = 0; a < G; a++)
+      for (int b = 0; b < G; b++) {
+        if (a == b) continue;
+        if (cnt[a][b] > 0)
+          NCCL_G(ncclSend(send[a] + soff[a][b], (size_t)cnt[a][b], ncclFloat64, b, g->comms[a],
+                          stream_of(g, a)));
+        if (cnt[b][a] > 0)
+          NCCL_G(ncclRecv(recv[a] + roff[a][b], (size_t)cnt[b][a], ncclFloat64, b, g->comms[a],
+                          stream_of(g, a)));
+      }
+    NCCL_G(ncclGroupEnd());
+  }
+  if (g->transport == XPORT_LOOPBACK) return lb_barrier(g);
+  return KNN_OK;
+}
+
 extern "C" {
 
 int knn_group_create(knn_group** out, int ndev, const int* devs, int mode) {
-  if (!out || ndev <= 0 || (mode != 0 && mode != 1))
+  const int base = mode & 0xff;
+  if (!out || ndev <= 0 || (base != 0 && base != 1) || (mode & ~(0xff | KNN_GROUP_RCCL)))
     return knn_fail(KNN_ERR_ARG, "bad group arguments");
+  if (ndev > knnk::kMaxParts) return knn_fail(KNN_ERR_ARG, "at most 64 ranks per group");
   *out = nullptr;
   knn_group* g = new knn_group();
   g->ndev = ndev;
-  g->mode = mode;
+  g->mode = base;
   for (int i = 0; i < ndev; i++) g->devs.push_back(devs ? devs[i] : i);
+  bool shared = false;
+  for (int i = 0; i < ndev; i++)
+    for (int j = 0; j < i; j++) shared |= g->devs[i] == g->devs[j];
+  const char* env = getenv("KNN_GROUP_RCCL");
+  const bool force = (mode & KNN_GROUP_RCCL) || (env && !strcmp(env, "1"));
+  g->transport = shared ? XPORT_LOOPBACK : (ndev > 1 || force) ? XPORT_RCCL : XPORT_NONE;
   g->ctx.assign(ndev, nullptr);
   for (int i = 0; i < ndev; i++) {
     int rc = knn_create(&g->ctx[i], g->devs[i]);
@@ -91,7 +249,7 @@ int knn_group_create(knn_group** out, int ndev, const int* devs, int mode) {
     }
   }
   g->comms.assign(ndev, nullptr);
-  if (ndev > 1) {
+  if (g->transport == XPORT_RCCL) {
     ncclResult_t r = ncclCommInitAll(g->comms.data(), ndev, g->devs.data());
     if (r != ncclSuccess) {
       g->comms.clear();
@@ -99,19 +257,42 @@ int knn_group_create(knn_group** out, int ndev, const int* devs, int mode) {
       return knn_fail(KNN_ERR_COMM, std::string("ncclCommInitAll failed: ") + ncclGetErrorString(r));
     }
   }
-  for (auto* v : {&g->X, &g->lab, &g->Q, &g->olab, &g->oidx, &g->odist, &g->oflags, &g->pk,
-                  &g->gk, &g->nX, &g->nmm})
+  for (auto* v : {&g->X, &g->lab, &g->labA, &g->Q, &g->olab, &g->oidx, &g->odist, &g->oflags,
+                  &g->pk, &g->gk, &g->tq, &g->tcnt, &g->tsel, &g->trow, &g->tsend, &g->trecv,
+                  &g->nX, &g->nmm})
     v->resize(ndev);
   g->ev0.assign(ndev, nullptr);
   g->ev1.assign(ndev, nullptr);
+  g->evx.assign(ndev, nullptr);
   for (int i = 0; i < ndev; i++) {
     if (hipSetDevice(g->devs[i]) != hipSuccess || hipEventCreate(&g->ev0[i]) != hipSuccess ||
-        hipEventCreate(&g->ev1[i]) != hipSuccess) {
+        hipEventCreate(&g->ev1[i]) != hipSuccess ||
+        hipEventCreateWithFlags(&g->evx[i], hipEventDisableTiming) != hipSuccess) {
       knn_group_destroy(g);
       return knn_fail(KNN_ERR_DEVICE, "hipEventCreate failed");
     }
   }
   *out = g;
+  return KNN_OK;
+}
+
+int knn_group_transport(knn_group* g) { return g ? g->transport : -1; }
+
+int knn_group_set_precision(knn_group* g, int mode) {
+  if (!g) return knn_fail(KNN_ERR_ARG, "null group");
+  for (auto* c : g->ctx) {
+    int rc = knn_set_precision(c, mode);
+    if (rc) return rc;
+  }
+  return KNN_OK;
+}
+
+int knn_group_set_tuning(knn_group* g, const char* key, int64_t value) {
+  if (!g) return knn_fail(KNN_ERR_ARG, "null group");
+  for (auto* c : g->ctx) {
+    int rc = knn_set_tuning(c, key, value);
+    if (rc) return rc;
+  }
   return KNN_OK;
 }
 
@@ -122,10 +303,11 @@ int knn_group_destroy(knn_group* g) {
       (void)hipSetDevice(g->devs[i]);
       (void)hipDeviceSynchronize();
     }
-    for (auto* v : {&g->X, &g->lab, &g->Q, &g->olab, &g->oidx, &g->odist, &g->oflags, &g->pk,
-                    &g->gk, &g->nX, &g->nmm})
+    for (auto* v : {&g->X, &g->lab, &g->labA, &g->Q, &g->olab, &g->oidx, &g->odist, &g->oflags,
+                    &g->pk, &g->gk, &g->tq, &g->tcnt, &g->tsel, &g->trow, &g->tsend, &g->trecv,
+                    &g->nX, &g->nmm})
       if (i < (int)v->size()) (*v)[i].release();
-    for (auto* ev : {&g->ev0, &g->ev1})
+    for (auto* ev : {&g->ev0, &g->ev1, &g->evx})
       if (i < (int)ev->size() && (*ev)[i]) (void)hipEventDestroy((*ev)[i]);
   }
   for (auto c : g->comms)
@@ -146,9 +328,10 @@ int knn_group_set_train(knn_group* g, const double* X, const int32_t* labels, in
   g->n = n;
   g->d = d;
   g->class_cnt = class_cnt;
+  g->trained = false;
   const int G = g->ndev;
   if (g->mode == 0) {
-    // root copy on the first GPU, then RCCL broadcast over xGMI (cpp:224-225)
+    // root copy on the first GPU, then a broadcast over xGMI (cpp:224-225)
     for (int i = 0; i < G; i++) {
       HIP_G(hipSetDevice(g->devs[i]));
       int rc;
@@ -160,34 +343,36 @@ int knn_group_set_train(knn_group* g, const double* X, const int32_t* labels, in
                          g->ctx[0]->stream));
     HIP_G(hipMemcpyAsync(g->lab[0].p, labels, (size_t)n * sizeof(int32_t),
                          hipMemcpyHostToDevice, g->ctx[0]->stream));
-    if (G > 1) {
-      NCCL_G(ncclGroupStart());
-      for (int i = 0; i < G; i++) {
-        NCCL_G(ncclBroadcast(g->X[0].p, g->X[i].p, (size_t)n * d, ncclFloat64, 0, g->comms[i],
-                             g->ctx[i]->stream));
-        NCCL_G(ncclBroadcast(g->lab[0].p, g->lab[i].p, (size_t)n, ncclInt32, 0, g->comms[i],
-                             g->ctx[i]->stream));
-      }
-      NCCL_G(ncclGroupEnd());
+    std::vector<void*> xb(G), lb(G);
+    for (int i = 0; i < G; i++) {
+      xb[i] = g->X[i].p;
+      lb[i] = g->lab[i].p;
     }
-    int rc = for_each_dev(g, [&](int i) {
+    int rc;
+    if ((rc = coll_bcast(g, xb, (size_t)n * d, ncclFloat64, 8, 0))) return rc;
+    if ((rc = coll_bcast(g, lb, (size_t)n, ncclInt32, 4, 0))) return rc;
+    rc = for_each_dev(g, [&](int i) {
       return knn_set_train_device(g->ctx[i], (const double*)g->X[i].p,
                                   (const int32_t*)g->lab[i].p, n, d, class_cnt, 0);
     });
     if (rc) return rc;
   } else {
-    // train-sharded: contiguous row shards, global index offsets
+    // train-sharded: contiguous row shards, global index offsets; every
+    // label on every device for the reference-order pass (4 B per row)
+    if (n < G) return knn_fail(KNN_ERR_ARG, "more ranks than train rows");
     int rc = for_each_dev(g, [&](int i) {
       const int64_t r0 = n * i / G, r1 = n * (i + 1) / G;
       const int64_t ni = r1 - r0;
-      if (ni <= 0) return knn_fail(KNN_ERR_ARG, "more GPUs than train rows");
       int e;
       if ((e = g->X[i].ensure((size_t)ni * d * sizeof(double)))) return e;
       if ((e = g->lab[i].ensure((size_t)ni * sizeof(int32_t)))) return e;
+      if ((e = g->labA[i].ensure((size_t)n * sizeof(int32_t)))) return e;
       hipStream_t s = g->ctx[i]->stream;
       if (hipMemcpyAsync(g->X[i].p, X + r0 * d, (size_t)ni * d * sizeof(double),
                          hipMemcpyHostToDevice, s) != hipSuccess ||
           hipMemcpyAsync(g->lab[i].p, labels + r0, (size_t)ni * sizeof(int32_t),
+                         hipMemcpyHostToDevice, s) != hipSuccess ||
+          hipMemcpyAsync(g->labA[i].p, labels, (size_t)n * sizeof(int32_t),
                          hipMemcpyHostToDevice, s) != hipSuccess)
         return knn_fail(KNN_ERR_DEVICE, "H2D of train shard failed");
       return knn_set_train_device(g->ctx[i], (const double*)g->X[i].p,
@@ -199,12 +384,126 @@ int knn_group_set_train(knn_group* g, const double* X, const int32_t* labels, in
   return KNN_OK;
 }
 
+}  // extern "C"
+
+// Train-sharded: the queries the merges flagged KNN_FLAG_TIE_PENDING (their
+// label depends on the reference's order among equal distances over the
+// whole train set) get the reference's order.  The host reads the owners'
+// queues (one small copy per device; the call waits for its devices at the
+// end anyway), then per batch: every shard computes the batch's exact
+// distances to its rows, an all-to-all moves each owner's blocks to it, and
+// the owner re-sorts and votes (knn_tie_resolve_device).
+static int resolve_ties(knn_group* g, int64_t m, int k, int metric) {
+  const int G = g->ndev;
+  const int64_t n = g->n;
+  g->last_ties = 0;
+  std::vector<int> hc(G, 0);
+  for (int i = 0; i < G; i++) {
+    HIP_G(hipSetDevice(g->devs[i]));
+    HIP_G(hipMemcpyAsync(&hc[i], g->tcnt[i].p, sizeof(int), hipMemcpyDeviceToHost,
+                         stream_of(g, i)));
+  }
+  int64_t total = 0;
+  for (int i = 0; i < G; i++) {
+    HIP_G(hipSetDevice(g->devs[i]));
+    HIP_G(hipStreamSynchronize(stream_of(g, i)));
+    total += hc[i];
+  }
+  if (total == 0) return KNN_OK;
+  std::vector<std::vector<int>> own(G);  // owner's queued output rows (slice-local)
+  for (int i = 0; i < G; i++) {
+    own[i].resize(hc[i]);
+    if (!hc[i]) continue;
+    HIP_G(hipSetDevice(g->devs[i]));
+    HIP_G(hipMemcpy(own[i].data(), g->tq[i].p, hc[i] * sizeof(int), hipMemcpyDeviceToHost));
+    std::sort(own[i].begin(), own[i].end());
+  }
+  std::vector<int64_t> rows(G), r0(G);
+  for (int i = 0; i < G; i++) {
+    r0[i] = n * i / G;
+    rows[i] = n * (i + 1) / G - r0[i];
+  }
+  // queries per batch: the owner receives up to B x n distances (<= 1 GB)
+  const int64_t B = std::max<int64_t>(1, std::min<int64_t>(4096, (1ll << 30) / (8 * n)));
+  std::vector<size_t> pos(G, 0);
+  int rc;
+  while (true) {
+    std::vector<int64_t> cnt(G, 0);
+    std::vector<int> sel;
+    std::vector<std::vector<int>> orow(G);
+    for (int r = 0; r < G && (int64_t)sel.size() < B; r++)
+      while (pos[r] < own[r].size() && (int64_t)sel.size() < B) {
+        const int qo = own[r][pos[r]++];
+        sel.push_back((int)(m * r / G) + qo);  // global query row
+        orow[r].push_back(qo);
+        cnt[r]++;
+      }
+    const int Bt = (int)sel.size();
+    if (Bt == 0) break;
+    for (int i = 0; i < G; i++) {
+      HIP_G(hipSetDevice(g->devs[i]));
+      if ((rc = g->tsel[i].ensure((size_t)B * sizeof(int)))) return rc;
+      if ((rc = g->trow[i].ensure((size_t)B * sizeof(int)))) return rc;
+      if ((rc = g->tsend[i].ensure((size_t)B * rows[i] * sizeof(double)))) return rc;
+      if ((rc = g->trecv[i].ensure((size_t)B * n * sizeof(double)))) return rc;
+      hipStream_t s = stream_of(g, i);
+      HIP_G(hipMemcpyAsync(g->tsel[i].p, sel.data(), Bt * sizeof(int), hipMemcpyHostToDevice, s));
+      if (cnt[i])
+        HIP_G(hipMemcpyAsync(g->trow[i].p, orow[i].data(), cnt[i] * sizeof(int),
+                             hipMemcpyHostToDevice, s));
+      if ((rc = knn_shard_distances_device(g->ctx[i], (const double*)g->Q[i].p,
+                                           (const int32_t*)g->tsel[i].p, Bt, metric,
+                                           (double*)g->tsend[i].p, s)))
+        return rc;
+    }
+    // shard a's block for owner b: [cnt_b][rows_a] at (sum of earlier owners'
+    // counts) x rows_a; it lands at cnt_b x r0_a on b (parts in row order)
+    std::vector<std::vector<int64_t>> c2(G, std::vector<int64_t>(G)), so(G, std::vector<int64_t>(G)),
+        ro(G, std::vector<int64_t>(G));
+    for (int a = 0; a < G; a++) {
+      int64_t before = 0;
+      for (int b = 0; b < G; b++) {
+        c2[a][b] = cnt[b] * rows[a];
+        so[a][b] = before * rows[a];
+        before += cnt[b];
+      }
+    }
+    for (int b = 0; b < G; b++)
+      for (int a = 0; a < G; a++) ro[b][a] = cnt[b] * r0[a];
+    std::vector<double*> sb(G), rb(G);
+    for (int i = 0; i < G; i++) {
+      sb[i] = (double*)g->tsend[i].p;
+      rb[i] = (double*)g->trecv[i].p;
+    }
+    if ((rc = coll_alltoallv(g, sb, rb, c2, so, ro))) return rc;
+    for (int b = 0; b < G; b++) {
+      if (!cnt[b]) continue;
+      HIP_G(hipSetDevice(g->devs[b]));
+      if ((rc = knn_tie_resolve_device(g->ctx[b], (const double*)g->trecv[b].p, G, rows.data(),
+                                       (int)cnt[b], (const int32_t*)g->labA[b].p,
+                                       (const int32_t*)g->trow[b].p, k, (int32_t*)g->olab[b].p,
+                                       (int64_t*)g->oidx[b].p, (double*)g->odist[b].p,
+                                       (int32_t*)g->oflags[b].p, stream_of(g, b))))
+        return rc;
+    }
+    for (int i = 0; i < G; i++) {  // the host lists of this batch are reused
+      HIP_G(hipSetDevice(g->devs[i]));
+      HIP_G(hipStreamSynchronize(stream_of(g, i)));
+    }
+    g->last_ties += Bt;
+  }
+  return KNN_OK;
+}
+
+extern "C" {
+
 int knn_group_classify(knn_group* g, const double* Q, int64_t m, int32_t k, int32_t metric,
                        int32_t* out_labels, int64_t* out_idx, double* out_dist,
                        int32_t* out_flags) {
   if (!g || !g->trained) return knn_fail(KNN_ERR_STATE, "group classify before set_train");
   if (m < 0 || !out_labels || (m > 0 && !Q)) return knn_fail(KNN_ERR_ARG, "bad classify arguments");
   if (k < 0 || k > g->n) return knn_fail(KNN_ERR_ARG, "bad k");
+  if (m >= (int64_t)INT32_MAX) return knn_fail(KNN_ERR_ARG, "m must be < 2^31 per call");
   if (m == 0) return KNN_OK;
   const int G = g->ndev;
   const int d = g->d;
@@ -284,6 +583,7 @@ int knn_group_classify(knn_group* g, const double* Q, int64_t m, int32_t k, int3
   }
 
   // ---- train-sharded
+  g->last_ties = 0;
   if (k == 0) {
     for (int64_t q = 0; q < m; q++) out_labels[q] = -1;
     if (out_flags)
@@ -294,6 +594,7 @@ int knn_group_classify(knn_group* g, const double* Q, int64_t m, int32_t k, int3
   // K <= N_train like cpp:328 (unions beyond 4096 entries: the rank merge)
   const int w = (int)std::min<int64_t>((int64_t)k + 1, g->n);
   const int64_t PB = knnk::packed_part_bytes(m, w);
+  const int ties = g->ctx[0]->tune_ties;
   for (int i = 0; i < G; i++) {
     int64_t q0, mi;
     slice(i, q0, mi);
@@ -301,15 +602,17 @@ int knn_group_classify(knn_group* g, const double* Q, int64_t m, int32_t k, int3
     if ((rc = g->Q[i].ensure((size_t)m * d * sizeof(double)))) return rc;
     // this GPU's lists packed [dist | idx | label] (one all-gather per step)
     if ((rc = g->pk[i].ensure((size_t)PB))) return rc;
-    if (G > 1 && (rc = g->gk[i].ensure((size_t)G * PB))) return rc;
+    if (g->transport != XPORT_NONE && (rc = g->gk[i].ensure((size_t)G * PB))) return rc;
     if ((rc = g->olab[i].ensure((size_t)std::max<int64_t>(mi, 1) * sizeof(int32_t)))) return rc;
     if ((rc = g->oflags[i].ensure((size_t)std::max<int64_t>(mi, 1) * sizeof(int32_t)))) return rc;
     if ((rc = g->oidx[i].ensure((size_t)std::max<int64_t>(mi, 1) * k * sizeof(int64_t)))) return rc;
     if ((rc = g->odist[i].ensure((size_t)std::max<int64_t>(mi, 1) * k * sizeof(double)))) return rc;
+    if ((rc = g->tq[i].ensure((size_t)std::max<int64_t>(mi, 1) * sizeof(int)))) return rc;
+    if ((rc = g->tcnt[i].ensure(sizeof(int)))) return rc;
     if (const int64_t sb = knnk::merge_scratch_bytes(G, w, k, mi))
       if ((rc = g->ctx[i]->mrg.ensure((size_t)sb))) return rc;
   }
-  // queries to the first GPU, RCCL broadcast to the rest
+  // queries to the first GPU, broadcast to the rest
   HIP_G(hipSetDevice(g->devs[0]));
   HIP_G(hipMemcpyAsync(g->Q[0].p, Q, (size_t)m * d * sizeof(double), hipMemcpyHostToDevice,
                        g->ctx[0]->stream));
@@ -317,40 +620,48 @@ int knn_group_classify(knn_group* g, const double* Q, int64_t m, int32_t k, int3
     HIP_G(hipSetDevice(g->devs[i]));
     HIP_G(hipEventRecord(g->ev0[i], g->ctx[i]->stream));
   }
-  if (G > 1) {
-    NCCL_G(ncclGroupStart());
-    for (int i = 0; i < G; i++)
-      NCCL_G(ncclBroadcast(g->Q[0].p, g->Q[i].p, (size_t)m * d, ncclFloat64, 0, g->comms[i],
-                           g->ctx[i]->stream));
-    NCCL_G(ncclGroupEnd());
-  }
+  std::vector<void*> qb(G), sp(G), rp(G);
   for (int i = 0; i < G; i++) {
+    qb[i] = g->Q[i].p;
+    sp[i] = g->pk[i].p;
+    rp[i] = g->gk[i].p;
+  }
+  if ((rc = coll_bcast(g, qb, (size_t)m * d, ncclFloat64, 8, 0))) return rc;
+  for (int i = 0; i < G; i++) {
+    HIP_G(hipSetDevice(g->devs[i]));
     unsigned char* pb = (unsigned char*)g->pk[i].p;
     if ((rc = knn_search_partial_device(g->ctx[i], (const double*)g->Q[i].p, m, w, metric,
                                         (double*)pb, (int64_t*)(pb + 8 * m * w),
                                         (int32_t*)(pb + 16 * m * w), nullptr)))
       return rc;
   }
-  if (G > 1) {  // one all-gather of the packed lists (≙ the reference's MPI_Gather, cpp:340)
-    NCCL_G(ncclGroupStart());
-    for (int i = 0; i < G; i++)
-      NCCL_G(ncclAllGather(g->pk[i].p, g->gk[i].p, (size_t)PB, ncclUint8, g->comms[i],
-                           g->ctx[i]->stream));
-    NCCL_G(ncclGroupEnd());
-  }
+  // one all-gather of the packed lists (≙ the reference's MPI_Gather, cpp:340)
+  if ((rc = coll_allgather(g, sp, rp, (size_t)PB))) return rc;
   for (int i = 0; i < G; i++) {
     int64_t q0, mi;
     slice(i, q0, mi);
     HIP_G(hipSetDevice(g->devs[i]));
     hipStream_t s = g->ctx[i]->stream;
     if (mi > 0) {
-      const double* sk = (const double*)(G > 1 ? g->gk[i].p : g->pk[i].p);
+      const double* sk = (const double*)(g->transport != XPORT_NONE ? g->gk[i].p : g->pk[i].p);
+      knnk::MergeTies mt;
+      mt.mode = ties;
+      mt.q = (int*)g->tq[i].p;
+      mt.cnt = (int*)g->tcnt[i].p;
+      HIP_G(hipMemsetAsync(mt.cnt, 0, sizeof(int), s));
       knnk::launch_merge_vote_partials(sk, nullptr, nullptr, G, m, w, k, (int32_t*)g->olab[i].p,
                                        (int64_t*)g->oidx[i].p, (double*)g->odist[i].p,
-                                       (int32_t*)g->oflags[i].p, s, q0, mi, PB, g->ctx[i]->mrg.p);
+                                       (int32_t*)g->oflags[i].p, s, q0, mi, PB, g->ctx[i]->mrg.p,
+                                       mt);
       HIP_G(hipGetLastError());
+    } else {
+      HIP_G(hipMemsetAsync(g->tcnt[i].p, 0, sizeof(int), s));
     }
-    HIP_G(hipEventRecord(g->ev1[i], s));
+  }
+  if (ties && (rc = resolve_ties(g, m, k, metric))) return rc;
+  for (int i = 0; i < G; i++) {
+    HIP_G(hipSetDevice(g->devs[i]));
+    HIP_G(hipEventRecord(g->ev1[i], g->ctx[i]->stream));
   }
   for (int i = 0; i < G; i++) {
     int64_t q0, mi;
@@ -362,6 +673,8 @@ int knn_group_classify(knn_group* g, const double* Q, int64_t m, int32_t k, int3
 }
 
 double knn_group_last_compute_seconds(knn_group* g) { return g ? g->last_compute : -1.0; }
+
+int64_t knn_group_last_tie_count(knn_group* g) { return g ? g->last_ties : -1; }
 
 int knn_group_normalize(knn_group* g, double* const* sets, const int64_t* rows, int32_t nsets,
                         int32_t d) {
@@ -401,16 +714,9 @@ int knn_group_normalize(knn_group* g, double* const* sets, const int64_t* rows, 
     return KNN_OK;
   });
   if (rc) return rc;
-  if (G > 1) {  // ≙ MPI_Allreduce MAX / MIN, cpp:276-277
-    NCCL_G(ncclGroupStart());
-    for (int i = 0; i < G; i++) {
-      double* mx = (double*)g->nmm[i].p;
-      NCCL_G(ncclAllReduce(mx, mx, d, ncclFloat64, ncclMax, g->comms[i], g->ctx[i]->stream));
-      NCCL_G(ncclAllReduce(mx + d, mx + d, d, ncclFloat64, ncclMin, g->comms[i],
-                           g->ctx[i]->stream));
-    }
-    NCCL_G(ncclGroupEnd());
-  }
+  std::vector<double*> mm(G);
+  for (int i = 0; i < G; i++) mm[i] = (double*)g->nmm[i].p;
+  if ((rc = coll_allreduce_maxmin(g, mm, d))) return rc;  // ≙ MPI_Allreduce, cpp:276-277
   return for_each_dev(g, [&](int i) {  // cpp:279-305 on each shard, back to the host
     knn_ctx* c = g->ctx[i];
     const double* mx = (const double*)g->nmm[i].p;

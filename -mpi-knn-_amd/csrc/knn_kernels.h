@@ -208,11 +208,41 @@ void launch_rescan(int metric, const TrainDev& t, const double* Q64, const Resca
 // each entry by binary searches and need merge_scratch_bytes() of device
 // scratch (0 when the LDS kernel serves the geometry).
 int64_t merge_scratch_bytes(int parts, int w, int k, int64_t mq);
+// Reference tie order in the merge: mode as Sink::tie_mode; a query whose
+// label can depend on the order among equal distances across shards gets
+// kFlagTiePending and, when q is set, its output row appended to q (count in
+// cnt[0]) for the train-sharded reference-order pass (launch_tie_resolve).
+constexpr int kFlagTiePending = 64;  // KNN_FLAG_TIE_PENDING
+struct MergeTies {
+  int mode = 0;
+  int* q = nullptr;
+  int* cnt = nullptr;
+};
 void launch_merge_vote_partials(const double* dist, const int64_t* idx, const int32_t* lab,
                                 int parts, int64_t m, int w, int k, int32_t* out_lab,
                                 int64_t* out_idx, double* out_dist, int32_t* out_flags,
                                 hipStream_t s, int64_t q0 = 0, int64_t mq = -1,
-                                int64_t pstride = 0, void* scratch = nullptr);
+                                int64_t pstride = 0, void* scratch = nullptr,
+                                const MergeTies& mt = MergeTies{});
+// Train-sharded reference tie order (knn_select.hip): out[i][j] = the exact
+// fp64 distance (reference operation order) of shard row j to query
+// Q64[qsel[i]] (qsel null: row i), [nsel][t.n].
+void launch_shard_dist(int metric, const TrainDev& t, const double* Q64, const int* qsel, int nsel,
+                       double* out, hipStream_t s);
+// Global row layout of the exchanged distance blocks: part p holds rows
+// [off[p], off[p+1]) (parts <= kMaxParts).
+constexpr int kMaxParts = 64;
+struct PartRows {
+  int parts;
+  int64_t off[kMaxParts + 1];
+};
+// D = parts blocks [nsel][rows_p] at offsets nsel * off[p]; lab_all the labels
+// of all off[parts] rows; outputs at sink rows orow[i] (labels, idx = global
+// row, dist, flags: TIE_PENDING -> TIE_REF).  Scratch per workgroup:
+// tie_scratch_bytes(off[parts], class_cnt); totals: running count (nullable).
+void launch_tie_resolve(const double* D, const PartRows& pr, int nsel, const int32_t* lab_all,
+                        const int* orow, int class_cnt, unsigned char* scratch, int64_t per_wg,
+                        int nwg, const Sink& sink, unsigned long long* totals, hipStream_t s);
 // byte stride of one part's packed [dist | idx | label] lists of m x w entries
 inline int64_t packed_part_bytes(int64_t m, int w) { return (m * w * 20 + 15) / 16 * 16; }
 // k beyond kMaxK (knn_select.hip, large_k_kernel): the exact path over every

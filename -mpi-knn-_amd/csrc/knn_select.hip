@@ -7,6 +7,38 @@
 namespace knnk {
 
 // ------------------------------------------------ finish: vote / outputs
+// Could the reference's order among EXACTLY equal distances (what its
+// std::sort over all rows leaves, cpp:323/366) give this query another
+// label than the (dist, idx) order?  mode 1: the runner-up count m2 (classes
+// other than the winner) and gin, the top-k entries of a tie across the k-th
+// place -- the order among equal distances only decides between classes
+// sharing the top count, and the membership of that tie group moves at most
+// gin entries from one class to another; mode 2: any tie in the top k.
+// lab(t) / dist(t): entry t of the (dist, idx)-sorted top k; M the winner's
+// count; tie the TIE_VOTE / TIE_ORDER bits; bnd: dist[k-1] == dist[k];
+// m2_known >= 0 supplies the runner-up count.  One wave, wave-uniform result.
+template <class LabAt, class DistAt>
+__device__ bool tie_order_matters(LabAt lab, DistAt dist, int k, int winner, int M, int tie,
+                                  bool bnd, int mode, int m2_known = -1) {
+  if (mode == 2) return bnd || tie != 0;
+  if (mode != 1 || !(bnd || (tie & 4))) return false;
+  const int lane = threadIdx.x & 63;
+  int m2 = 0, gin = 0;
+  const double dlast = dist(k - 1);
+  for (int t = lane; t < k; t += 64) {
+    const int lt = lab(t);
+    if (m2_known < 0 && lt != winner) {
+      int c = 0;
+      for (int s2 = 0; s2 < k; ++s2) c += (lab(s2) == lt);
+      m2 = max(m2, c);
+    }
+    gin += bnd && dist(t) == dlast;
+  }
+  m2 = m2_known >= 0 ? m2_known : wave_max_i(m2);
+  gin = wave_sum_i(gin);
+  return (bnd && M - m2 <= 2 * gin) || ((tie & 4) && m2 == M);
+}
+
 // Sorted exact neighbours (dk ascending, di local train index) are in LDS;
 // ls[t] already holds the label of entry t for t < needed.  One wave.
 //
@@ -32,29 +64,8 @@ __device__ void finish_single(int64_t q, const double* dk, const int* di, const 
     if (dk[t] == dk[t + 1]) tie |= ls[t] != ls[t + 1] ? 4 : 8;  // TIE_VOTE / TIE_ORDER
   tie = wave_or_i(tie);
   const bool bnd = k > 0 && k < cnt && dk[k - 1] == dk[k];  // KNN_FLAG_TIE_BOUNDARY
-  bool queue = false;
-  if (sink.tie_mode == 1 && (bnd || (tie & 4))) {
-    // could the reference's tie order give another label?  The runner-up
-    // count m2 (classes other than the winner) and gin, the top-k entries in
-    // a tie across the k-th place: the order among equal distances only
-    // decides between classes sharing the top count, and the membership of
-    // that tie group moves at most gin entries from one class to another
-    int m2 = 0, gin = 0;
-    for (int t = lane; t < k; t += 64) {
-      const int lt = ls[t];
-      if (lt != winner) {
-        int c = 0;
-        for (int s2 = 0; s2 < k; ++s2) c += (ls[s2] == lt);
-        m2 = max(m2, c);
-      }
-      gin += bnd && dk[t] == dk[k - 1];
-    }
-    m2 = wave_max_i(m2);
-    gin = wave_sum_i(gin);
-    queue = (bnd && M - m2 <= 2 * gin) || ((tie & 4) && m2 == M);
-  } else if (sink.tie_mode == 2) {
-    queue = bnd || tie;
-  }
+  const bool queue = tie_order_matters([&](int t) { return ls[t]; }, [&](int t) { return dk[t]; },
+                                       k, winner, M, tie, bnd, sink.tie_mode);
   if (lane == 0) {
     sink.labels[q] = winner;
     const int f = flag0 | tie | (bnd ? 2 : 0);
@@ -1268,14 +1279,16 @@ __device__ void ref_sort_prefix(double* D, int* P, int* Lb, int* Rb, int n, int 
   __syncthreads();
 }
 
-// Every row's exact distance to qrow (reference operation order, as
-// rescan_full) into D[0..n): per-wave staged 64-B row pieces.  All threads.
+// Exact distances of rows [r_begin, r_end) to qrow (reference operation
+// order, as rescan_full) into D[j] (absolute row index j): per-wave staged
+// 64-B row pieces.  All threads.
 template <int METRIC>
-__device__ void exact_all_dist(const TrainDev& t, const double* qrow, double* D, double* tb) {
+__device__ void exact_rows_dist(const TrainDev& t, const double* qrow, int64_t r_begin,
+                                int64_t r_end, double* D, double* tb) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nt = blockDim.x;
   const int d = t.d;
-  const int64_t n = t.n;
-  for (int64_t s0 = 0; s0 < n; s0 += nt) {
+  const int64_t n = r_end;
+  for (int64_t s0 = r_begin; s0 < n; s0 += nt) {
     const int64_t r0 = s0 + wv * 64;
     const int nr = (int)max((int64_t)0, min((int64_t)64, n - r0));
     double r = 0.0;
@@ -1304,26 +1317,33 @@ __device__ void exact_all_dist(const TrainDev& t, const double* qrow, double* D,
   }
 }
 
+template <int METRIC>
+__device__ void exact_all_dist(const TrainDev& t, const double* qrow, double* D, double* tb) {
+  exact_rows_dist<METRIC>(t, qrow, 0, t.n, D, tb);
+}
+
 // Outputs of a query whose first k records are in reference order: the
-// vote exactly as cpp:324-337 (sequential, per-class counts in `cnt`),
-// idx / dist, flags |= KNN_FLAG_TIE_REF.  All threads.
-__device__ void ref_finish(int64_t q, const double* D, const int* P, int k, const TrainDev& t,
-                           int class_cnt, int* cnt, const Sink& sink) {
+// vote exactly as cpp:324-337 (sequential, per-class counts in `cnt`; lab
+// indexed by the records' row numbers P), idx = P + idx_base, dist, flags
+// |= KNN_FLAG_TIE_REF (and KNN_FLAG_TIE_PENDING cleared).  All threads.
+__device__ void ref_finish(int64_t q, const double* D, const int* P, int k, const int32_t* lab,
+                           int64_t idx_base, int class_cnt, int* cnt, const Sink& sink) {
   const int tid = threadIdx.x;
   for (int c = tid; c < class_cnt; c += blockDim.x) cnt[c] = 0;
   __syncthreads();
   if (tid == 0) {
-    int best = 0, lab = -1;
+    int best = 0, winner = -1;
     for (int i = 0; i < k; ++i) {
-      const int lb = t.lab[P[i]];
+      const int lb = lab[P[i]];
+      if ((unsigned)lb >= (unsigned)class_cnt) continue;  // (labels are range-checked at set_train)
       const int c = ++cnt[lb];
-      if (c > best) { best = c; lab = lb; }
+      if (c > best) { best = c; winner = lb; }
     }
-    sink.labels[q] = lab;
-    if (sink.flags) sink.flags[q] |= kFlagTieRef;
+    sink.labels[q] = winner;
+    if (sink.flags) sink.flags[q] = (sink.flags[q] & ~kFlagTiePending) | kFlagTieRef;
   }
   for (int i = tid; i < k; i += blockDim.x) {
-    if (sink.idx) sink.idx[q * k + i] = (int64_t)P[i] + sink.idx_off;
+    if (sink.idx) sink.idx[q * k + i] = (int64_t)P[i] + idx_base;
     if (sink.dist) sink.dist[q * k + i] = D[i];
   }
   __syncthreads();
@@ -1357,8 +1377,87 @@ tie_order_kernel(TrainDev t, const double* __restrict__ Q64, const int* __restri
     for (int64_t j = threadIdx.x; j < n; j += kTieThreads) P[j] = (int)j;
     __syncthreads();
     ref_sort_prefix(D, P, Lb, Rb, (int)n, sink.k, s);
-    ref_finish(q, D, P, sink.k, t, class_cnt, cnt, sink);
+    ref_finish(q, D, P, sink.k, t.lab, sink.idx_off, class_cnt, cnt, sink);
   }
+}
+
+// ---- the same for the train-sharded mode (north_star mode b).  The
+// reference's std::sort runs over all N_train records of the WHOLE train set
+// in global row order (cpp:360-366), so its order among equal distances
+// depends on every shard's distances.  After the k-way merge flags a query
+// KNN_FLAG_TIE_PENDING, every shard computes that query's exact distances to
+// all of its rows (shard_dist_kernel), the blocks travel to the query's owner
+// (an all-to-all: RCCL send/recv in knn_group, torch.distributed in
+// knn_dist.py), which assembles them in global row order and runs the same
+// introsort emulation and vote (tie_resolve_kernel).
+
+// out[i][j] = exact distance of shard row j to query qsel[i] (qsel null: i).
+// Grid (ceil(n / kTieThreads), nsel): one 1024-row chunk of one query.
+template <int METRIC>
+__global__ void __launch_bounds__(kTieThreads)
+shard_dist_kernel(TrainDev t, const double* __restrict__ Q64, const int* __restrict__ qsel,
+                  double* __restrict__ out) {
+  __shared__ double tiles[kTieThreads / 64][64 * (kFullDC + 1)];
+  const int64_t i = blockIdx.y;
+  const int64_t q = qsel ? qsel[i] : i;
+  const int64_t r0 = (int64_t)blockIdx.x * kTieThreads;
+  exact_rows_dist<METRIC>(t, Q64 + q * t.d, r0, min(t.n, r0 + kTieThreads), out + i * t.n,
+                          tiles[threadIdx.x >> 6]);
+}
+
+void launch_shard_dist(int metric, const TrainDev& t, const double* Q64, const int* qsel, int nsel,
+                       double* out, hipStream_t s) {
+  const unsigned nx = (unsigned)((t.n + kTieThreads - 1) / kTieThreads);
+  for (int i0 = 0; i0 < nsel; i0 += 65535) {  // grid y limit
+    const int ny = min(65535, nsel - i0);
+    const int* qs = qsel ? qsel + i0 : nullptr;
+    double* o = out + (int64_t)i0 * t.n;
+    const double* Qb = qsel ? Q64 : Q64 + (int64_t)i0 * t.d;
+    if (metric == 0)
+      hipLaunchKernelGGL(shard_dist_kernel<0>, dim3(nx, ny), dim3(kTieThreads), 0, s, t, Qb, qs, o);
+    else
+      hipLaunchKernelGGL(shard_dist_kernel<1>, dim3(nx, ny), dim3(kTieThreads), 0, s, t, Qb, qs, o);
+  }
+}
+
+// D: the nsel queries' distances to every row as parts blocks, block p =
+// [nsel][rows_p] at offset nsel * off[p] (global rows off[p] .. off[p+1]).
+// Output row orow[i] of the sink (labels / idx / dist / flags).
+__global__ void __launch_bounds__(kTieThreads)
+tie_resolve_kernel(const double* __restrict__ Din, PartRows pr, int nsel,
+                   const int32_t* __restrict__ lab_all, const int* __restrict__ orow, int class_cnt,
+                   unsigned char* __restrict__ scratch, int64_t per_wg, Sink sink,
+                   unsigned long long* totals) {
+  __shared__ RefSortShared s;
+  const int64_t n = pr.off[pr.parts];
+  if (blockIdx.x == 0 && threadIdx.x == 0 && totals) atomicAdd(totals, (unsigned long long)nsel);
+  unsigned char* base = scratch + (int64_t)blockIdx.x * per_wg;
+  double* D = (double*)base;
+  int* P = (int*)(D + n);
+  int* Lb = P + n;
+  int* Rb = Lb + n;
+  int* cnt = Rb + n;
+  for (int i = blockIdx.x; i < nsel; i += gridDim.x) {
+    for (int p = 0; p < pr.parts; ++p) {  // global row order = the reference's fill order
+      const int64_t o = pr.off[p], rows = pr.off[p + 1] - o;
+      const double* src = Din + (int64_t)nsel * o + (int64_t)i * rows;
+      for (int64_t j = threadIdx.x; j < rows; j += kTieThreads) {
+        D[o + j] = src[j];
+        P[o + j] = (int)(o + j);
+      }
+    }
+    __syncthreads();
+    ref_sort_prefix(D, P, Lb, Rb, (int)n, sink.k, s);
+    ref_finish(orow[i], D, P, sink.k, lab_all, 0, class_cnt, cnt, sink);
+  }
+}
+
+void launch_tie_resolve(const double* D, const PartRows& pr, int nsel, const int32_t* lab_all,
+                        const int* orow, int class_cnt, unsigned char* scratch, int64_t per_wg,
+                        int nwg, const Sink& sink, unsigned long long* totals, hipStream_t s) {
+  if (nwg <= 0 || nsel <= 0) return;
+  hipLaunchKernelGGL(tie_resolve_kernel, dim3(nwg), dim3(kTieThreads), 0, s, D, pr, nsel, lab_all,
+                     orow, class_cnt, scratch, per_wg, sink, totals);
 }
 
 void launch_tie_order(int metric, const TrainDev& t, const double* Q64, const int* tie_q,
@@ -1637,6 +1736,10 @@ merge_vote_partials_kernel(const double* __restrict__ dist, const int64_t* __res
   int cnt = 0;
   for (int e = lane; e < P2; e += 64) cnt += (gi[e] != LLONG_MAX);
   cnt = wave_sum_i(cnt);
+  if (cnt == 0 && k > 0) {  // no shard listed a neighbour: a non-finite query
+    finish_nonfinite(qo, sink);
+    return;
+  }
   int bc = 0, bt = INT_MAX;
   for (int t = lane; t < k; t += 64) {
     const int lt = ls[t];
@@ -1646,21 +1749,27 @@ merge_vote_partials_kernel(const double* __restrict__ dist, const int64_t* __res
   }
   const int M = wave_max_i(bc);
   const int tmin = wave_min_i(bc == M ? bt : INT_MAX);
+  const int winner = k > 0 ? ls[tmin] : -1;
+  const int kk = min(k, cnt);  // slots [kk, k) are empty (fewer rows than k)
   int tie = 0;
-  for (int t = lane; t + 1 < k; t += 64)
+  for (int t = lane; t + 1 < kk; t += 64)
     if (dk[t] == dk[t + 1]) tie |= ls[t] != ls[t + 1] ? 4 : 8;
   tie = wave_or_i(tie);
+  const bool bnd = k > 0 && k < cnt && dk[k - 1] == dk[k];
+  // the order among equal distances across shards is the reference's
+  // std::sort's over the whole train set: flagged for the exchange of
+  // knn_group / knn_dist.py and tie_resolve_kernel
+  const bool pend = kk == k &&
+                    tie_order_matters([&](int t) { return ls[t]; }, [&](int t) { return dk[t]; },
+                                      k, winner, M, tie, bnd, sink.tie_mode);
   if (lane == 0) {
-    sink.labels[qo] = k > 0 ? ls[tmin] : -1;
-    if (sink.flags) {
-      int f = tie;
-      if (k > 0 && k < cnt && dk[k - 1] == dk[k]) f |= 2;
-      sink.flags[qo] = f;
-    }
+    sink.labels[qo] = winner;
+    if (sink.flags) sink.flags[qo] = tie | (bnd ? 2 : 0) | (pend ? kFlagTiePending : 0);
+    if (pend && sink.tie_q) sink.tie_q[atomicAdd(sink.tie_cnt, 1)] = (int)qo;
   }
   for (int t = lane; t < k; t += 64) {
-    if (sink.idx) sink.idx[qo * k + t] = gi[t];
-    if (sink.dist) sink.dist[qo * k + t] = dk[t];
+    if (sink.idx) sink.idx[qo * k + t] = t < kk ? gi[t] : -1;
+    if (sink.dist) sink.dist[qo * k + t] = t < kk ? dk[t] : KNN_INF_D;
   }
 }
 
@@ -1764,6 +1873,10 @@ merge_rank_vote_kernel(PartLists L, int parts, int k, int64_t q0,
     cnt += lo;
   }
   for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+  if (cnt == 0 && k > 0) {  // no shard listed a neighbour: a non-finite query
+    finish_nonfinite(qo, sink);
+    return;
+  }
   const int kk = (int)min<int64_t>(k, cnt);  // slots [kk, k) are empty: label -1
   const unsigned char* row = scratch + qo * merge_row_bytes(k);
   const double* rd = (const double*)row;
@@ -1773,7 +1886,7 @@ merge_rank_vote_kernel(PartLists L, int parts, int k, int64_t q0,
   int maxlab = -1;
   for (int t = lane; t < kk; t += 64) maxlab = max(maxlab, rl[t]);
   maxlab = wave_max_i(maxlab);
-  int winner = -1;
+  int winner = -1, M = 0, m2 = -1;
   if (maxlab + 2 <= kVoteLdsClasses) {
     // cpp:324-337 as written: counts per class (slot 0: the empty label -1),
     // the first label whose count strictly exceeds the running max wins
@@ -1786,7 +1899,15 @@ merge_rank_vote_kernel(PartLists L, int parts, int k, int64_t q0,
         const int c = ++counts[lb + 1];
         if (c > best) { best = c; winner = lb; }
       }
+      M = best;
     }
+    __syncthreads();
+    winner = __shfl(winner, 0, 64);
+    M = __shfl(M, 0, 64);
+    int r2 = 0;  // the runner-up count, for the tie rule
+    for (int c = lane; c < maxlab + 2; c += 64)
+      if (c != winner + 1) r2 = max(r2, counts[c]);
+    m2 = wave_max_i(r2);
   } else {
     // (labels beyond the LDS table) the same rule in parallel: the winner is
     // the label of the first slot whose running count reaches the final max
@@ -1797,7 +1918,7 @@ merge_rank_vote_kernel(PartLists L, int parts, int k, int64_t q0,
       for (int s2 = 0; s2 <= t; ++s2) c += (slot_lab(s2) == lt);
       if (c > bc) { bc = c; bt = t; }
     }
-    const int M = wave_max_i(bc);
+    M = wave_max_i(bc);
     const int tmin = wave_min_i(bc == M ? bt : INT_MAX);
     winner = k > 0 ? slot_lab(tmin) : -1;
   }
@@ -1805,13 +1926,13 @@ merge_rank_vote_kernel(PartLists L, int parts, int k, int64_t q0,
   for (int t = lane; t + 1 < kk; t += 64)
     if (rd[t] == rd[t + 1]) tie |= rl[t] != rl[t + 1] ? 4 : 8;
   tie = wave_or_i(tie);
+  const bool bnd = k > 0 && k < cnt && rd[k - 1] == rd[k];
+  const bool pend = kk == k && tie_order_matters(slot_lab, [&](int t) { return rd[t]; }, k, winner,
+                                                 M, tie, bnd, sink.tie_mode, m2);
   if (lane == 0) {
     sink.labels[qo] = winner;
-    if (sink.flags) {
-      int f = tie;
-      if (k > 0 && k < cnt && rd[k - 1] == rd[k]) f |= 2;
-      sink.flags[qo] = f;
-    }
+    if (sink.flags) sink.flags[qo] = tie | (bnd ? 2 : 0) | (pend ? kFlagTiePending : 0);
+    if (pend && sink.tie_q) sink.tie_q[atomicAdd(sink.tie_cnt, 1)] = (int)qo;
   }
   for (int t = lane; t < k; t += 64) {
     if (sink.idx) sink.idx[qo * k + t] = t < kk ? ri[t] : -1;
@@ -1828,7 +1949,7 @@ void launch_merge_vote_partials(const double* dist, const int64_t* idx, const in
                                 int parts, int64_t m, int w, int k, int32_t* out_lab,
                                 int64_t* out_idx, double* out_dist, int32_t* out_flags,
                                 hipStream_t s, int64_t q0, int64_t mq, int64_t pstride,
-                                void* scratch) {
+                                void* scratch, const MergeTies& mt) {
   if (mq < 0) mq = m - q0;
   if (mq <= 0) return;
   Sink sink{};
@@ -1838,6 +1959,9 @@ void launch_merge_vote_partials(const double* dist, const int64_t* idx, const in
   sink.idx = out_idx;
   sink.dist = out_dist;
   sink.flags = out_flags;
+  sink.tie_mode = mt.mode;
+  sink.tie_q = mt.q;
+  sink.tie_cnt = mt.cnt;
   if ((int64_t)parts * w > kMergeLdsEntries) {
     const PartLists L{dist, idx, lab, m, pstride, w};
     const int nch = (parts * w + kMergeRankThreads - 1) / kMergeRankThreads;

@@ -27,7 +27,7 @@ DRIVER_PATH = os.path.join(HERE, "bin", "knn_mpi_amd")
 
 L2, L1 = 0, 1
 FLAG_EXACT_RESCAN, FLAG_TIE_BOUNDARY, FLAG_TIE_VOTE, FLAG_TIE_ORDER = 1, 2, 4, 8
-FLAG_NONFINITE, FLAG_TIE_REF = 16, 32
+FLAG_NONFINITE, FLAG_TIE_REF, FLAG_TIE_PENDING = 16, 32, 64
 EXPORTED = (
     "knn_version", "knn_last_error", "knn_device_count", "knn_create", "knn_destroy",
     "knn_set_train", "knn_set_train_device", "knn_classify", "knn_classify_device",
@@ -37,7 +37,11 @@ EXPORTED = (
     "knn_last_geometry", "knn_set_precision", "knn_last_candidate_path", "knn_set_tuning",
     "knn_minmax_device", "knn_normalize_device", "knn_normalize", "knn_group_normalize",
     "knn_timing_totals", "knn_rescan_totals", "knn_last_kernel_name", "knn_tie_totals",
+    "knn_shard_distances_device", "knn_tie_resolve_device", "knn_group_transport",
+    "knn_group_last_tie_count", "knn_group_set_precision", "knn_group_set_tuning",
 )
+GROUP_RCCL = 0x100  # knn_group_create mode flag: RCCL collectives also at one GPU
+TRANSPORT_NONE, TRANSPORT_RCCL, TRANSPORT_LOOPBACK = 0, 1, 2
 PRECISION_AUTO, PRECISION_FP32, PRECISION_BF16X3, PRECISION_FP16 = 0, 1, 2, 3
 PHASE_PREP, PHASE_CANDIDATE, PHASE_RERANK, PHASE_RESCAN = 0, 1, 2, 3
 
@@ -122,6 +126,13 @@ def lib():
         "knn_rescan_totals": ([P, ctypes.POINTER(i64), ctypes.c_int], ctypes.c_int),
         "knn_last_kernel_name": ([P], ctypes.c_char_p),
         "knn_tie_totals": ([P, ctypes.POINTER(i64), ctypes.c_int], ctypes.c_int),
+        "knn_shard_distances_device": ([P, P, P, i32, i32, P, P], ctypes.c_int),
+        "knn_tie_resolve_device": ([P, P, i32, ctypes.POINTER(i64), i32, P, P, i32, P, P, P, P,
+                                    P], ctypes.c_int),
+        "knn_group_transport": ([P], ctypes.c_int),
+        "knn_group_last_tie_count": ([P], i64),
+        "knn_group_set_precision": ([P, ctypes.c_int], ctypes.c_int),
+        "knn_group_set_tuning": ([P, ctypes.c_char_p, i64], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -232,6 +243,22 @@ class Classifier:
                                            int(k), int(q0), int(mq), d_labels, d_out_idx,
                                            d_out_dist, d_flags, stream))
 
+    def shard_distances_device(self, dQ_ptr, d_qsel, nsel, metric, d_out, stream=None):
+        """Exact fp64 distances of this context's shard rows to nsel queries
+        (dQ rows d_qsel[i], or i when d_qsel is None): d_out [nsel][n_shard]."""
+        _check(lib().knn_shard_distances_device(self._h, dQ_ptr, d_qsel, int(nsel), int(metric),
+                                                d_out, stream))
+
+    def tie_resolve_device(self, d_D, rows, nsel, d_lab_all, d_orow, k, d_labels, d_idx=None,
+                           d_dist=None, d_flags=None, stream=None):
+        """Reference order (std::sort over the whole train set) for nsel
+        queries whose distances to every row are in d_D as len(rows) blocks
+        [nsel][rows[p]] in global row order; rewrites output rows d_orow."""
+        arr = (ctypes.c_int64 * len(rows))(*[int(r) for r in rows])
+        _check(lib().knn_tie_resolve_device(self._h, d_D, len(rows), arr, int(nsel), d_lab_all,
+                                            d_orow, int(k), d_labels, d_idx, d_dist, d_flags,
+                                            stream))
+
     def sync(self):
         _check(lib().knn_sync(self._h))
 
@@ -309,12 +336,27 @@ class Classifier:
 
 class Group:
     """Single-process multi-GPU classifier over RCCL (mode 0 query-sharded,
-    1 train-sharded); see include/knn_amd.h."""
+    1 train-sharded); see include/knn_amd.h.  rccl=True runs every
+    collective through RCCL even on one GPU; repeated devices (e.g. [0, 0])
+    run several ranks on one GPU over loopback copies."""
 
-    def __init__(self, devices, mode=0):
+    def __init__(self, devices, mode=0, rccl=False):
         self._h = ctypes.c_void_p()
         arr = (ctypes.c_int * len(devices))(*devices)
-        _check(lib().knn_group_create(ctypes.byref(self._h), len(devices), arr, int(mode)))
+        flags = GROUP_RCCL if rccl else 0
+        _check(lib().knn_group_create(ctypes.byref(self._h), len(devices), arr, int(mode) | flags))
+
+    def transport(self):
+        return int(lib().knn_group_transport(self._h))
+
+    def set_precision(self, mode):
+        _check(lib().knn_group_set_precision(self._h, int(mode)))
+
+    def set_tuning(self, key, value):
+        _check(lib().knn_group_set_tuning(self._h, key.encode(), int(value)))
+
+    def last_tie_count(self):
+        return int(lib().knn_group_last_tie_count(self._h))
 
     def close(self):
         if self._h:

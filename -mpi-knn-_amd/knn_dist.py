@@ -123,11 +123,13 @@ def normalize_sharded(local_sets, minmax, apply, d, device=None):
     return mx, mn
 
 
-def train_sharded(search_partial, merge_vote, Q, m, w, k, device=None):
+def train_sharded(search_partial, merge_vote, Q, m, w, k, device=None, ties=None):
     """Mode b.  search_partial(Q) -> (dist f64[m,w], idx i64[m,w], lab i32[m,w])
     for this rank's train shard (global indices); merge_vote(d, i, l, parts,
     q0, q1) -> labels i32[q1-q0] for the query slice of the [parts][m][w]
-    lists.  Returns this rank's label slice and its [q0, q1)."""
+    lists.  ties (optional, see resolve_ties) restores the reference's order
+    among equal distances across shards for the queries the merge flagged.
+    Returns this rank's label slice and its [q0, q1)."""
     world, rank = world_info()
     d, i, l = search_partial(Q)
     if world > 1:  # one all-gather of the packed partial lists -> [W][m][w] each
@@ -135,4 +137,64 @@ def train_sharded(search_partial, merge_vote, Q, m, w, k, device=None):
     else:
         gd, gi, gl = d[None], i[None], l[None]
     q0, q1 = shard_range(m, world, rank)
-    return merge_vote(gd, gi, gl, world, q0, q1), (q0, q1)
+    out = merge_vote(gd, gi, gl, world, q0, q1)
+    if ties is not None:
+        resolve_ties(ties, m, device)
+    return out, (q0, q1)
+
+
+def resolve_ties(ties, m, device=None, budget_bytes=1 << 30):
+    """The reference sorts all N_train records of a query with std::sort
+    (cpp:366): among EXACTLY equal distances its order depends on every
+    row, so a merged query whose label that order decides (the merge's
+    KNN_FLAG_TIE_PENDING) needs every shard's exact distances.  `ties`:
+      pending()           -> int64[T_r] this rank's flagged rows of its slice
+      shard_distances(s)  -> f64[len(s), n_rank] exact distances of this
+                             rank's rows to the global query rows s (int32)
+      resolve(D, rows, o) -> rewrite slice rows o (int32) from D = the
+                             blocks [T][rows[g]] of every rank in row order
+      n_total             -> train rows over all ranks
+    Per batch: all-gather of the flagged ids, each rank's distances, one
+    all-to-all (≙ the owner receiving every shard's block), resolve on the
+    owner.  Returns the number of queries resolved over all ranks."""
+    world, rank = world_info()
+    n = ties.n_total
+    rows = [shard_range(n, world, r)[1] - shard_range(n, world, r)[0] for r in range(world)]
+    pend = ties.pending().to(torch.int64)
+    q0 = shard_range(m, world, rank)[0]
+    cnt = torch.tensor([pend.numel()], dtype=torch.int64, device=device)
+    if world > 1:
+        counts = [int(c.item()) for c in _all_gather_stack(cnt)]
+    else:
+        counts = [int(cnt.item())]
+    total = sum(counts)
+    if total == 0:
+        return 0
+    pad = torch.full((max(counts),), -1, dtype=torch.int64, device=device)
+    pad[:pend.numel()] = pend + q0
+    ids = _all_gather_stack(pad) if world > 1 else pad[None]
+    owned = [ids[r, :counts[r]] for r in range(world)]  # global query rows, owner order
+    B = max(1, min(4096, budget_bytes // (8 * n)))
+    pos = [0] * world
+    while True:
+        take, left = [], B
+        for r in range(world):
+            t = min(left, counts[r] - pos[r])
+            take.append(t)
+            left -= t
+        if sum(take) == 0:
+            break
+        sel = torch.cat([owned[r][pos[r]:pos[r] + take[r]] for r in range(world)]).to(torch.int32)
+        mine = owned[rank][pos[rank]:pos[rank] + take[rank]]
+        for r in range(world):
+            pos[r] += take[r]
+        D = ties.shard_distances(sel).reshape(-1)
+        if world > 1:
+            recv = torch.empty(take[rank] * n, dtype=torch.float64, device=device)
+            dist.all_to_all_single(recv, D, [take[rank] * rows[g] for g in range(world)],
+                                   [take[r] * rows[rank] for r in range(world)])
+        else:
+            recv = D
+        if take[rank]:
+            ties.resolve(recv, rows, (mine - q0).to(torch.int32))
+    return total

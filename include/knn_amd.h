@@ -81,6 +81,11 @@ extern "C" {
                                    orders it (libstdc++ introsort emulated over all
                                    n distances): label, indices and their order are
                                    the reference's (knn_set_tuning "ties") */
+#define KNN_FLAG_TIE_PENDING 64 /* knn_merge_vote_device: the label can depend on the
+                                   reference's order among equal distances ACROSS
+                                   shards; knn_shard_distances_device +
+                                   knn_tie_resolve_device give the reference's order
+                                   (knn_group mode 1 does this itself) */
 
 typedef struct knn_ctx knn_ctx;
 typedef struct knn_group knn_group;
@@ -141,11 +146,38 @@ int knn_search_partial_device(knn_ctx* ctx, const double* dQ, int64_t m, int32_t
  * (the layout an all-gather of knn_search_partial outputs produces), then
  * the reference vote over the first k of the merged order, for queries
  * [q0, q0+mq) (a rank's slice; q0=0, mq=m for all).  Outputs are indexed
- * from 0 (row q-q0).  Device pointers; d_out_idx/d_out_dist/d_flags nullable. */
+ * from 0 (row q-q0).  Device pointers; d_out_idx/d_out_dist/d_flags nullable.
+ * Within exact distance ties the merged order is (dist, global idx); a query
+ * whose label that order could decide (tuning "ties" of ctx: 1 vote-affecting
+ * ties, 2 every tie, 0 none) gets KNN_FLAG_TIE_PENDING in d_flags.  A query
+ * no shard listed a neighbour for (non-finite) gets label -1,
+ * KNN_FLAG_NONFINITE, idx -1, dist NaN; with fewer than k rows in all, the
+ * empty slots are idx -1, dist +inf. */
 int knn_merge_vote_device(knn_ctx* ctx, const double* d_dist, const int64_t* d_idx,
                           const int32_t* d_lab, int32_t parts, int64_t m, int32_t w, int32_t k,
                           int64_t q0, int64_t mq, int32_t* d_labels, int64_t* d_out_idx,
                           double* d_out_dist, int32_t* d_flags, void* stream);
+
+/* ---- train-sharded reference tie order (cpp:323/366 over the WHOLE train
+ * set, whose std::sort order among equal distances depends on every row).
+ * For the KNN_FLAG_TIE_PENDING queries of all ranks (rare):
+ * 1. every shard: knn_shard_distances_device -- d_out[i][j] = the exact fp64
+ *    distance (cpp:33-67 operation order) of shard row j to query
+ *    dQ[d_qsel[i]] (d_qsel NULL: query i), [nsel][n_shard];
+ * 2. an all-to-all moves each owner's [nsel_r][n_shard] block to it;
+ * 3. the owner: knn_tie_resolve_device over d_D = parts blocks in global row
+ *    order, block p = [nsel][rows[p]] at offset nsel * (rows[0] + ... +
+ *    rows[p-1]) (what the all-to-all delivers), d_lab_all = the labels of all
+ *    rows (global order); runs libstdc++'s introsort as the reference does
+ *    and the vote, and rewrites output row d_orow[i] of d_labels / d_idx /
+ *    d_dist (k per row) / d_flags (TIE_PENDING -> TIE_REF).  parts <= 64,
+ *    sum(rows) < 2^31.  Scratch: ~20 B per row per concurrent query. */
+int knn_shard_distances_device(knn_ctx* ctx, const double* dQ, const int32_t* d_qsel,
+                               int32_t nsel, int32_t metric, double* d_out, void* stream);
+int knn_tie_resolve_device(knn_ctx* ctx, const double* d_D, int32_t parts, const int64_t* rows,
+                           int32_t nsel, const int32_t* d_lab_all, const int32_t* d_orow,
+                           int32_t k, int32_t* d_labels, int64_t* d_idx, double* d_dist,
+                           int32_t* d_flags, void* stream);
 
 /* ---- min-max normalisation (replaces cpp:229-306, bit-exact in fp64) -----
  * Transductive, like the reference: per-dimension max/min over the train
@@ -256,8 +288,23 @@ int knn_tie_totals(knn_ctx* ctx, int64_t* out, int reset);
  *          cpp:340/383).
  * mode 1 = train-sharded: every GPU holds n/G rows; each computes the exact
  *          local top-(k+1) for all queries; ncclAllGather exchanges the lists;
- *          each GPU k-way merges and votes its slice of the queries. */
+ *          each GPU k-way merges and votes its slice of the queries; queries
+ *          whose label the reference's tie order decides (KNN_FLAG_TIE_PENDING)
+ *          get it from an RCCL send/recv exchange of their exact distances
+ *          (knn_tie_resolve_device), so every mode gives the same labels.
+ * Transport: RCCL whenever G > 1 and the devices are distinct.
+ *   | KNN_GROUP_RCCL: RCCL also at G = 1 (a one-rank communicator: every
+ *     collective of the path runs through RCCL; env KNN_GROUP_RCCL=1 too).
+ *   Repeated devices in devs (e.g. {0, 0, 0}): several ranks share a GPU and
+ *     the collectives run as stream-ordered device copies (loopback) -- the
+ *     whole G-rank decomposition on fewer GPUs, for tests. */
+#define KNN_GROUP_RCCL 0x100
 int knn_group_create(knn_group** out, int ndev, const int* devs, int mode);
+/* Transport of a group: 0 none (G = 1), 1 RCCL, 2 loopback copies. */
+int knn_group_transport(knn_group* g);
+/* knn_set_precision / knn_set_tuning on every rank's context. */
+int knn_group_set_precision(knn_group* g, int mode);
+int knn_group_set_tuning(knn_group* g, const char* key, int64_t value);
 int knn_group_destroy(knn_group* g);
 int knn_group_set_train(knn_group* g, const double* X, const int32_t* labels, int64_t n,
                         int32_t d, int32_t class_cnt);
@@ -267,6 +314,9 @@ int knn_group_classify(knn_group* g, const double* Q, int64_t m, int32_t k, int3
 /* Seconds of the last group classify spent between the first enqueue and
  * the last device completion (device-resident inputs, excludes H2D/D2H). */
 double knn_group_last_compute_seconds(knn_group* g);
+/* Mode 1: queries of the last classify that took the cross-shard reference
+ * tie order (KNN_FLAG_TIE_PENDING -> KNN_FLAG_TIE_REF). */
+int64_t knn_group_last_tie_count(knn_group* g);
 /* Normalisation over the group (cpp:229-306 with the reference's own
  * decomposition): GPU g takes rows [r*g/G, r*(g+1)/G) of every host set,
  * reduces its max/min, ncclAllReduce MAX/MIN combines them (≙ MPI_Allreduce

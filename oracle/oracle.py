@@ -39,6 +39,10 @@ def lib():
         L.oracle_acc.restype = f64
         L.oracle_read_csv.argtypes = [ctypes.c_char_p, i32, i32, i64, P, P]
         L.oracle_read_csv.restype = i64
+        L.oracle_row_distances.argtypes = [P, P, i64, i32, i32, P]
+        L.oracle_row_distances.restype = None
+        L.oracle_sort_vote.argtypes = [P, P, i64, i32, i32, P, i32]
+        L.oracle_sort_vote.restype = i32
         _lib = L
     return _lib
 
@@ -82,6 +86,27 @@ def distance(q, x, euclidean=True):
     q = np.ascontiguousarray(q, np.float64)
     x = np.ascontiguousarray(x, np.float64)
     return lib().oracle_distance(_p(q), _p(x), q.shape[0], int(bool(euclidean)))
+
+
+def row_distances(q, X, euclidean=True):
+    """dist(q, X[j]) for every row j (cpp:33-67 arithmetic)."""
+    q = np.ascontiguousarray(q, np.float64)
+    X = np.ascontiguousarray(X, np.float64)
+    out = np.empty(X.shape[0], np.float64)
+    lib().oracle_row_distances(_p(q), _p(X), X.shape[0], X.shape[1], int(bool(euclidean)),
+                               _p(out))
+    return out
+
+
+def sort_vote(D, labels, K, class_cnt, n_out=0):
+    """The reference's std::sort of records (labels[j], D[j]) in fill order j,
+    then its vote over the first K: (label, first n_out record indices)."""
+    D = np.ascontiguousarray(D, np.float64)
+    labels = np.ascontiguousarray(labels, np.int32)
+    idx = np.empty(max(n_out, 1), np.int64)
+    lab = lib().oracle_sort_vote(_p(D), _p(labels), D.shape[0], int(K), int(class_cnt), _p(idx),
+                                 int(n_out))
+    return int(lab), idx[:n_out]
 
 
 def acc(real, pred):

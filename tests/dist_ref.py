@@ -15,8 +15,10 @@ def vote(labels):
     return best_lab
 
 
-def merge_vote(gd, gi, gl, k, q0, q1):
-    """gd/gi/gl: [parts][m][w] arrays; returns labels, idx[k], dist[k] for q0..q1."""
+def merge_vote(gd, gi, gl, k, q0, q1, pending=None):
+    """gd/gi/gl: [parts][m][w] arrays; returns labels, idx[k], dist[k] for q0..q1.
+    pending (a list) receives the slice rows with any exact tie in the top k
+    or across the k-th place (the merge's KNN_FLAG_TIE_PENDING at ties = 2)."""
     parts = gd.shape[0]
     labs, idxs, dists = [], [], []
     for q in range(q0, q1):
@@ -30,7 +32,25 @@ def merge_vote(gd, gi, gl, k, q0, q1):
         labs.append(vote([e[2] for e in top]))
         idxs.append([e[1] for e in top])
         dists.append([e[0] for e in top])
+        dv = [e[0] for e in ent[:k + 1]]
+        if pending is not None and any(a == b for a, b in zip(dv, dv[1:])):
+            pending.append(q - q0)
     return np.array(labs, np.int32), np.array(idxs, np.int64), np.array(dists, np.float64)
+
+
+def sorted_partial(tr_shard, r0, lab_shard, Q, w, euclidean=True):
+    """A shard's exact top-w per query ordered by (dist, global idx), from
+    the oracle's reference-arithmetic distances (knn_search_partial's
+    semantics): (dist[m][w], idx[m][w], label[m][w])."""
+    import oracle
+    m = Q.shape[0]
+    dd = np.empty((m, w), np.float64)
+    ii = np.empty((m, w), np.int64)
+    for q in range(m):
+        D = oracle.row_distances(Q[q], tr_shard, euclidean)
+        o = np.lexsort((np.arange(D.shape[0]), D))[:w]
+        dd[q], ii[q] = D[o], o + r0
+    return dd, ii, lab_shard[ii - r0].astype(np.int32)
 
 
 def minmax_fold(X, mx, mn, init):

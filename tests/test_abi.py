@@ -71,6 +71,34 @@ def test_version_string(libpath):
     assert b"gfx950" in L.knn_version()
 
 
+class _CandLaunch(ctypes.Structure):
+    """knnk::CandLaunch (csrc/knn_kernels.h), field for field."""
+    _fields_ = [("metric", ctypes.c_int), ("DP", ctypes.c_int), ("R", ctypes.c_int),
+                ("S", ctypes.c_int), ("n_qt", ctypes.c_int), ("n_pad", ctypes.c_int64),
+                ("X32", ctypes.c_void_p), ("xinit", ctypes.c_void_p), ("Q32", ctypes.c_void_p),
+                ("out_v", ctypes.c_void_p), ("out_i", ctypes.c_void_p), ("ablate", ctypes.c_int),
+                ("nw", ctypes.c_int), ("qpb", ctypes.c_int), ("gthr", ctypes.c_void_p),
+                ("xsw", ctypes.c_int), ("gk", ctypes.c_int)]
+
+
+def test_resident_kernel_refuses_mismatched_query_tile(libpath):
+    """The resident candidate kernels index nw x (queries per wave) queries per
+    workgroup; a launch whose host query tile differs (the round-3 fault:
+    group objects of two builds) is refused before anything reaches the
+    device: launch_cand returns false (knn_run_search -> KNN_ERR_ARG).
+    Only the refusal is exercised here -- no kernel is launched."""
+    L = ctypes.CDLL(libpath)
+    sym = "_ZN4knnk11launch_candERKNS_10CandLaunchEP12ihipStream_t"
+    fn = getattr(L, sym)
+    fn.argtypes = [ctypes.POINTER(_CandLaunch), ctypes.c_void_p]
+    fn.restype = ctypes.c_bool
+    for metric, DP, nw, qpb in ((5, 128, 8, 257), (5, 128, 8, 512), (4, 128, 8, 128),
+                                (0, 64, 4, 64), (5, 96, 8, 0)):
+        c = _CandLaunch(metric=metric, DP=DP, R=4 if metric >= 3 else 8, S=1, n_qt=1,
+                        n_pad=256, nw=nw, qpb=qpb)
+        assert fn(ctypes.byref(c), None) is False, (metric, DP, nw, qpb)
+
+
 @pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU behaviour")
 def test_no_gpu_fails_loudly(libpath):
     knn = _load_mirror()

@@ -37,6 +37,16 @@ def _data(n=3000, m=257, d=24, classes=5, seed=4):
     return X[:n].copy(), lab[:n].copy(), X[n:].copy()
 
 
+def _tie_data(n=2500, m=120, d=12, classes=5, seed=71):
+    """Integer codes 0..255 around 5 centres: many exactly equal distances
+    (the reference's own kind of data: MNIST pixels are integers)."""
+    rng = np.random.default_rng(seed)
+    centres = rng.integers(0, 256, (classes, d))
+    lab = rng.integers(0, classes, n + m).astype(np.int32)
+    X = np.clip(centres[lab] + rng.integers(-5, 6, (n + m, d)), 0, 255).astype(np.float64)
+    return X[:n].copy(), lab[:n].copy(), X[n:].copy()
+
+
 def _worker(rank, world, port, mode, out_path):
     import sys
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -68,6 +78,52 @@ def _worker(rank, world, port, mode, out_path):
         full = kd.gather_slices(torch.from_numpy(got), m)  # ≙ MPI_Gather cpp:383
         el = kd.timed(lambda: None, 3, 1, lambda: None)
         result = dict(labels=full.numpy(), el=np.array([el]))
+    elif mode == "train_ties":
+        # integer data full of exact distance ties, 3 shards of unequal size:
+        # the flagged queries take every shard's distances to their owner,
+        # which sorts them as the reference's std::sort does
+        tr, lab, te = _tie_data()
+        n, m, k = tr.shape[0], te.shape[0], 10
+        w = k + 1
+        r0, r1 = kd.shard_range(n, world, rank)
+        q0, q1 = kd.shard_range(m, world, rank)
+        slice_out = {}
+
+        def search_partial(Q):
+            return tuple(torch.from_numpy(a) for a in
+                         dist_ref.sorted_partial(tr[r0:r1], r0, lab[r0:r1], Q, w))
+
+        def merge_vote(gd, gi, gl, parts, a, b):
+            pend = []
+            labs, idx, _ = dist_ref.merge_vote(gd.numpy(), gi.numpy(), gl.numpy(), k, a, b, pend)
+            slice_out.update(labs=labs, idx=idx, pend=np.array(pend, np.int64))
+            return torch.from_numpy(labs)
+
+        class Ties:
+            n_total = n
+
+            def pending(self):
+                return torch.from_numpy(slice_out["pend"])
+
+            def shard_distances(self, sel):
+                return torch.from_numpy(np.stack([oracle.row_distances(te[int(q)], tr[r0:r1])
+                                                  for q in sel.numpy()]))
+
+            def resolve(self, D, rows, orow):
+                T, off = orow.numel(), np.cumsum([0] + list(rows))
+                Dn = D.numpy()
+                for i, o in enumerate(orow.numpy()):
+                    Dq = np.concatenate([Dn[T * off[g] + i * rows[g]:T * off[g] + (i + 1) * rows[g]]
+                                         for g in range(len(rows))])
+                    lb, ix = oracle.sort_vote(Dq, lab, k, 5, n_out=k)
+                    slice_out["labs"][o], slice_out["idx"][o] = lb, ix
+
+        kd.train_sharded(search_partial, merge_vote, te, m, w, k, ties=Ties())
+        labs = kd.gather_slices(torch.from_numpy(slice_out["labs"]), m)
+        idx = kd.gather_slices(torch.from_numpy(slice_out["idx"]), m)
+        npend = torch.tensor([len(slice_out["pend"])])
+        dist.all_reduce(npend)
+        result = dict(labels=labs.numpy(), idx=idx.numpy(), pending=npend.numpy())
     else:
         if mode == "train_bigk":
             # any K <= N_train like cpp:328: the union of the ranks' lists
@@ -124,6 +180,26 @@ def test_two_rank_decomposition_matches_single_process(mode, tmp_path):
         want, _, _ = oracle.knn(tr, lab, te, 7, True, 5)
     got = np.load(out)["labels"]
     np.testing.assert_array_equal(got, want)
+
+
+def test_three_rank_reference_tie_order(tmp_path):
+    """Train-sharded mode on tie-heavy integer data over 3 gloo ranks
+    (ragged shards): the merge flags every query with an exact tie in its
+    top k, the flagged queries' distances to every shard go to their owner
+    (all-gather of ids + all-to-all of distance blocks, knn_dist.resolve_ties)
+    and the owner's std::sort over the whole train set gives the reference's
+    labels AND neighbour order for every query."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    out = str(tmp_path / "t.npz")
+    mp.spawn(_worker, args=(3, _free_port(), "train_ties", out), nprocs=3, join=True)
+    tr, lab, te = _tie_data()
+    want, widx, _ = oracle.knn(tr, lab, te, 10, True, 5, n_out=10)
+    got = np.load(out)
+    assert int(got["pending"][0]) > 30, "expected many tied queries"
+    np.testing.assert_array_equal(got["labels"], want)
+    np.testing.assert_array_equal(got["idx"], widx)
 
 
 def test_shard_ranges_cover_ragged():

@@ -78,12 +78,17 @@ def test_normalize_matches_oracle(clf, n, m, v, d):
                                                 0))
 
 
-def test_group_normalize_matches_oracle(knn):
+@pytest.mark.parametrize("devs,rccl", [([0], False), ([0], True), ([0, 0, 0], False)])
+def test_group_normalize_matches_oracle(knn, devs, rccl):
+    """The group's sharded normalisation: one GPU; one GPU with the MAX / MIN
+    all-reduce through a one-rank RCCL communicator; three ranks on one GPU
+    (loopback transport: ragged shards, the all-reduce over three partials)."""
     tr, te, va = _sets(4099, 501, 250, 96, seed=3)
     wtr, wte, wva = tr.copy(), te.copy(), va.copy()
     oracle.normalize(wtr, wte, wva)
-    g = knn.Group([0], mode=0)
+    g = knn.Group(devs, mode=0, rccl=rccl)
     try:
+        assert g.transport() == (2 if len(devs) > 1 else 1 if rccl else 0)
         g.normalize(tr, te, va)
     finally:
         g.close()
