@@ -268,15 +268,28 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   }
 
   constexpr int NQL = M16 ? QB : 1;  // queries (lists) per lane
-  float L[NQL][R];
+  // int8: lists of the accumulators themselves (KNN_I8_ILIST, knn_device.h)
+  constexpr bool ILIST = I8 && KNN_I8_ILIST;
+  using LT = std::conditional_t<ILIST, int, float>;
+  LT L[NQL][R];
   int I[NQL][R];
   float thr[NQL];
 #pragma unroll
   for (int b = 0; b < NQL; ++b) {
 #pragma unroll
-    for (int t = 0; t < R; ++t) { L[b][t] = KNN_INF_F; I[b][t] = -1; }
+    for (int t = 0; t < R; ++t) {
+      if constexpr (ILIST) L[b][t] = INT_MIN;
+      else L[b][t] = KNN_INF_F;
+      I[b][t] = -1;
+    }
     thr[b] = KNN_INF_F;
   }
+  // the int8 selection on either list form
+  auto select_i8 = [&](const auto& a, const auto& b, int row0, auto& Lq, auto& Iq, float& teq,
+                       int& tnq, SelCount& sc) {
+    if constexpr (ILIST) select_quad_i8i<R>(a, b, row0, Lq, Iq, tnq, sc);
+    else select_quad_i8<R>(a, b, row0, Lq, Iq, teq, tnq, sc);
+  };
 
   // Global per-query threshold.  The query's lists are spread over S
   // workgroups; they form G groups by split % G (disjoint row sets), and slot
@@ -387,7 +400,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
     const int t = split + it * S;
     if constexpr (TEC) {
 #pragma unroll
-      for (int b = 0; b < NQL; ++b) thr[b] = L[b][R - 1];  // for the exchange below
+      for (int b = 0; b < NQL; ++b) thr[b] = lval(L[b][R - 1]);  // for the exchange below
     }
     {
       // this wave's pieces of tile `it` have landed once at most the pieces
@@ -445,7 +458,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
               for (int b = 0; b < QB; ++b) {
                 float u[4];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) u[e] = L[b][e];
+                for (int e = 0; e < 4; ++e) u[e] = lval(L[b][e]);
                 mb[b] = union_kth<4>(u, gk);
               }
             } else {
@@ -462,7 +475,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
             if (gk) {
               float u[4];
 #pragma unroll
-              for (int e = 0; e < 4; ++e) u[e] = L[0][e];
+              for (int e = 0; e < 4; ++e) u[e] = lval(L[0][e]);
               m = union_kth<2>(u, gk);
             } else {
               const auto sw = __builtin_amdgcn_permlane32_swap(
@@ -547,7 +560,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
         if (!(abl & 2)) {
 #pragma unroll
           for (int qb = 0; qb < QB; ++qb)
-            select_quad_i8<R>(accp[0][qb], accp[1][qb], rowp, L[qb], I[qb], te[qb], tn[qb], selc);
+            select_i8(accp[0][qb], accp[1][qb], rowp, L[qb], I[qb], te[qb], tn[qb], selc);
 #pragma unroll
           for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
@@ -559,7 +572,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       } else if (!(abl & 2)) {
 #pragma unroll
         for (int qb = 0; qb < QB; ++qb)
-          select_quad_i8<R>(acc[0][qb], acc[1][qb], row0, L[qb], I[qb], te[qb], tn[qb], selc);
+          select_i8(acc[0][qb], acc[1][qb], row0, L[qb], I[qb], te[qb], tn[qb], selc);
       } else if (acc[0][0][0] == 12345 && acc[1][1][3] == 12345) {
         thr[0] = (float)acc[0][1][2];  // keep the accumulators live
       }
@@ -721,7 +734,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
 #pragma unroll
       for (int qb = 0; qb < QB; ++qb) {
         if constexpr (I8)
-          select_quad_i8<R>(accp[0][qb], accp[1][qb], rowp, L[qb], I[qb], te[qb], tn[qb], selc);
+          select_i8(accp[0][qb], accp[1][qb], rowp, L[qb], I[qb], te[qb], tn[qb], selc);
         else
           select_quad_te<R>(accp[0][qb], accp[1][qb], rowp, L[qb], I[qb], te[qb]);
       }
@@ -743,7 +756,8 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       const int64_t o = ((qb0 + 16 * qb) * (4 * S) + split * 4 + g16) * R;
 #pragma unroll
       for (int t = 0; t < R; t += 4) {
-        *(float4*)(out_v + o + t) = make_float4(L[qb][t], L[qb][t + 1], L[qb][t + 2], L[qb][t + 3]);
+        *(float4*)(out_v + o + t) = make_float4(lval(L[qb][t]), lval(L[qb][t + 1]),
+                                                lval(L[qb][t + 2]), lval(L[qb][t + 3]));
         *(int4*)(out_i + o + t) = make_int4(I[qb][t], I[qb][t + 1], I[qb][t + 2], I[qb][t + 3]);
       }
     }

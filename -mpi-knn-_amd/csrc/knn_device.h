@@ -504,6 +504,62 @@ __device__ __forceinline__ void select_quad_i8(const i32x4& a, const i32x4& b, i
   }
 }
 
+// int8 kernel lists in the accumulator domain (KNN_I8_ILIST): entries are the
+// int32 accumulators themselves, best (largest) first, INT_MIN = empty; the
+// proxy -2 acc (a float, exact below 2^24) is formed only where a float is
+// needed -- the per-tile exchange and the final write.  An insertion is then
+// integer min/max selects and the filter update one v_max (no conversions).
+#ifndef KNN_I8_ILIST
+#define KNN_I8_ILIST 1
+#endif
+__device__ __forceinline__ float i8_proxy(int acc) {
+  return acc == INT_MIN ? KNN_INF_F : (float)(-2 * acc);
+}
+// a list entry as the proxy the merge reads (float lists: itself)
+__device__ __forceinline__ float lval(float v) { return v; }
+__device__ __forceinline__ float lval(int acc) { return i8_proxy(acc); }
+template <int R>
+__device__ __forceinline__ void list_insert_desc(int (&L)[R], int (&I)[R], int v, int id) {
+  bool cc = true;  // v > L[R-1] by precondition
+#pragma unroll
+  for (int t = R - 1; t > 0; --t) {
+    const bool cp = v > L[t - 1];
+    L[t] = min(L[t - 1], max(v, L[t]));
+    I[t] = cp ? I[t - 1] : (cc ? id : I[t]);
+    cc = cp;
+  }
+  I[0] = cc ? id : I[0];
+  L[0] = max(v, L[0]);
+}
+// tn: the quad's filter (i8_neg_half of the tile's te) raised by this lane's
+// own insertions; tn >= L[R-1] always, so v > tn meets the insert precondition
+template <int R>
+__device__ __forceinline__ void select_quad_i8i(const i32x4& a, const i32x4& b, int row0,
+                                                int (&L)[R], int (&I)[R], int& tn, SelCount& sc) {
+  const int m1 = max(max(a[0], a[1]), a[2]);
+  const int m2 = max(max(a[3], b[0]), b[1]);
+  const int m3 = max(max(b[2], b[3]), m1);
+  const int mx = max(m2, m3);
+#if KNN_COUNT_SEL
+  sc.calls++;
+  sc.lane_pass += mx > tn;
+  sc.wave_pass += __builtin_amdgcn_ballot_w64(mx > tn) != 0;
+#endif
+  if (__builtin_amdgcn_ballot_w64(mx > tn)) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int v = i < 4 ? a[i] : b[i - 4];
+      if (v > tn) {
+#if KNN_COUNT_SEL
+        sc.inserts++;
+#endif
+        list_insert_desc<R>(L, I, v, row_at(row0, i < 4 ? i : 16 + i - 4));
+        tn = max(tn, L[R - 1]);
+      }
+    }
+  }
+}
+
 // Lists are stored [query][split][half][R] so a query's 2S lists are contiguous.
 template <int R>
 __device__ __forceinline__ void write_lists(float* __restrict__ out_v, int* __restrict__ out_i,

@@ -170,6 +170,8 @@ def resolve_ties(ties, m, device=None, budget_bytes=1 << 30):
     total = sum(counts)
     if total == 0:
         return 0
+    if hasattr(ties, "prepare"):  # collective set-up every rank runs (e.g. the global labels)
+        ties.prepare()
     pad = torch.full((max(counts),), -1, dtype=torch.int64, device=device)
     pad[:pend.numel()] = pend + q0
     ids = _all_gather_stack(pad) if world > 1 else pad[None]
@@ -198,3 +200,44 @@ def resolve_ties(ties, m, device=None, budget_bytes=1 << 30):
         if take[rank]:
             ties.resolve(recv, rows, (mine - q0).to(torch.int32))
     return total
+
+
+class HipTies:
+    """The `ties` of resolve_ties on the HIP library (knn_amd.Classifier of
+    this rank's shard): the merge's KNN_FLAG_TIE_PENDING rows of the slice
+    outputs, knn_shard_distances_device, knn_tie_resolve_device into the same
+    outputs.  Every train label is all-gathered the first time any rank has
+    a flagged query (4 B per row)."""
+    FLAG_TIE_PENDING = 64
+
+    def __init__(self, ctx, Q, lab_shard, n_total, k, outs, mq, metric=0, stream=None,
+                 device=None):
+        self.ctx, self.Q, self.lab_shard, self.n_total, self.k = ctx, Q, lab_shard, n_total, k
+        self.o_lab, self.o_idx, self.o_dist, self.o_flags = outs
+        self.mq, self.metric, self.stream, self.device = mq, metric, stream, device
+        self.lab_all = None
+        self.resolved = 0
+
+    def pending(self):
+        return torch.nonzero(self.o_flags[:self.mq] & self.FLAG_TIE_PENDING).flatten()
+
+    def prepare(self):
+        if self.lab_all is None:
+            self.lab_all = gather_slices(self.lab_shard, self.n_total, self.device).contiguous()
+
+    def shard_distances(self, sel):
+        sel = sel.contiguous()
+        D = torch.empty((sel.numel(), self.lab_shard.shape[0]), dtype=torch.float64,
+                        device=self.device)
+        self.ctx.shard_distances_device(self.Q.data_ptr(), sel.data_ptr(), sel.numel(),
+                                        self.metric, D.data_ptr(), self.stream)
+        return D
+
+    def resolve(self, D, rows, orow):
+        orow = orow.contiguous()
+        self.ctx.tie_resolve_device(D.data_ptr(), rows, orow.numel(), self.lab_all.data_ptr(),
+                                    orow.data_ptr(), self.k, self.o_lab.data_ptr(),
+                                    None if self.o_idx is None else self.o_idx.data_ptr(),
+                                    None if self.o_dist is None else self.o_dist.data_ptr(),
+                                    self.o_flags.data_ptr(), self.stream)
+        self.resolved += orow.numel()

@@ -1,0 +1,49 @@
+#!/bin/bash
+# One GPU call of the build/measure loop (replaces round 3's per-tag
+# r3*_gpu.sh scripts).  Steps, each with its own time limit, stopping at the
+# first failure:
+#   TESTS=1        the whole -m gpu suite          -> gpurun_out/$TAG_tests.log
+#   TESTS="<args>" those pytest arguments instead
+#   AB_VARIANTS    cross-process A/B of lib/libknn_amd_<v>.so ("base" = default)
+#                  with tools/tune.py $AB_ARGS, REPS rounds -> $TAG_ab_<v>_<rep>.log
+#   BENCH=1        bench.py --steps 20 --warmup 5 -> $TAG_bench.log / .json
+#   PROF=1         rocprofv3 kernel trace + stats of a short bench -> $TAG_prof/
+# Usage: TAG=r4b TESTS=1 AB_VARIANTS="base fl" AB_ARGS="--rounds 5 auto:0:0" \
+#        bash tools/gpu_round.sh
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+O=gpurun_out
+mkdir -p $O
+TAG=${TAG:-run}
+if [ -n "$TESTS" ]; then
+  args="tests"
+  [ "$TESTS" = 1 ] || args="$TESTS"
+  timeout -k 10 ${TEST_LIMIT:-600} python -u -m pytest -x -q -m gpu --timeout 300 \
+      --timeout-method thread $args > $O/${TAG}_tests.log 2>&1
+  rc=$?; echo "tests rc=$rc"; tail -5 $O/${TAG}_tests.log
+  [ $rc = 0 ] || exit $rc
+fi
+if [ -n "$AB_VARIANTS" ]; then
+  for rep in $(seq 1 ${REPS:-2}); do
+    for v in $AB_VARIANTS; do
+      if [ $v = base ]; then unset KNN_AMD_VARIANT; else export KNN_AMD_VARIANT=$v; fi
+      timeout -k 10 200 python3 -u tools/tune.py $AB_ARGS > $O/${TAG}_ab_${v}_$rep.log 2>&1
+      rc=$?; echo "ab $v $rep rc=$rc"; grep " cand " $O/${TAG}_ab_${v}_$rep.log
+      [ $rc = 0 ] || exit $rc
+    done
+  done
+  unset KNN_AMD_VARIANT
+fi
+if [ -n "$BENCH" ]; then
+  timeout -k 10 ${BENCH_LIMIT:-400} python3 -u bench.py --steps 20 --warmup 5 ${BENCH_ARGS} \
+      > $O/${TAG}_bench.json 2> $O/${TAG}_bench.log
+  rc=$?; echo "bench rc=$rc"; tail -c 600 $O/${TAG}_bench.json
+  [ $rc = 0 ] || exit $rc
+fi
+if [ -n "$PROF" ]; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/${TAG}_prof -o prof -- \
+      python3 -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-fp32-path --no-continuous --no-dropin --no-train-sharded --cfg3-queries 0 > $O/${TAG}_prof.log 2>&1
+  rc=$?; echo "prof rc=$rc"
+  [ $rc = 0 ] || exit $rc
+fi
+exit 0
