@@ -369,7 +369,7 @@ static int ensure_fp16_s3(knn_ctx* ctx, hipStream_t s) {
 // train set: identical operands and seeds for those rows, hence identical
 // proxies) and seeds every query's slots with the need-th smallest proxy of
 // its sample lists (launch_seed_gthr).  Measured a net loss at cfg2, one
-// setting per process (gpurun_out/r3o_*.log): int8 candidate phase 1.40-1.43
+// setting per process (profiles/ab_log.md: r3o_*): int8 candidate phase 1.40-1.43
 // ms off, 1.42-1.45 with 8192 rows, 1.44-1.46 with 16384, 1.53 with 32768;
 // fp16 2.28 off vs 2.47 -- the sample pass runs cold itself (every lane
 // inserts) and a sample-rank threshold saves little next to the thresholds
@@ -729,7 +729,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   // queries per wave of the resident kernel (int8: 16 x the build's query
   // blocks); the int8 kernel with 64 queries per wave also runs 4 waves
   const int qpw = !s3 && DP <= 256 ? cand_queries_per_wave(kmetric, DP) : 32;
-  if (kmetric == 5 && ctx->tune_nw && qpw > 32) nw = ctx->tune_nw;
+  if (kmetric == 5 && ctx->tune_nw) nw = ctx->tune_nw;  // 4 or 8 (int8 builds have both)
   if (s3) nw = 8;
   const int qpb = s3 ? kS3Rows : (DP <= 256 ? qpw * nw : kQPB);
   const int n_qt = (int)((m + qpb - 1) / qpb);
@@ -768,7 +768,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   // W <= 123); else, in the resident kernel, the lists' R-th entries in 4
   // groups.  cfg2 (W = 11): K = 2, the candidate pass 3 % faster than K = 3
   // and 2-4 % faster than the list thresholds (in-process A/B,
-  // gpurun_out/r2f_ab_gk.log, r2g_ab_pair.log); K = 1 (8 rows < W) sends 5 %
+  // profiles/ab_log.md: r2f_ab_gk, r2g_ab_pair); K = 1 (8 rows < W) sends 5 %
   // of the queries to the rescan.
   int gk = (W + 5 + kGthrSlots - 1) / kGthrSlots;
   if (gk > (s3 ? 16 : 4)) gk = 0;

@@ -45,7 +45,7 @@ static_assert(KNN_RES_TPB * knnk::kTR == knnk::kResTileRows || KNN_RES_TPB != 2,
 // int8 kernel: 32-row sub-tiles per staged tile (8: 256-row tiles, half the
 // barriers and per-tile work per MFMA of 128-row tiles, and a 256-row lead
 // for the streamed rows; n_pad is a multiple of kRowAlign = 256): cfg2
-// candidate pass 1.636 -> 1.50 ms against 4 (gpurun_out/r3c_ab_*.log), where
+// candidate pass 1.636 -> 1.50 ms against 4 (profiles/ab_log.md: r3c_ab_*), where
 // a third LDS buffer of 128-row tiles measured +4 % and 64 queries per wave
 // +12 %
 #ifndef KNN_I8_TPB
@@ -364,7 +364,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   // barrier of tile e + XPD); KNN_XPD_MIN = 2 lets them pass the barrier of
   // tile e + 1 even at PD = 1 (counted as younger than its pieces), but the
   // thresholds then arrive a tile later: int8 cfg2 candidate +2.5 %
-  // (gpurun_out/r3e_ab_*.log), so the default waits at tile e + 1
+  // (profiles/ab_log.md: r3e_ab_*), so the default waits at tile e + 1
 #ifndef KNN_XPD_MIN
 #define KNN_XPD_MIN 1
 #endif
@@ -796,14 +796,14 @@ static void launch_res(const CandLaunch& c, hipStream_t s) {
 
 // Instantiated variants: R in {4, 8, 16}; METRIC 0/2 with NW in {4, 8};
 // METRIC 4 also with NW = 16 (512 queries share each staged tile); METRIC 5
-// (int8) with R = 4, NW = 8 at DP % 64 == 0;
+// (int8) with R = 4 (8 on request), NW = 8 or 4 at DP % 64 == 0;
 // METRIC 1 (L1, not perf-graded) with NW = 4 and R in {8, 16}; METRIC 2
 // needs DP % 16 == 0.
 template <int DP, int R, int M, int NW>
 constexpr bool res_variant() {
   return (M != 2 || DP % 16 == 0) && (M != 1 || (NW == 4 && R != 4)) &&
          (M < 3 || (DP % 32 == 0 && (R == 4 || (M == 5 && R == 8)) && (NW == 8 || M >= 4))) && (NW != 16 || M == 4) &&
-         (M != 5 || (DP % 64 == 0 && (NW == 8 || (NW == 4 && KNN_I8_QB > 2))));
+         (M != 5 || (DP % 64 == 0 && (NW == 8 || NW == 4)));
 }
 
 template <int DP>

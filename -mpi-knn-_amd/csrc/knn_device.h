@@ -450,7 +450,7 @@ __device__ __forceinline__ int i8_neg_half(float te) {
 // the no-insertion case is 4 v_max3 + 1 compare per call.
 // KNN_I8_UBR: the no-candidate test as a wave-uniform branch (v_cmp into an
 // SGPR pair + s_cbranch_vccz) instead of an exec-masked region (cfg2
-// candidate pass -1.3 %, gpurun_out/r3d_ab_*.log)
+// candidate pass -1.3 %, profiles/ab_log.md: r3d_ab_*)
 #ifndef KNN_I8_UBR
 #define KNN_I8_UBR 1
 #endif

@@ -40,12 +40,15 @@ def knn():
     return mod
 
 
-def _tie_set(metric, n=5000, m=300, d=12, seed=71):
-    """The integer tie-heavy set of test_reference_tie_order_everywhere."""
+def _tie_set(metric, n=5000, m=300, d=6, seed=171):
+    """Integer codes 0..9 in 6 dims with labels independent of position:
+    nearly every query has exactly equal distances with different labels in
+    its top k (the oracle finds 299 of 300 at k = 10), and a tie across the
+    k-th place in most -- the label then depends on the reference's
+    std::sort order."""
     rng = np.random.default_rng(seed + metric)
-    centres = rng.integers(0, 256, (5, d))
+    X = rng.integers(0, 10, (n + m, d)).astype(np.float64)
     lab = rng.integers(0, 5, n + m).astype(np.int32)
-    X = np.clip(centres[lab] + rng.integers(-5, 6, (n + m, d)), 0, 255).astype(np.float64)
     return X[:n].copy(), lab[:n].copy(), X[n:].copy()
 
 
@@ -90,6 +93,12 @@ def test_group_train_sharded_reference_tie_order(knn, devs, rccl, metric):
         np.testing.assert_array_equal(idx[ref], widx[ref])
         assert_neighbors_match(idx, dist, widx, wdist, flags)
     assert tie_votes > 50, "expected many exact-tie votes"
+    # without the exchange ("ties" = 0: index order inside ties) some labels
+    # differ from the reference's -- the set exercises label-deciding ties
+    want, _, _ = oracle.knn(tr, lab, te, 10, metric == 0, 5)
+    g.set_tuning("ties", 0)
+    got0 = g.classify(te, 10, metric)
+    assert (got0 != want).sum() > 0
     g.set_tuning("ties", 2)
     want, widx, wdist = oracle.knn(tr, lab, te, 10, metric == 0, 5, n_out=10)
     got, idx, dist, flags = g.classify(te, 10, metric, return_neighbors=True)
