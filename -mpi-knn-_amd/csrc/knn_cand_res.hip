@@ -278,7 +278,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   for (int b = 0; b < NQL; ++b) {
 #pragma unroll
     for (int t = 0; t < R; ++t) {
-      if constexpr (ILIST) L[b][t] = INT_MIN;
+      if constexpr (ILIST) L[b][t] = kI8Floor;
       else L[b][t] = KNN_INF_F;
       I[b][t] = -1;
     }
@@ -287,7 +287,8 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   // the int8 selection on either list form
   auto select_i8 = [&](const auto& a, const auto& b, int row0, auto& Lq, auto& Iq, float& teq,
                        int& tnq, SelCount& sc) {
-    if constexpr (ILIST) select_quad_i8i<R>(a, b, row0, Lq, Iq, tnq, sc);
+    if constexpr (ILIST && KNN_I8_SLOW == 2) select_quad_i8t<R>(a, b, row0, Lq, Iq, tnq, sc);
+    else if constexpr (ILIST) select_quad_i8i<R>(a, b, row0, Lq, Iq, tnq, sc);
     else select_quad_i8<R>(a, b, row0, Lq, Iq, teq, tnq, sc);
   };
 
@@ -332,7 +333,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
 #pragma unroll
   for (int b = 0; b < NQL; ++b) {
     tq[b] = te[b] = KNN_INF_F;
-    tn[b] = INT_MIN;
+    tn[b] = kI8Floor;
   }
   uint32_t last_pub = kKeyInf;
   int x_ops = 0, x_age = -1;  // ops of the pending exchange, tiles since it
@@ -341,14 +342,14 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   constexpr bool PIPE = TEC && KNN_M4_PIPE && DP <= 192;  // DP 256: no registers to spare
   using AccT = std::conditional_t<I8, i32x4, f32x4>;
   // PIPE: the previous sub-tile's accumulators; before the first sub-tile
-  // they hold values no filter passes (int8: INT_MIN, fp16: +inf), so the
+  // they hold values no filter passes (int8: kI8Floor, fp16: +inf), so the
   // pipelined selection needs no first-sub-tile check
   AccT accp[2][QB];
 #pragma unroll
   for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
     for (int qb = 0; qb < QB; ++qb) {
-      if constexpr (I8) accp[rb][qb] = i32x4{INT_MIN, INT_MIN, INT_MIN, INT_MIN};
+      if constexpr (I8) accp[rb][qb] = i32x4{kI8Floor, kI8Floor, kI8Floor, kI8Floor};
       else accp[rb][qb] = f32x4{KNN_INF_F, KNN_INF_F, KNN_INF_F, KNN_INF_F};
     }
   int rowp = 0;

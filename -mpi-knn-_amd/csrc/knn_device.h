@@ -442,9 +442,15 @@ __device__ __forceinline__ void select_quad_te(const f32x4& a, const f32x4& b, i
 // acc > -te / 2, so the filter runs on the accumulators as they stand (a
 // max-tree, no per-value conversion); only an insertion forms the proxy.
 typedef int i32x4 __attribute__((ext_vector_type(4)));
+// Below every real accumulator: codes and query codes lie in [-128, 127] and
+// d <= 256, so q.k >= -2^22 and the seed >= -2^21, i.e. acc > -2^23.  Pad
+// rows carry it as their seed (acc = kI8Floor exactly, the codes being 0),
+// empty list entries and the empty filter hold it, and the strict test
+// acc > tn never selects a pad row.  Keys acc * 8 + position fit in int32.
+constexpr int kI8Floor = -(1 << 23);
 __device__ __forceinline__ int i8_neg_half(float te) {
-  // -te/2 as an int (te: even integers, +inf -> INT_MIN: every row passes)
-  return te > 3.0e38f ? INT_MIN : (int)(-0.5f * te);
+  // -te/2 as an int (te: even integers, +inf -> kI8Floor: every real row passes)
+  return te > 3.0e38f ? kI8Floor : (int)(-0.5f * te);
 }
 // tn = i8_neg_half(te), kept by the caller (refreshed with te per tile):
 // the no-insertion case is 4 v_max3 + 1 compare per call.
@@ -505,7 +511,7 @@ __device__ __forceinline__ void select_quad_i8(const i32x4& a, const i32x4& b, i
 }
 
 // int8 kernel lists in the accumulator domain (KNN_I8_ILIST): entries are the
-// int32 accumulators themselves, best (largest) first, INT_MIN = empty; the
+// int32 accumulators themselves, best (largest) first, kI8Floor = empty; the
 // proxy -2 acc (a float, exact below 2^24) is formed only where a float is
 // needed -- the per-tile exchange and the final write.  An insertion is then
 // integer min/max selects and the filter update one v_max (no conversions).
@@ -513,7 +519,7 @@ __device__ __forceinline__ void select_quad_i8(const i32x4& a, const i32x4& b, i
 #define KNN_I8_ILIST 1
 #endif
 __device__ __forceinline__ float i8_proxy(int acc) {
-  return acc == INT_MIN ? KNN_INF_F : (float)(-2 * acc);
+  return acc <= kI8Floor ? KNN_INF_F : (float)(-2 * acc);
 }
 // a list entry as the proxy the merge reads (float lists: itself)
 __device__ __forceinline__ float lval(float v) { return v; }
@@ -555,6 +561,67 @@ __device__ __forceinline__ void select_quad_i8i(const i32x4& a, const i32x4& b, 
 #endif
         list_insert_desc<R>(L, I, v, row_at(row0, i < 4 ? i : 16 + i - 4));
         tn = max(tn, L[R - 1]);
+      }
+    }
+  }
+}
+
+// KNN_I8_SLOW = 2: the slow path inserts each lane's best passing value
+// first, found with its position by a max over keys acc * 8 + position
+// (exact and order-preserving: acc >= kI8Floor = -2^23), and tests the lane's second
+// best before the per-value loop: the common slow call (each passing lane
+// has one passing value) is one insertion for all its lanes instead of one
+// per distinct position, and no per-value exec-mask branches
+#ifndef KNN_I8_SLOW
+#define KNN_I8_SLOW 1
+#endif
+template <int R>
+__device__ __forceinline__ void select_quad_i8t(const i32x4& a, const i32x4& b, int row0,
+                                                int (&L)[R], int (&I)[R], int& tn, SelCount& sc) {
+  const int m1 = max(max(a[0], a[1]), a[2]);
+  const int m2 = max(max(a[3], b[0]), b[1]);
+  const int m3 = max(max(b[2], b[3]), m1);
+  const int mx = max(m2, m3);
+#if KNN_COUNT_SEL
+  sc.calls++;
+  sc.lane_pass += mx > tn;
+  sc.wave_pass += __builtin_amdgcn_ballot_w64(mx > tn) != 0;
+#endif
+  if (__builtin_amdgcn_ballot_w64(mx > tn)) {
+    int k[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) k[i] = (i < 4 ? a[i] : b[i - 4]) * 8 + i;
+    // top two keys of the eight
+    int hi[4], lo[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      hi[p] = max(k[2 * p], k[2 * p + 1]);
+      lo[p] = min(k[2 * p], k[2 * p + 1]);
+    }
+    const int hA = max(hi[0], hi[1]), lA = max(min(hi[0], hi[1]), max(lo[0], lo[1]));
+    const int hB = max(hi[2], hi[3]), lB = max(min(hi[2], hi[3]), max(lo[2], lo[3]));
+    const int k1 = max(hA, hB), k2 = max(min(hA, hB), max(lA, lB));
+    int tk = tn * 8 + 7;  // acc > tn  <=>  key > tk (acc, tn >= kI8Floor: no overflow)
+    if (k1 > tk) {
+#if KNN_COUNT_SEL
+      sc.inserts++;
+#endif
+      const int p = k1 & 7;
+      list_insert_desc<R>(L, I, k1 >> 3, row0 + p + 12 * (p >> 2));
+      tn = max(tn, L[R - 1]);
+      tk = tn * 8 + 7;
+    }
+    if (__builtin_amdgcn_ballot_w64(k2 > tk)) {  // a lane with more passing values
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if (k[i] > tk && k[i] != k1) {
+#if KNN_COUNT_SEL
+          sc.inserts++;
+#endif
+          list_insert_desc<R>(L, I, k[i] >> 3, row_at(row0, i < 4 ? i : 16 + i - 4));
+          tn = max(tn, L[R - 1]);
+          tk = tn * 8 + 7;
+        }
       }
     }
   }

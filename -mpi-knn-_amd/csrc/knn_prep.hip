@@ -411,7 +411,7 @@ void launch_grid_stats(const double* X64, int64_t n, int d, double* partial, dou
 // row 4g, j = 0..3) is -ceil(||k||^2 / 2), the accumulator seed: the kernel
 // ends at dot(q, k) - ceil(||k||^2 / 2) = -(proxy + (||k||^2 & 1)) / 2 with
 // proxy = ||k||^2 - 2 q.k, i.e. it ranks by proxy + (0 or 1).  Pad rows:
-// INT_MIN (never selected).  codes_max receives max ||k||^2.
+// kI8Floor (below every real accumulator: never selected).  codes_max receives max ||k||^2.
 __global__ void __launch_bounds__(256)
 prep_i8_train_kernel(const double* __restrict__ X64, const double* __restrict__ cent, int64_t n,
                      int d, int DP, int64_t n_pad, int s, signed char* __restrict__ out,
@@ -433,7 +433,7 @@ prep_i8_train_kernel(const double* __restrict__ X64, const double* __restrict__ 
     }
     q2 = wave_sum_i(q2);
     mx = max(mx, (unsigned)q2);
-    const int seed = row < n ? -((q2 + 1) >> 1) : INT_MIN;
+    const int seed = row < n ? -((q2 + 1) >> 1) : kI8Floor;
     // seeds of rows 4g .. 4g+3 in the pad of row 4g (n_pad % 4 == 0): every
     // row writes its own slot of its group leader's pad
     if (lane == 0) ((int*)(out + (row & ~3ll) * row_bytes + DP))[row & 3] = seed;
