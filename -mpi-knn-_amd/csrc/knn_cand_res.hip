@@ -67,6 +67,10 @@ static_assert(KNN_RES_TPB * knnk::kTR == knnk::kResTileRows || KNN_RES_TPB != 2,
 #ifndef KNN_I8_QB
 #define KNN_I8_QB 2
 #endif
+// int8 kernel: LDS fragments of the next sub-tile read ahead (see cand_kernel)
+#ifndef KNN_I8_PF
+#define KNN_I8_PF 0
+#endif
 #ifndef KNN_I8_WPE
 #define KNN_I8_WPE 2
 #endif
@@ -514,6 +518,29 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
         if constexpr (I8) tn[b] = i8_neg_half(te[b]);
       }
     }
+    // int8: the LDS fragments (seeds and A) of a sub-tile; with KNN_I8_PF
+    // those of sub-tile s+1 are read before the MFMAs of s are issued, so
+    // their latency hides behind s's MFMAs (sub-tile 0 of a tile reads its
+    // own after the barrier)
+    constexpr bool I8PF = I8 && KNN_I8_PF;
+    i32x4 pf_sd[2], pf_af[I8 ? DP / 64 : 1][2];
+    const int g16s = g16 ^ (xsw ? xh_swz(c16) : 0);
+    auto i8_seeds = [&](const float* b, i32x4 (&sd)[2]) {
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+        sd[rb] = __builtin_bit_cast(i32x4, *(const float4*)(b + (rb * 16 + 4 * g16) * RSF + SEED));
+    };
+    auto i8_frags = [&](const float* b, i32x4 (&sd)[2], i32x4 (&af)[I8 ? DP / 64 : 1][2]) {
+      // (KNN_I8_PF = 2: the seeds are read with their own sub-tile)
+      if (KNN_I8_PF != 2) i8_seeds(b, sd);
+#pragma unroll
+      for (int ks = 0; ks < (I8 ? DP / 64 : 1); ++ks)
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+          af[ks][rb] = __builtin_bit_cast(
+              i32x4, *(const float4*)(b + (rb * 16 + c16) * RSF + 16 * ks + 4 * g16s));
+    };
+    if constexpr (I8PF) i8_frags(lds + cur * BUFF, pf_sd, pf_af);
 #pragma unroll
     for (int sub = 0; sub < TPB; ++sub) {
     const float* base = lds + cur * BUFF + sub * kTR * RSF;
@@ -522,25 +549,31 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       // int8 codes on v_mfma_i32_16x16x64_i8, exact: the accumulators start
       // at -ceil(||k||^2 / 2) (the pad of row 4g carries rows 4g .. 4g+3)
       // and end at q.k - ceil(||k||^2 / 2); one MFMA per 64 dims
-      i32x4 acc[2][QB];
-#pragma unroll
-      for (int rb = 0; rb < 2; ++rb) {
-        const i32x4 sd = __builtin_bit_cast(i32x4, *(const float4*)(base + (rb * 16 + 4 * g16) * RSF + SEED));
-#pragma unroll
-        for (int qb = 0; qb < QB; ++qb) acc[rb][qb] = sd;
-      }
-      const int g16s = g16 ^ (xsw ? xh_swz(c16) : 0);
       // every A fragment of the sub-tile (DP / 32 reads) is read before its
       // MFMAs, fenced (KNN_I8_SCHED): the registers are there (the query
       // image is half the fp16 one), and the compiler's own schedule would
       // wait on each read just before its two MFMAs
-      i32x4 af[DP / 64][2];
+      i32x4 sdv[2], af[DP / 64][2];
+      if constexpr (I8PF) {
+        if constexpr (KNN_I8_PF == 2) {
+          i8_seeds(base, sdv);
+        } else {
 #pragma unroll
-      for (int ks = 0; ks < DP / 64; ++ks)
+          for (int rb = 0; rb < 2; ++rb) sdv[rb] = pf_sd[rb];
+        }
 #pragma unroll
-        for (int rb = 0; rb < 2; ++rb)
-          af[ks][rb] = __builtin_bit_cast(
-              i32x4, *(const float4*)(base + (rb * 16 + c16) * RSF + 16 * ks + 4 * g16s));
+        for (int ks = 0; ks < DP / 64; ++ks)
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb) af[ks][rb] = pf_af[ks][rb];
+        if (sub + 1 < TPB) i8_frags(base + kTR * RSF, pf_sd, pf_af);
+      } else {
+        i8_frags(base, sdv, af);
+      }
+      i32x4 acc[2][QB];
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) acc[rb][qb] = sdv[rb];
 #if KNN_I8_SCHED
       __builtin_amdgcn_sched_barrier(0);
 #endif
