@@ -312,26 +312,29 @@ static int ensure_fp16(knn_ctx* ctx, hipStream_t s) {
   return KNN_OK;
 }
 
-// The int8 image for kernel metric 5 (knn_prep.hip): codes x 2^s - c of
-// every row (16-B chunks swizzled as the fp16 image) + the accumulator seeds
-// -ceil(||k||^2 / 2); rows of DP + 16 bytes, n_pad rows.
-static int ensure_i8(knn_ctx* ctx, hipStream_t s) {
+// The int8 image for kernel metrics 5 / 6 (knn_prep.hip): codes x 2^s - c of
+// every row (16-B chunks swizzled as the fp16 image for metric 5, plain for
+// metric 6) + the accumulator seeds -ceil(||k||^2 / 2); rows of DP + 16
+// bytes, n_pad rows.
+static int ensure_i8(knn_ctx* ctx, int kmetric, hipStream_t s) {
   const TrainDev& t = ctx->train;
-  const int DPi = pad_dim_i8(t.d);
+  const int DPi = kmetric == 6 ? pad_dim_i8w(t.d) : pad_dim_i8(t.d);
+  const int swz = kmetric == 6 ? 0 : 1;
   if (!ctx->i8_ok || DPi <= 0) return knn_fail(KNN_ERR_ARG, "train set not integer-coded (int8 pass)");
-  if (ctx->DPi == DPi) return KNN_OK;
+  if (ctx->DPi == DPi && ctx->i8_swz == swz) return KNN_OK;
   int rc;
   if ((rc = ctx->XI.ensure((size_t)t.n_pad * (DPi + 16) + 1024))) return rc;
   unsigned* cmax = (unsigned*)((unsigned long long*)ctx->stats.p + 3);
   HIP_TRY(hipMemsetAsync(cmax, 0, 8, s));
   launch_prep_i8_train(t.X64, (const double*)ctx->i8_cent.p, t.n, t.d, DPi, t.n_pad, ctx->i8_s,
-                       (signed char*)ctx->XI.p, cmax, s);
+                       (signed char*)ctx->XI.p, cmax, swz, s);
   HIP_TRY(hipGetLastError());
   unsigned cm = 0;
   HIP_TRY(hipMemcpyAsync(&cm, cmax, sizeof cm, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   ctx->i8_x2max = std::ldexp((double)cm, -2 * ctx->i8_s);
   ctx->DPi = DPi;
+  ctx->i8_swz = swz;
   return KNN_OK;
 }
 
@@ -400,7 +403,7 @@ static int ensure_sample(knn_ctx* ctx, int kmetric, int DP, int64_t ns, hipStrea
   HIP_TRY(hipMemsetAsync(ctx->smp_scr.p, 0, 16, s));
   if (kmetric == 5) {
     launch_prep_i8_train((const double*)ctx->smp_x64.p, (const double*)ctx->i8_cent.p, ns, d, DP, ns,
-                         ctx->i8_s, (signed char*)ctx->smp_img.p, (unsigned*)ctx->smp_scr.p, s);
+                         ctx->i8_s, (signed char*)ctx->smp_img.p, (unsigned*)ctx->smp_scr.p, 1, s);
   } else {
     // the fp16 image's seeds are the rows' fl32 ||x'||^2 of the main copy
     HIP_TRY(hipMemcpy2DAsync(ctx->smp_xl2.p, 4, t.xinit_l2, (size_t)stride * 4, 4, (size_t)ns,
@@ -445,6 +448,16 @@ static bool use_i8(const knn_ctx* ctx, int metric, int64_t m, int W) {
   if (ctx->tune_fp16 == 1) return false;
   if (ctx->precision != KNN_PRECISION_AUTO || ctx->i8_off) return false;
   return m >= 4096 && W <= kQuadMaxW;
+}
+
+// Which int8 kernel: metric 6 (v_mfma_i32_32x32x32_i8, K granularity 32)
+// where it issues fewer padded dims than metric 5 (16x16x64, K 64): d = 96
+// runs 96 dims instead of 128 (configs[3]).  Tuning key "i8w": -1 auto,
+// 0 always 16x16x64, 1 always 32x32x32.
+static int i8_kernel(const knn_ctx* ctx) {
+  const int d = ctx->train.d;
+  if (ctx->tune_i8w >= 0) return ctx->tune_i8w > 0 && pad_dim_i8w(d) > 0 ? 6 : 5;
+  return pad_dim_i8w(d) > 0 && pad_dim_i8w(d) < pad_dim_i8(d) ? 6 : 5;
 }
 
 static bool use_bf16x3(const knn_ctx* ctx, int metric) {
@@ -505,7 +518,8 @@ static void choose_geometry(knn_ctx* ctx, int metric, bool streamed, int DP, int
                             int64_t n_tiles, int W, int C, bool s3q, int& S_out, int& R_out) {
   int S_hi = (int)std::max<int64_t>(1, std::min<int64_t>(64, n_tiles));
   int bestS = 1, bestR = 8;
-  const bool quad = !streamed && metric >= 3;  // 16x16 layouts (bf16x3, fp16, int8)
+  const bool quad = !streamed && metric >= 3 && metric <= 5;  // 16x16 layouts (bf16x3, fp16, int8)
+  const bool pair4 = metric == 6;  // int8 on 32x32x32: 2 lists of R = 4 per split
   const int lps = quad || s3q ? 4 : 2;  // lists per query per split
   // S3 on 16x16x32 (s3q): R = 8 quad lists, 4 * S * 8 <= kMaxUnion entries
   if (s3q) S_hi = std::min(S_hi, kMaxUnion / (4 * 8));
@@ -515,7 +529,7 @@ static void choose_geometry(knn_ctx* ctx, int metric, bool streamed, int DP, int
     // only on request (resident kernel; tuning experiments)
     // (int8: R = 8 quad lists on request, tuning key "R")
     const bool q8 = quad && metric == 5 && ctx->tune_R == 8;
-    if (quad ? R != (q8 ? 8 : 4) : (ctx->tune_R ? R != ctx->tune_R : R == 4)) continue;
+    if (pair4 ? R != 4 : quad ? R != (q8 ? 8 : 4) : (ctx->tune_R ? R != ctx->tune_R : R == 4)) continue;
     if (R == 4 && (DP > 256 || metric == 1)) continue;
     const int64_t slots =
         (int64_t)(s3q ? s3q_blocks_per_cu() : cand_blocks_per_cu(metric, DP, R, nw)) * ctx->cu_count;
@@ -534,7 +548,7 @@ static void choose_geometry(knn_ctx* ctx, int metric, bool streamed, int DP, int
     if (q8) {
       S_lo = std::max(S_lo, W);  // an 8-entry list holding 8 of the top W: negligible
       S_hi = std::min(S_hi, kMaxUnion / (4 * 8));
-    } else if (quad) {
+    } else if (quad || pair4) {
       const int mult = n_qt >= 512 ? 4 : 2;
       S_lo = std::max(S_lo, std::max<int>(W, (int)std::min<int64_t>(mult * W, n_tiles / 32)));
     }
@@ -639,7 +653,7 @@ static void auto_check(knn_ctx* ctx) {
   // than 1/16 of its queries to the rescan (data whose neighbour gaps are
   // too fine for fp16 operands): later batches take bf16x3
   if ((int64_t)ctx->h_counts[0] * 16 > ctx->auto_m) {
-    if (ctx->auto_kind == 5) ctx->i8_off = true;
+    if (ctx->auto_kind >= 5) ctx->i8_off = true;
     else ctx->fp16_off = true;
   }
   ctx->auto_pending = false;
@@ -692,8 +706,8 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   const float* Xk = t.X32;
   bool s3h = false;  // fp16 on the S3 stream kernel (d > 256)
   if (use_i8(ctx, metric, m, W)) {
-    if ((rc = ensure_i8(ctx, s))) return rc;
-    kmetric = 5;
+    kmetric = i8_kernel(ctx);
+    if ((rc = ensure_i8(ctx, kmetric, s))) return rc;
     DP = ctx->DPi;
     Xk = (const float*)ctx->XI.p;
   } else if (use_fp16(ctx, metric, m, W)) {
@@ -729,7 +743,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   // queries per wave of the resident kernel (int8: 16 x the build's query
   // blocks); the int8 kernel with 64 queries per wave also runs 4 waves
   const int qpw = !s3 && DP <= 256 ? cand_queries_per_wave(kmetric, DP) : 32;
-  if (kmetric == 5 && ctx->tune_nw) nw = ctx->tune_nw;  // 4 or 8 (int8 builds have both)
+  if (kmetric == 5 && ctx->tune_nw) nw = ctx->tune_nw;  // 4 or 8 (16x16x64 builds have both)
   if (s3) nw = 8;
   const int qpb = s3 ? kS3Rows : (DP <= 256 ? qpw * nw : kQPB);
   const int n_qt = (int)((m + qpb - 1) / qpb);
@@ -749,8 +763,9 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   const bool s3q = s3h && ctx->tune_s3q != 0 && s3q_S <= kMaxUnion / 32 && s3q_S <= n_tiles;
   choose_geometry(ctx, kmetric, s3, DP, nw, n_qt, n_tiles, W, C, s3q, S, R);
   // 16x16 layouts: 4 lists per query per split
-  const bool quad_lists = (!s3 && kmetric >= 3) || s3q;
+  const bool quad_lists = (!s3 && kmetric >= 3 && kmetric <= 5) || s3q;
   if (quad_lists && !s3q && !(kmetric == 5 && R == 8)) R = 4;
+  if (kmetric == 6) R = 4;  // (2 lists per query per split, pair_min filter)
   const int NL = (quad_lists ? 4 : 2) * S;
   C = std::min(C, NL * R);
   // rescan workspace: the fast path serves the first `cap` failed queries
@@ -811,9 +826,9 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   const double qscale = metric == KNN_METRIC_L2 ? -2.0 : 1.0;
   float* qvalid = (float*)ctx->qvalid.p;
   launch_query_check(dQ, t.mu, m, t.d, m_pad, qscale, t.jx,
-                     kmetric == 5 ? DBL_MAX : kmetric == 4 ? 65000.0 : std::ldexp(1.0, 100), qvalid,
+                     kmetric >= 5 ? DBL_MAX : kmetric == 4 ? 65000.0 : std::ldexp(1.0, 100), qvalid,
                      s);
-  if (kmetric == 5)  // codes of the train set's grid; a query off it: valid 0 (rescan)
+  if (kmetric >= 5)  // codes of the train set's grid; a query off it: valid 0 (rescan)
     launch_prep_i8_queries(dQ, (const double*)ctx->i8_cent.p, m, t.d, DP, m_pad, ctx->i8_s,
                            (signed char*)ctx->Q32.p, qvalid, s);
   else if (s3h)
@@ -848,7 +863,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   cl.qpb = qpb;
   cl.gthr = use_gthr ? (uint32_t*)ctx->gthr.p : nullptr;
   cl.gk = gk;
-  cl.xsw = kmetric == 5 ? 1 : ctx->xh_swz;  // the int8 image is always swizzled
+  cl.xsw = kmetric >= 5 ? ctx->i8_swz : ctx->xh_swz;
   // slots of groups without a split stay 0 (never the max)
   // (experiment, tuning "ablate" bit 5: keep the previous call's final
   // thresholds -- valid only for a repeat of the same queries; measures what
@@ -903,7 +918,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   sm.mask = (unsigned long long*)ctx->rescan_mask.p;
   sm.nkeep = (int*)ctx->rescan_nkeep.p;
   sm.keep = (int*)ctx->fr_buf.p;
-  if (kmetric == 5) {
+  if (kmetric >= 5) {
     // int8 proxies are exact up to +1 (the odd-norm half of the seed): the
     // merge sees the pass's own centre and scale (codes (x - cent/2^s) 2^s),
     // an absolute error of one code unit (DP x up / DP) and each query's
@@ -965,7 +980,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   // (a later fp16 call re-arms it with its own count)
   ctx->auto_pending = !abl && ((kmetric == 4 && ctx->precision == KNN_PRECISION_AUTO &&
                                 ctx->tune_fp16 < 0) ||
-                               (kmetric == 5 && ctx->tune_i8 < 0));
+                               (kmetric >= 5 && ctx->tune_i8 < 0));
   ctx->auto_kind = kmetric;
   ctx->auto_m = m;
   return KNN_OK;
@@ -1345,6 +1360,9 @@ int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value) {
   } else if (!strcmp(key, "i8")) {
     if (value < -1 || value > 1) return knn_fail(KNN_ERR_ARG, "i8 must be -1, 0 or 1");
     ctx->tune_i8 = (int)value;
+  } else if (!strcmp(key, "i8w")) {
+    if (value < -1 || value > 1) return knn_fail(KNN_ERR_ARG, "i8w must be -1, 0 or 1");
+    ctx->tune_i8w = (int)value;
   } else if (!strcmp(key, "seed")) {
     if (value < -1) return knn_fail(KNN_ERR_ARG, "seed must be 0 / -1 (off) or N = sample rows");
     ctx->tune_seed = value;

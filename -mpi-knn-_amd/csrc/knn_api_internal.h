@@ -43,6 +43,7 @@ struct knn_ctx {
   bool i8_ok = false;
   int i8_s = 0;
   int DPi = 0;           // padded dim of the int8 image (0 = not built)
+  int i8_swz = 1;        // the int8 image's chunks are swizzled (16x16x64 kernel; 0: 32x32x32)
   double i8_x2max = 0.0; // max ||k||^2 / 2^(2 s) of the image
   bool i8_off = false;   // AUTO: int8 pass retired for this train set
   int auto_kind = 0;     // the pass the pending AUTO decision is about (4 fp16, 5 int8)
@@ -61,6 +62,7 @@ struct knn_ctx {
   int tune_xhswz = 1;          // fp16 train image chunk swizzle (xh_swz): 1 on, 0 off (A/B)
   int tune_fp16 = -1;          // fp16 candidate pass: -1 auto, 0 off, 1 on
   int tune_i8 = -1;            // int8 candidate pass: -1 auto, 0 off, 1 on (where the data allow)
+  int tune_i8w = -1;           // int8 on 32x32x32 (metric 6): -1 auto (where it pads less), 0 off, 1 on
   int tune_ties = 1;           // reference tie order: 0 off, 1 vote-affecting ties, 2 all ties
   int tune_m16 = -1;           // bf16x3 on the 16x16x32 MFMA layout: -1 auto, 0 off, 1 on
   int64_t tune_seed = 0;       // seeded thresholds: 0 / -1 off, N sample rows (experiment)

@@ -591,6 +591,14 @@ int pad_dim_i8(int d) {
   return DP <= 256 ? DP : -1;
 }
 
+// int8 on the 32x32x32 kernel (metric 6): the smallest resident DP >= d
+// that is a multiple of 32 (d = 96 -> 96, where 16x16x64 pads to 128)
+int pad_dim_i8w(int d) {
+  for (int DP : {32, 64, 96, 128, 160, 192, 256})
+    if (DP >= d) return DP;
+  return -1;
+}
+
 // fp16 S3 kernel above 256 dims: any multiple of 32
 int pad_dim_fp16_s3(int d) {
   const int DP = (d + 31) / 32 * 32;

@@ -67,10 +67,6 @@ static_assert(KNN_RES_TPB * knnk::kTR == knnk::kResTileRows || KNN_RES_TPB != 2,
 #ifndef KNN_I8_QB
 #define KNN_I8_QB 2
 #endif
-// int8 kernel: LDS fragments of the next sub-tile read ahead (see cand_kernel)
-#ifndef KNN_I8_PF
-#define KNN_I8_PF 0
-#endif
 #ifndef KNN_I8_WPE
 #define KNN_I8_WPE 2
 #endif
@@ -118,7 +114,7 @@ __device__ __forceinline__ bool exchange_tile(int it) {
 template <int DP, int R, int METRIC>
 constexpr int res_wpe() {
   if (METRIC == 5 && KNN_I8_QB > 2) return KNN_I8_WPE;
-  return (METRIC == 5 ? DP / 4 : METRIC == 4 ? DP / 2 : DP) <= 160 && R <= 8 ? 4 : 1;
+  return (METRIC >= 5 ? DP / 4 : METRIC == 4 ? DP / 2 : DP) <= 160 && R <= 8 ? 4 : 1;
 }
 
 // queries per wave: 16 per query block (the 16x16 layouts), 32 otherwise
@@ -129,7 +125,7 @@ constexpr int res_qpw() {
 
 template <int METRIC>
 constexpr int res_tpb() {
-  return METRIC == 5 ? KNN_I8_TPB : METRIC == 4 ? KNN_M4_TPB : KNN_RES_TPB;
+  return METRIC >= 5 ? KNN_I8_TPB : METRIC == 4 ? KNN_M4_TPB : KNN_RES_TPB;
 }
 
 // Train rows in HBM (X32 for fp32/L1, XB for bf16x3) share one padded row
@@ -189,13 +185,19 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   // v_mfma_i32_16x16x64_i8, the same fragment layout with 64 dims per MFMA
   constexpr bool F16 = METRIC == 4;
   constexpr bool I8 = METRIC == 5;
-  constexpr bool TEC = (F16 || I8) && KNN_M4_TE_CACHE;
-  constexpr int DPF = I8 ? DP / 4 : (F16 ? DP / 2 : DP);  // payload floats per row
+  // int8 codes on v_mfma_i32_32x32x32_i8 (METRIC 6): the 32x32 layout of
+  // METRIC 0 (lane (j, h): query j, rows (i&3) + 8(i>>2) + 4h) with 32 dims
+  // per MFMA, so d = 96, 160, 224 issue no padded dims (16x16x64 pads them
+  // to a multiple of 64)
+  constexpr bool I8W = METRIC == 6;
+  constexpr bool I8A = I8 || I8W;  // either int8 form: int accumulators, seeds, int lists
+  constexpr bool TEC = (F16 || I8A) && KNN_M4_TE_CACHE;
+  constexpr int DPF = I8A ? DP / 4 : (F16 ? DP / 2 : DP);  // payload floats per row
   constexpr int RSF = DPF + 4;              // row stride (floats), HBM and LDS
   constexpr int TPB = res_tpb<METRIC>();    // 32-row sub-tiles per staged tile
   constexpr int TBY = kTR * TPB * RSF * 4;  // tile bytes
   constexpr int NG = (TBY + 1023) / 1024;   // 1-KiB LDS-DMA pieces per tile
-  constexpr int NB = I8 ? KNN_I8_NB : KNN_RES_NB;  // LDS buffers (prefetch distance NB - 1)
+  constexpr int NB = I8A ? KNN_I8_NB : KNN_RES_NB;  // LDS buffers (prefetch distance NB - 1)
   constexpr int BUFF = NG * 256;            // floats per buffer
   constexpr int SEED = METRIC == 1 ? DP + 1 : DPF;  // seed float within a row
   __shared__ __attribute__((aligned(16))) float lds[NB * BUFF];
@@ -225,7 +227,8 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   // METRIC 4: fp16 -2q (the train set's power-of-two scale), float4 qb*(DP/32)+ks
   // = dims 32ks + 8*g16 .. +7 of query block qb.
   // METRIC 5: int8 codes, float4 qb*(DP/64)+ks = dims 64ks + 16*g16 .. +15
-  constexpr int NQF = METRIC == 1 ? 1 : (I8 ? QB * DP / 64 : (F16 ? QB * DP / 32 : DP / 8));
+  // METRIC 6: int8 codes, float4 ks = dims 32ks + 16h .. +15 of query j
+  constexpr int NQF = METRIC == 1 ? 1 : I8W ? DP / 32 : (I8 ? QB * DP / 64 : (F16 ? QB * DP / 32 : DP / 8));
   float4 qf[NQF];
   if constexpr (METRIC != 1) {
     // Loaded with inline asm (loads + their vmcnt(0) in one statement): with
@@ -239,7 +242,9 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int c = c0 + u < NQF ? c0 + u : c0;
-        if constexpr (I8) {
+        if constexpr (I8W) {
+          p[u] = Q32 + qg * (DP / 4) + 8 * c + 4 * h;
+        } else if constexpr (I8) {
           const int ks = c % (DP / 64), qb = c / (DP / 64);
           p[u] = Q32 + (qb0 + 16 * qb) * (DP / 4) + 16 * ks + 4 * g16;
         } else if constexpr (F16) {
@@ -273,7 +278,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
 
   constexpr int NQL = M16 ? QB : 1;  // queries (lists) per lane
   // int8: lists of the accumulators themselves (KNN_I8_ILIST, knn_device.h)
-  constexpr bool ILIST = I8 && KNN_I8_ILIST;
+  constexpr bool ILIST = I8A && KNN_I8_ILIST;
   using LT = std::conditional_t<ILIST, int, float>;
   LT L[NQL][R];
   int I[NQL][R];
@@ -344,7 +349,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
 
   const int my_nt = split < n_tiles ? (n_tiles - split + S - 1) / S : 0;
   constexpr bool PIPE = TEC && KNN_M4_PIPE && DP <= 192;  // DP 256: no registers to spare
-  using AccT = std::conditional_t<I8, i32x4, f32x4>;
+  using AccT = std::conditional_t<I8A, i32x4, f32x4>;
   // PIPE: the previous sub-tile's accumulators; before the first sub-tile
   // they hold values no filter passes (int8: kI8Floor, fp16: +inf), so the
   // pipelined selection needs no first-sub-tile check
@@ -353,9 +358,15 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
     for (int qb = 0; qb < QB; ++qb) {
-      if constexpr (I8) accp[rb][qb] = i32x4{kI8Floor, kI8Floor, kI8Floor, kI8Floor};
+      if constexpr (I8A) accp[rb][qb] = i32x4{kI8Floor, kI8Floor, kI8Floor, kI8Floor};
       else accp[rb][qb] = f32x4{KNN_INF_F, KNN_INF_F, KNN_INF_F, KNN_INF_F};
     }
+  // METRIC 6: the previous sub-tile's 32x32 accumulators
+  i32x16 accw;
+  if constexpr (I8W) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) accw[i] = kI8Floor;
+  }
   int rowp = 0;
   SelCount selc;
 
@@ -514,38 +525,54 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       // larger value only admits more insertions)
 #pragma unroll
       for (int b = 0; b < NQL; ++b) {
-        te[b] = __builtin_fminf(quad_min(thr[b]), tq[b]);
-        if constexpr (I8) tn[b] = i8_neg_half(te[b]);
+        te[b] = __builtin_fminf(I8W ? pair_min(thr[b]) : quad_min(thr[b]), tq[b]);
+        if constexpr (I8A) tn[b] = i8_neg_half(te[b]);
       }
     }
-    // int8: the LDS fragments (seeds and A) of a sub-tile; with KNN_I8_PF
-    // those of sub-tile s+1 are read before the MFMAs of s are issued, so
-    // their latency hides behind s's MFMAs (sub-tile 0 of a tile reads its
-    // own after the barrier)
-    constexpr bool I8PF = I8 && KNN_I8_PF;
-    i32x4 pf_sd[2], pf_af[I8 ? DP / 64 : 1][2];
-    const int g16s = g16 ^ (xsw ? xh_swz(c16) : 0);
-    auto i8_seeds = [&](const float* b, i32x4 (&sd)[2]) {
-#pragma unroll
-      for (int rb = 0; rb < 2; ++rb)
-        sd[rb] = __builtin_bit_cast(i32x4, *(const float4*)(b + (rb * 16 + 4 * g16) * RSF + SEED));
-    };
-    auto i8_frags = [&](const float* b, i32x4 (&sd)[2], i32x4 (&af)[I8 ? DP / 64 : 1][2]) {
-      // (KNN_I8_PF = 2: the seeds are read with their own sub-tile)
-      if (KNN_I8_PF != 2) i8_seeds(b, sd);
-#pragma unroll
-      for (int ks = 0; ks < (I8 ? DP / 64 : 1); ++ks)
-#pragma unroll
-        for (int rb = 0; rb < 2; ++rb)
-          af[ks][rb] = __builtin_bit_cast(
-              i32x4, *(const float4*)(b + (rb * 16 + c16) * RSF + 16 * ks + 4 * g16s));
-    };
-    if constexpr (I8PF) i8_frags(lds + cur * BUFF, pf_sd, pf_af);
 #pragma unroll
     for (int sub = 0; sub < TPB; ++sub) {
     const float* base = lds + cur * BUFF + sub * kTR * RSF;
 
-    if constexpr (I8) {
+    if constexpr (I8W) {
+      // int8 codes on v_mfma_i32_32x32x32_i8, exact: lane (j, h) holds query
+      // j against rows (i&3) + 8(i>>2) + 4h; the accumulators start at the
+      // rows' seeds -ceil(||k||^2 / 2) (the pad of row 4g carries rows 4g ..
+      // 4g+3: groups 2c + h, c = i >> 2) and end at q.k - ceil(||k||^2 / 2)
+      i32x16 acc;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const i32x4 sd = __builtin_bit_cast(i32x4, *(const float4*)(base + (8 * c + 4 * h) * RSF + SEED));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[4 * c + e] = sd[e];
+      }
+      // A fragment of k-step ks: row j, dims 32ks + 16h .. +15 (the image of
+      // this kernel is not chunk-swizzled: the 32x32 reads are conflict-free)
+      i32x4 af[DP / 32];
+#pragma unroll
+      for (int ks = 0; ks < DP / 32; ++ks)
+        af[ks] = __builtin_bit_cast(i32x4, *(const float4*)(base + j * RSF + 8 * ks + 4 * h));
+#if KNN_I8_SCHED
+      __builtin_amdgcn_sched_barrier(0);
+#endif
+#pragma unroll
+      for (int ks = 0; ks < DP / 32; ++ks)
+        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[ks], __builtin_bit_cast(i32x4, qf[ks]), acc,
+                                                    0, 0, 0);
+      const int row0 = (t * TPB + sub) * kTR + 4 * h;
+      if constexpr (PIPE) {
+        if (!(abl & 2)) {
+          select_block_i8<R>(accw, rowp, L[0], I[0], tn[0], selc);
+          accw = acc;
+          rowp = row0;
+        } else if (acc[0] == 12345 && acc[15] == 12345) {
+          thr[0] = (float)acc[7];  // keep the accumulators live
+        }
+      } else if (!(abl & 2)) {
+        select_block_i8<R>(acc, row0, L[0], I[0], tn[0], selc);
+      } else if (acc[0] == 12345 && acc[15] == 12345) {
+        thr[0] = (float)acc[7];
+      }
+    } else if constexpr (I8) {
       // int8 codes on v_mfma_i32_16x16x64_i8, exact: the accumulators start
       // at -ceil(||k||^2 / 2) (the pad of row 4g carries rows 4g .. 4g+3)
       // and end at q.k - ceil(||k||^2 / 2); one MFMA per 64 dims
@@ -553,27 +580,21 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       // MFMAs, fenced (KNN_I8_SCHED): the registers are there (the query
       // image is half the fp16 one), and the compiler's own schedule would
       // wait on each read just before its two MFMAs
-      i32x4 sdv[2], af[DP / 64][2];
-      if constexpr (I8PF) {
-        if constexpr (KNN_I8_PF == 2) {
-          i8_seeds(base, sdv);
-        } else {
-#pragma unroll
-          for (int rb = 0; rb < 2; ++rb) sdv[rb] = pf_sd[rb];
-        }
-#pragma unroll
-        for (int ks = 0; ks < DP / 64; ++ks)
-#pragma unroll
-          for (int rb = 0; rb < 2; ++rb) af[ks][rb] = pf_af[ks][rb];
-        if (sub + 1 < TPB) i8_frags(base + kTR * RSF, pf_sd, pf_af);
-      } else {
-        i8_frags(base, sdv, af);
-      }
       i32x4 acc[2][QB];
 #pragma unroll
-      for (int rb = 0; rb < 2; ++rb)
+      for (int rb = 0; rb < 2; ++rb) {
+        const i32x4 sd = __builtin_bit_cast(i32x4, *(const float4*)(base + (rb * 16 + 4 * g16) * RSF + SEED));
 #pragma unroll
-        for (int qb = 0; qb < QB; ++qb) acc[rb][qb] = sdv[rb];
+        for (int qb = 0; qb < QB; ++qb) acc[rb][qb] = sd;
+      }
+      const int g16s = g16 ^ (xsw ? xh_swz(c16) : 0);
+      i32x4 af[DP / 64][2];
+#pragma unroll
+      for (int ks = 0; ks < DP / 64; ++ks)
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+          af[ks][rb] = __builtin_bit_cast(
+              i32x4, *(const float4*)(base + (rb * 16 + c16) * RSF + 16 * ks + 4 * g16s));
 #if KNN_I8_SCHED
       __builtin_amdgcn_sched_barrier(0);
 #endif
@@ -763,7 +784,9 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
 
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if constexpr (PIPE) {
+  if constexpr (PIPE && I8W) {
+    if (!(abl & 2)) select_block_i8<R>(accw, rowp, L[0], I[0], tn[0], selc);
+  } else if constexpr (PIPE) {
     if (!(abl & 2)) {
 #pragma unroll
       for (int qb = 0; qb < QB; ++qb) {
@@ -776,7 +799,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   }
 
 #if KNN_COUNT_SEL
-  if constexpr (I8) {
+  if constexpr (I8A) {
     atomicAdd(&knn_sel_cnt[0], (unsigned long long)selc.calls);
     atomicAdd(&knn_sel_cnt[1], (unsigned long long)selc.lane_pass);
     if (lane == 0) atomicAdd(&knn_sel_cnt[2], (unsigned long long)selc.wave_pass);
@@ -795,6 +818,11 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
         *(int4*)(out_i + o + t) = make_int4(I[qb][t], I[qb][t + 1], I[qb][t + 2], I[qb][t + 3]);
       }
     }
+  } else if constexpr (ILIST) {
+    float Lf[R];
+#pragma unroll
+    for (int t = 0; t < R; ++t) Lf[t] = lval(L[0][t]);
+    write_lists<R>(out_v, out_i, qg, S, split, h, Lf, I[0]);
   } else {
     write_lists<R>(out_v, out_i, qg, S, split, h, L[0], I[0]);
   }
@@ -817,7 +845,8 @@ static void with_M(int M, F f) {
   else if (M == 2) f(std::integral_constant<int, 2>{});
   else if (M == 3) f(std::integral_constant<int, 3>{});
   else if (M == 4) f(std::integral_constant<int, 4>{});
-  else f(std::integral_constant<int, 5>{});
+  else if (M == 5) f(std::integral_constant<int, 5>{});
+  else f(std::integral_constant<int, 6>{});
 }
 
 template <int DP, int R, int METRIC, int NW>
@@ -837,7 +866,7 @@ template <int DP, int R, int M, int NW>
 constexpr bool res_variant() {
   return (M != 2 || DP % 16 == 0) && (M != 1 || (NW == 4 && R != 4)) &&
          (M < 3 || (DP % 32 == 0 && (R == 4 || (M == 5 && R == 8)) && (NW == 8 || M >= 4))) && (NW != 16 || M == 4) &&
-         (M != 5 || (DP % 64 == 0 && (NW == 8 || NW == 4)));
+         (M != 5 || (DP % 64 == 0 && (NW == 8 || NW == 4))) && (M != 6 || (NW == 8 && R == 4));
 }
 
 template <int DP>
@@ -900,7 +929,7 @@ static bool launch_res_dp(const CandLaunch& c, hipStream_t s) {
   int blocks_res_##v(int R, int metric, int nw) { return blocks_per_cu_res<v>(R, metric, nw); } \
   int qpw_res_##v(int metric) { return metric == 5 ? res_qpw<5>() : res_qpw<0>(); } \
   int trows_res_##v(int metric) {                                                        \
-    return kTR * (metric == 5 ? res_tpb<5>() : metric == 4 ? res_tpb<4>() : res_tpb<0>()); \
+    return kTR * (metric >= 5 ? res_tpb<5>() : metric == 4 ? res_tpb<4>() : res_tpb<0>()); \
   }
 KNN_GROUP_DPS(KNN_DEF)
 #undef KNN_DEF

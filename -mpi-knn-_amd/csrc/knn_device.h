@@ -566,6 +566,49 @@ __device__ __forceinline__ void select_quad_i8i(const i32x4& a, const i32x4& b, 
   }
 }
 
+// METRIC 6 (v_mfma_i32_32x32x32_i8, the 32x32 layout): lane (j, h) holds
+// query j against rows row0 + (i&3) + 8(i>>2), i = 0..15 (row0 includes 4h),
+// one list per lane; lanes l and l^32 share the query (pair_min of their
+// thresholds is the per-tile filter).  The no-candidate test is a max over
+// 16 values; a slow call loops over the half (8 values) that has a pass.
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ float pair_min(float x) {
+  const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false,
+                                                   false);
+  return __builtin_fminf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+}
+template <int R>
+__device__ __forceinline__ void select_block_i8(const i32x16& a, int row0, int (&L)[R], int (&I)[R],
+                                                int& tn, SelCount& sc) {
+  const int h0 = max(max(max(a[0], a[1]), max(a[2], a[3])), max(max(a[4], a[5]), max(a[6], a[7])));
+  const int h1 = max(max(max(a[8], a[9]), max(a[10], a[11])),
+                     max(max(a[12], a[13]), max(a[14], a[15])));
+#if KNN_COUNT_SEL
+  sc.calls++;
+  sc.lane_pass += max(h0, h1) > tn;
+  sc.wave_pass += __builtin_amdgcn_ballot_w64(max(h0, h1) > tn) != 0;
+#endif
+  if (__builtin_amdgcn_ballot_w64(max(h0, h1) > tn)) {
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      if (__builtin_amdgcn_ballot_w64((half ? h1 : h0) > tn)) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int i = 8 * half + e;
+          const int v = a[i];
+          if (v > tn) {
+#if KNN_COUNT_SEL
+            sc.inserts++;
+#endif
+            list_insert_desc<R>(L, I, v, row_at(row0, (i & 3) + 8 * (i >> 2)));
+            tn = max(tn, L[R - 1]);
+          }
+        }
+      }
+    }
+  }
+}
+
 // KNN_I8_SLOW = 2: the slow path inserts each lane's best passing value
 // first, found with its position by a max over keys acc * 8 + position
 // (exact and order-preserving: acc >= kI8Floor = -2^23), and tests the lane's second

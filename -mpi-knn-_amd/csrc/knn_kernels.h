@@ -96,7 +96,8 @@ int cand_blocks_per_cu(int metric, int DP, int R, int nw);  // resident workgrou
 int cand_queries_per_wave(int metric, int DP);  // resident kernel: queries per wave
 
 // metric: 0 = L2 fp32 MFMA, 1 = L1 fp32 VALU, 2 = L2 bf16x3 MFMA (32x32x16),
-// 3 = L2 bf16x3 on 16x16x32, 4 = L2 fp16 on 16x16x32 (see knn_cand_res.hip)
+// 3 = L2 bf16x3 on 16x16x32, 4 = L2 fp16 on 16x16x32, 5 = L2 int8 on
+// 16x16x64, 6 = L2 int8 on 32x32x32 (see knn_cand_res.hip)
 struct CandLaunch {
   int metric, DP, R, S, n_qt;
   int64_t n_pad;
@@ -258,12 +259,15 @@ void launch_fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t s);
 // train values; partial holds col_mean_blocks(n) x 2d doubles.
 void launch_grid_stats(const double* X64, int64_t n, int d, double* partial, double* out,
                        unsigned* frac, hipStream_t s);
+// swz: 16-B chunks at ch ^ xh_swz(row) (the 16x16x64 kernel's image); 0 for
+// the 32x32x32 kernel's (its reads are conflict-free unswizzled)
 void launch_prep_i8_train(const double* X64, const double* cent, int64_t n, int d, int DP,
-                          int64_t n_pad, int s, signed char* out, unsigned* codes_max,
+                          int64_t n_pad, int s, signed char* out, unsigned* codes_max, int swz,
                           hipStream_t st);
 void launch_prep_i8_queries(const double* Q64, const double* cent, int64_t m, int d, int DP,
                             int64_t m_pad, int s, signed char* out, float* valid, hipStream_t st);
 int pad_dim_i8(int d);  // padded dim of the int8 kernel (a multiple of 64, <= 256), -1 if none
+int pad_dim_i8w(int d); // padded dim of the int8 32x32x32 kernel (metric 6), -1 if none
 // The reference's exact neighbour order on exact distance ties (knn_select.hip,
 // "reference tie order"): libstdc++ std::sort (introsort) emulated over all
 // n exact distances of each listed query, restricted to the ranges that

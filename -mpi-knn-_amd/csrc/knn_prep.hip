@@ -415,14 +415,14 @@ void launch_grid_stats(const double* X64, int64_t n, int d, double* partial, dou
 __global__ void __launch_bounds__(256)
 prep_i8_train_kernel(const double* __restrict__ X64, const double* __restrict__ cent, int64_t n,
                      int d, int DP, int64_t n_pad, int s, signed char* __restrict__ out,
-                     unsigned* __restrict__ codes_max) {
+                     unsigned* __restrict__ codes_max, int swz) {
   const int row_bytes = DP + 16;
   const int lane = threadIdx.x & 63;
   const int64_t wstride = (int64_t)gridDim.x * 4;
   unsigned mx = 0;
   for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n_pad; row += wstride) {
     int q2 = 0;
-    const int cx = xh_swz((int)(row & 15)) << 4;
+    const int cx = swz ? xh_swz((int)(row & 15)) << 4 : 0;
     for (int c = lane; c < DP; c += 64) {
       int k = 0;
       if (row < n && c < d) {
@@ -442,12 +442,12 @@ prep_i8_train_kernel(const double* __restrict__ X64, const double* __restrict__ 
 }
 
 void launch_prep_i8_train(const double* X64, const double* cent, int64_t n, int d, int DP,
-                          int64_t n_pad, int s, signed char* out, unsigned* codes_max,
+                          int64_t n_pad, int s, signed char* out, unsigned* codes_max, int swz,
                           hipStream_t st) {
   int64_t blocks = (n_pad + 3) / 4;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(prep_i8_train_kernel, dim3((unsigned)blocks), dim3(256), 0, st, X64, cent, n,
-                     d, DP, n_pad, s, out, codes_max);
+                     d, DP, n_pad, s, out, codes_max, swz);
 }
 
 // Query rows: int8 codes clamp(rint(q 2^s - c_i), -128, 127) (DP bytes,

@@ -95,7 +95,8 @@ def test_cfg4_100m_train_sharded(knn):
         c.sync()
         paths.append(c.last_candidate_path())
         c.close()
-    assert paths == [5, 4] * (parts // 2), "shards should run int8 (AUTO, grid data) / fp16 (forced)"
+    # d = 96: the int8 pass on 32x32x32 (metric 6, no padded dims)
+    assert paths == [6, 4] * (parts // 2), "shards should run int8 (AUTO, grid data) / fp16 (forced)"
     ol = torch.empty(m, dtype=torch.int32, device=DEV)
     oi = torch.empty((m, k), dtype=torch.int64, device=DEV)
     od = torch.empty((m, k), dtype=torch.float64, device=DEV)

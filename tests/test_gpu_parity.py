@@ -34,7 +34,7 @@ def knn():
     return mod
 
 
-@pytest.fixture(scope="module", params=["auto", "fp32", "m16", "fp16", "fp16w", "i8"])
+@pytest.fixture(scope="module", params=["auto", "fp32", "m16", "fp16", "fp16w", "i8", "i8w"])
 def clf(knn, request):
     """Every parity test runs with the default candidate path (AUTO: int8 for
     integer-coded data and fp16 otherwise for batches of >= 4096 queries at
@@ -43,14 +43,18 @@ def clf(knn, request):
     (every batch size), with the fp16 path's alternative forms (fp16w: the S3
     kernel on 32x32x16 above 256 dims, the resident kernel publishing list
     thresholds, gk = 0), and with the int8 path forced wherever the data are
-    integer-coded (i8; other data take the AUTO path)."""
+    integer-coded, on its AUTO kernel (i8) and on v_mfma_i32_32x32x32_i8 at
+    every width (i8w); other data take the AUTO path."""
     c = knn.Classifier(0)
     c.set_precision({"auto": knn.PRECISION_AUTO, "fp32": knn.PRECISION_FP32,
                      "m16": knn.PRECISION_BF16X3, "fp16": knn.PRECISION_FP16,
-                     "fp16w": knn.PRECISION_FP16, "i8": knn.PRECISION_AUTO}[request.param])
+                     "fp16w": knn.PRECISION_FP16, "i8": knn.PRECISION_AUTO,
+                     "i8w": knn.PRECISION_AUTO}[request.param])
     c.set_tuning("mfma16", 1 if request.param == "m16" else -1)
-    if request.param == "i8":
+    if request.param in ("i8", "i8w"):
         c.set_tuning("i8", 1)
+    if request.param == "i8w":
+        c.set_tuning("i8w", 1)
     if request.param == "fp16w":
         c.set_tuning("s3q", 0)
         c.set_tuning("gk", 0)
@@ -268,22 +272,38 @@ def _grid_codes(rng, n, m, d, classes, lo=0, hi=255, scale=256.0):
     return X[:n].copy(), lab[:n].copy(), X[n:].copy()
 
 
+def _i8_kernel(d, i8w):
+    """(kernel metric, padded dim) the int8 pass runs at: 32x32x32 (metric 6,
+    K granularity 32) where it pads less than 16x16x64 (metric 5, K 64), or
+    as forced by the "i8w" tuning key."""
+    w = min(p for p in (32, 64, 96, 128, 160, 192, 256) if p >= d)
+    q = (d + 63) // 64 * 64
+    if i8w == 1 or (i8w < 0 and w < q):
+        return 6, w
+    return 5, q
+
+
 @pytest.mark.parametrize("d", [32, 64, 96, 128, 200, 256])
-def test_int8_codes(knn, d):
-    """The int8 pass (v_mfma_i32_16x16x64_i8 on the data's integer codes,
-    exact) against the oracle on 8-bit grid data -- the full byte range
-    (codes 0..255, centre 128) -- forced and in AUTO at 4096+ queries; every
-    padded width (d = 96 and 200 pad to 128 / 256)."""
+@pytest.mark.parametrize("i8w", [-1, 0, 1])
+def test_int8_codes(knn, d, i8w):
+    """The int8 pass (exact integer dot products of the data's codes) against
+    the oracle on 8-bit grid data -- the full byte range (codes 0..255, centre
+    128) -- forced and in AUTO at 4096+ queries, on both kernels:
+    v_mfma_i32_16x16x64_i8 (metric 5, dims padded to 64) and
+    v_mfma_i32_32x32x32_i8 (metric 6, dims padded to 32: AUTO's choice at
+    d = 32 and 96); every padded width (d = 200 pads to 256)."""
     rng = np.random.default_rng(80 + d)
     tr, lab, te = _grid_codes(rng, 9000, 4200, d, 7)
     assert tr.min() == 0.0 and tr.max() == 255 / 256.0
+    km, dp = _i8_kernel(d, i8w)
     for mode in ("forced", "auto"):
         c = knn.Classifier(0)
+        c.set_tuning("i8w", i8w)
         if mode == "forced":
             c.set_tuning("i8", 1)
         run_case(c, knn, tr, lab, te, 10, 0, 7)
-        assert c.last_candidate_path() == 5, mode
-        assert c.last_kernel_name().startswith("cand_kernel<%d,4,5,8>" % ((d + 63) // 64 * 64))
+        assert c.last_candidate_path() == km, mode
+        assert c.last_kernel_name().startswith("cand_kernel<%d,4,%d,8>" % (dp, km))
         assert c.last_rescan_count() * 16 <= te.shape[0]
         c.close()
 
@@ -312,7 +332,7 @@ def test_int8_off_grid_queries(knn):
     c.close()
 
 
-@pytest.mark.parametrize("path", ["i8", "fp16", "s3"])
+@pytest.mark.parametrize("path", ["i8", "i8w", "fp16", "s3"])
 def test_targeted_rescan(knn, path):
     """Per-split certification: with few splits (tuning S = 2, 3) a lane list
     often holds R of a query's top W, so its bound fails; the merge then
@@ -321,8 +341,8 @@ def test_targeted_rescan(knn, path):
     rows (knn_select.hip).  Exact answers against the oracle on the int8
     (grid data), fp16 (continuous data) and fp16 S3 (d = 300) paths."""
     rng = np.random.default_rng(123)
-    if path == "i8":
-        tr, lab, te = _grid_codes(rng, 20000, 600, 64, 6)
+    if path in ("i8", "i8w"):
+        tr, lab, te = _grid_codes(rng, 20000, 600, 64 if path == "i8" else 96, 6)
         k = 10
     else:
         d = 300 if path == "s3" else 64
@@ -334,13 +354,13 @@ def test_targeted_rescan(knn, path):
     rescans = 0
     for S in (2, 3):
         c = knn.Classifier(0)
-        if path == "i8":
+        if path in ("i8", "i8w"):
             c.set_tuning("i8", 1)
         else:
             c.set_precision(knn.PRECISION_FP16)
         c.set_tuning("S", S)
         run_case(c, knn, tr, lab, te, k, 0, 6)
-        assert c.last_candidate_path() == (5 if path == "i8" else 4)
+        assert c.last_candidate_path() == {"i8": 5, "i8w": 6}.get(path, 4)
         assert c.last_geometry()["splits"] == S
         rescans += c.last_rescan_count()
         c.close()

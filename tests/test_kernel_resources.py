@@ -63,7 +63,7 @@ def test_hot_kernels_use_no_scratch(tmp_path):
     every S3 kernel, the merge and the rescan kernels -- use no scratch."""
     meta = kernel_metadata(str(tmp_path))
     hot = {k: v for k, v in meta.items()
-           if re.search(r"cand_kernelILi\d+ELi\d+ELi[45]E", k)
+           if re.search(r"cand_kernelILi\d+ELi\d+ELi[456]E", k)
            or any(s in k for s in ("cand_s3_kernel", "merge_rerank", "rescan"))}
     assert len(hot) > 15, "expected the candidate / merge / rescan kernels in the code objects"
     spilled = sorted(k for k, v in hot.items() if v.get("private_segment_fixed_size", 0) != 0)
@@ -81,10 +81,10 @@ def test_no_kernel_spills_more_than_a_few_registers(tmp_path):
 
 
 def test_fp16_resident_kernels_fit_4_waves(tmp_path):
-    # cand_kernel<DP, 4, 4 | 5, NW> (the fp16 / int8 default paths): <= 128
+    # cand_kernel<DP, 4, 4 | 5 | 6, NW> (the fp16 / int8 default paths): <= 128
     # registers per lane (VGPR + AGPR) so two 8-wave workgroups share a CU
     meta = kernel_metadata(str(tmp_path))
-    fp16 = {k: v for k, v in meta.items() if re.search(r"cand_kernelILi\d+ELi4ELi[45]ELi8E", k)}
+    fp16 = {k: v for k, v in meta.items() if re.search(r"cand_kernelILi\d+ELi4ELi[456]ELi8E", k)}
     assert fp16, "no fp16 resident kernels found"
     for k, v in fp16.items():
         dp = int(re.search(r"cand_kernelILi(\d+)E", k).group(1))
