@@ -529,7 +529,9 @@ static void choose_geometry(knn_ctx* ctx, int metric, bool streamed, int DP, int
     // only on request (resident kernel; tuning experiments)
     // (int8: R = 8 quad lists on request, tuning key "R")
     const bool q8 = quad && metric == 5 && ctx->tune_R == 8;
-    if (pair4 ? R != 4 : quad ? R != (q8 ? 8 : 4) : (ctx->tune_R ? R != ctx->tune_R : R == 4)) continue;
+    if (pair4 ? R != (ctx->tune_R == 8 ? 8 : 4) : quad ? R != (q8 ? 8 : 4)
+              : (ctx->tune_R ? R != ctx->tune_R : R == 4))
+      continue;
     if (R == 4 && (DP > 256 || metric == 1)) continue;
     const int64_t slots =
         (int64_t)(s3q ? s3q_blocks_per_cu() : cand_blocks_per_cu(metric, DP, R, nw)) * ctx->cu_count;
@@ -765,7 +767,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   // 16x16 layouts: 4 lists per query per split
   const bool quad_lists = (!s3 && kmetric >= 3 && kmetric <= 5) || s3q;
   if (quad_lists && !s3q && !(kmetric == 5 && R == 8)) R = 4;
-  if (kmetric == 6) R = 4;  // (2 lists per query per split, pair_min filter)
+  if (kmetric == 6) R = ctx->tune_R == 8 ? 8 : 4;  // (2 lists per query per split, pair_min filter)
   const int NL = (quad_lists ? 4 : 2) * S;
   C = std::min(C, NL * R);
   // rescan workspace: the fast path serves the first `cap` failed queries

@@ -865,8 +865,8 @@ static void launch_res(const CandLaunch& c, hipStream_t s) {
 template <int DP, int R, int M, int NW>
 constexpr bool res_variant() {
   return (M != 2 || DP % 16 == 0) && (M != 1 || (NW == 4 && R != 4)) &&
-         (M < 3 || (DP % 32 == 0 && (R == 4 || (M == 5 && R == 8)) && (NW == 8 || M >= 4))) && (NW != 16 || M == 4) &&
-         (M != 5 || (DP % 64 == 0 && (NW == 8 || NW == 4))) && (M != 6 || (NW == 8 && R == 4));
+         (M < 3 || (DP % 32 == 0 && (R == 4 || (M >= 5 && R == 8)) && (NW == 8 || M >= 4))) && (NW != 16 || M == 4) &&
+         (M != 5 || (DP % 64 == 0 && (NW == 8 || NW == 4))) && (M != 6 || (NW == 8 && (R == 4 || R == 8)));
 }
 
 template <int DP>

@@ -33,7 +33,8 @@
  *   - label = first label whose running count strictly exceeds the running
  *     maximum while scanning the k nearest in order; -1 when k == 0.
  *   - the GPU computes a certified candidate set on MFMA (by default exact
- *     int8 codes on v_mfma_i32_16x16x64_i8 for integer-coded train sets,
+ *     int8 codes on v_mfma_i32_16x16x64_i8 / 32x32x32_i8 for integer-coded
+ *     train sets,
  *     else fp16 operands on v_mfma_f32_16x16x32_f16; bf16x3 or fp32 by
  *     precision mode, see knn_set_precision) and re-ranks it in fp64; queries whose
  *     candidate set cannot be certified are re-run exactly (fp64 over all
@@ -229,10 +230,12 @@ int knn_last_geometry(knn_ctx* ctx, int64_t out[4]);
  *           (hi/lo bf16 split of the fp64 values, ~2^-16 relative error);
  *   FP16: q.x on v_mfma_f32_16x16x32_f16 with both operands in fp16 under
  *         power-of-two scales (~2^-10 relative error), d <= 256.
- * The int8 pass (kernel path 5) is exact: v_mfma_i32_16x16x64_i8 on the
- * codes, centred per dimension; a query off the train set's grid or beyond
- * the codes' range goes to the exact rescan.  It has no precision mode of
- * its own (tuning key "i8").
+ * The int8 pass (kernel paths 5 and 6) is exact: v_mfma_i32_16x16x64_i8
+ * (dims padded to 64) or v_mfma_i32_32x32x32_i8 (dims padded to 32, chosen
+ * where that pads fewer dims, e.g. d = 96) on the codes, centred per
+ * dimension; a query off the train set's grid or beyond the codes' range
+ * goes to the exact rescan.  It has no precision mode of its own (tuning
+ * keys "i8", "i8w").
  * Environment override at knn_create: KNN_PRECISION=fp32|bf16x3|fp16. */
 #define KNN_PRECISION_AUTO 0
 #define KNN_PRECISION_FP32 1
@@ -241,7 +244,7 @@ int knn_last_geometry(knn_ctx* ctx, int64_t out[4]);
 int knn_set_precision(knn_ctx* ctx, int mode);
 /* Candidate kernel flavour of the last search: 0 fp32 L2, 1 fp32 L1, 2 bf16x3
  * L2 (32x32x16 MFMA), 3 bf16x3 L2 (16x16x32), 4 fp16 L2 (16x16x32), 5 int8
- * L2 (16x16x64, exact integer dot products). */
+ * L2 (16x16x64, exact integer dot products), 6 int8 L2 (32x32x32). */
 int knn_last_candidate_path(knn_ctx* ctx);
 /* Name of the last candidate kernel launched, as rocprofv3 reports it
  * without namespace, spaces and argument list (e.g. "cand_kernel<128,4,4,8>"). */
@@ -254,7 +257,8 @@ const char* knn_last_kernel_name(knn_ctx* ctx);
  * L2-resident staging, no workgroup barrier -- results invalid; bit 2: no
  * per-query global threshold exchange, results stay exact); -1 = auto for "fp16" (fp16
  * candidate pass: 0 off, 1 on), "i8" (the int8 candidate pass where the
- * train set is integer-coded: 0 off, 1 on at every batch size), "mfma16" (bf16x3 on the 16x16x32 layout: 0
+ * train set is integer-coded: 0 off, 1 on at every batch size), "i8w" (int8
+ * kernel: -1 auto, 0 the 16x16x64 one, 1 the 32x32x32 one), "mfma16" (bf16x3 on the 16x16x32 layout: 0
  * off, 1 on), "s3q" (the fp16 d > 256 kernel on 16x16x32: 0 off, 1 on) and
  * "gk" (what the global threshold exchange publishes: 0 the lists' R-th
  * entries (resident kernel) / no exchange (S3), K = 1..16 the K-th smallest
