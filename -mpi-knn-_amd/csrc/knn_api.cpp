@@ -519,7 +519,7 @@ static void choose_geometry(knn_ctx* ctx, int metric, bool streamed, int DP, int
   int S_hi = (int)std::max<int64_t>(1, std::min<int64_t>(64, n_tiles));
   int bestS = 1, bestR = 8;
   const bool quad = !streamed && metric >= 3 && metric <= 5;  // 16x16 layouts (bf16x3, fp16, int8)
-  const bool pair4 = metric == 6;  // int8 on 32x32x32: 2 lists of R = 4 per split
+  const bool pair4 = metric == 6;  // int8 on 32x32x32: 2 lists of R = 8 (or 4) per split
   const int lps = quad || s3q ? 4 : 2;  // lists per query per split
   // S3 on 16x16x32 (s3q): R = 8 quad lists, 4 * S * 8 <= kMaxUnion entries
   if (s3q) S_hi = std::min(S_hi, kMaxUnion / (4 * 8));
@@ -529,7 +529,7 @@ static void choose_geometry(knn_ctx* ctx, int metric, bool streamed, int DP, int
     // only on request (resident kernel; tuning experiments)
     // (int8: R = 8 quad lists on request, tuning key "R")
     const bool q8 = quad && metric == 5 && ctx->tune_R == 8;
-    if (pair4 ? R != (ctx->tune_R == 8 ? 8 : 4) : quad ? R != (q8 ? 8 : 4)
+    if (pair4 ? R != (ctx->tune_R == 4 ? 4 : 8) : quad ? R != (q8 ? 8 : 4)
               : (ctx->tune_R ? R != ctx->tune_R : R == 4))
       continue;
     if (R == 4 && (DP > 256 || metric == 1)) continue;
@@ -767,7 +767,11 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   // 16x16 layouts: 4 lists per query per split
   const bool quad_lists = (!s3 && kmetric >= 3 && kmetric <= 5) || s3q;
   if (quad_lists && !s3q && !(kmetric == 5 && R == 8)) R = 4;
-  if (kmetric == 6) R = ctx->tune_R == 8 ? 8 : 4;  // (2 lists per query per split, pair_min filter)
+  // metric 6: 2 lists per query per split (pair_min filter), R = 8 by default:
+  // at a 12.5M x 96 shard R = 4 runs the candidate pass 2.7 % faster but
+  // sends 5 of 10k queries to the rescan (all phases 12.59 vs 12.27 ms,
+  // profiles/ab_log.md r4g4); tuning "R" = 4 selects the short lists
+  if (kmetric == 6) R = ctx->tune_R == 4 ? 4 : 8;
   const int NL = (quad_lists ? 4 : 2) * S;
   C = std::min(C, NL * R);
   // rescan workspace: the fast path serves the first `cap` failed queries
