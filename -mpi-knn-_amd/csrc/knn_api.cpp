@@ -174,6 +174,47 @@ static int detect_i8(knn_ctx* ctx, const double* dX, int64_t n, int d) {
   return KNN_OK;
 }
 
+// Region order of the train images (knn_order.hip): regions for n rows (0:
+// train order).  Auto: one region per 32K rows, at least 4 and at most 64
+// (a region then spans >= 128 tiles of 256 rows: several per split of a
+// 38-split launch), only where the resident kernels run (d <= 256).
+static int region_count(const knn_ctx* ctx, int64_t n, int d) {
+  if (ctx->tune_order == 0 || pad_dim_fp16(d) <= 0) return 0;
+  int P = (int)std::min<int64_t>(kRegionMax, n / 32768);
+  if (ctx->tune_order < 0) return P >= 4 ? P : 0;
+  if (ctx->tune_order >= 2) P = (int)std::min<int64_t>(ctx->tune_order, kRegionMax);
+  P = (int)std::min<int64_t>(P, n / 256);
+  return P >= 2 ? P : 0;
+}
+
+// k-means on a strided sample (8 Lloyd rounds), every row assigned, rows
+// counting-sorted by the chain rank of their region (knn_order.hip).
+static int build_order(knn_ctx* ctx, const double* dX, const double* mu, int64_t n, int d, int jx,
+                       int P) {
+  const int64_t ns = std::min<int64_t>(n, 65536);
+  const int64_t stride = n / ns;
+  const int64_t nb = region_sort_blocks(n);
+  int rc;
+  if ((rc = ctx->ord_cent.ensure((size_t)kRegionMax * d * sizeof(float)))) return rc;
+  if ((rc = ctx->ord_rank.ensure(kRegionMax * sizeof(int)))) return rc;
+  if ((rc = ctx->ord_rstart.ensure(kRegionMax * sizeof(int)))) return rc;
+  if ((rc = ctx->ord_tot.ensure(kRegionMax * sizeof(int)))) return rc;
+  if ((rc = ctx->ord_key.ensure((size_t)n * sizeof(int)))) return rc;
+  if ((rc = ctx->ord_bcnt.ensure((size_t)nb * kRegionMax * sizeof(int)))) return rc;
+  if ((rc = ctx->ord_perm.ensure((size_t)n * sizeof(int)))) return rc;
+  if ((rc = ctx->ord_ipos.ensure((size_t)n * sizeof(int)))) return rc;
+  float* cent = (float*)ctx->ord_cent.p;
+  int* rank = (int*)ctx->ord_rank.p;
+  int* key = (int*)ctx->ord_key.p;
+  launch_region_kmeans(dX, mu, ns, d, stride, jx, P, 8, cent, key, rank, ctx->stream);
+  launch_region_assign(dX, mu, n, d, 1, jx, cent, P, rank, key, ctx->stream);
+  launch_region_sort(key, n, (int*)ctx->ord_bcnt.p, (int*)ctx->ord_tot.p, (int*)ctx->ord_perm.p,
+                     (int*)ctx->ord_ipos.p, nullptr, nullptr, (int*)ctx->ord_rstart.p, ctx->stream);
+  HIP_TRY(hipGetLastError());
+  ctx->ord_P = P;
+  return KNN_OK;
+}
+
 // Builds the fp32 candidate copy + seeds + norm stats from fp64 rows that
 // already sit on the device.
 static int build_train(knn_ctx* ctx, const double* dX, const int32_t* dlab, int64_t n, int d,
@@ -223,8 +264,12 @@ static int build_train(knn_ctx* ctx, const double* dX, const int32_t* dlab, int6
   // measured representation error vanishes from the bound;
   // the shift is <= 2^-11 of max |x - mu|, immaterial for the centring
   launch_round_mu((double*)ctx->mu.p, d, jx + 2, ctx->stream);
+  ctx->ord_P = 0;
+  const int P = region_count(ctx, n, d);
+  if (P > 0 && (rc = build_order(ctx, dX, (const double*)ctx->mu.p, n, d, jx, P))) return rc;
+  const int* perm = ctx->ord_P ? (const int*)ctx->ord_perm.p : nullptr;
   launch_prep_train(dX, (const double*)ctx->mu.p, n, d, DP, n_pad, jx, (float*)ctx->X32.p,
-                    (float*)ctx->xl2.p, (float*)ctx->xl1.p, st_d, ctx->stream);
+                    (float*)ctx->xl2.p, (float*)ctx->xl1.p, st_d, ctx->stream, perm);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(ctx->h_stats, st_d, 2 * 8, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
@@ -245,6 +290,8 @@ static int build_train(knn_ctx* ctx, const double* dX, const int32_t* dlab, int6
   t.x2max = x2;
   t.x1max = x1;
   t.jx = jx;
+  t.perm = perm;
+  t.ipos = perm ? (const int*)ctx->ord_ipos.p : nullptr;
   ctx->class_cnt = class_cnt;
   ctx->idx_off = idx_off;
   ctx->DPb = 0;  // bf16x3 / fp16 copies are rebuilt lazily for the new train set
@@ -274,11 +321,11 @@ static int ensure_bf16x3(knn_ctx* ctx, hipStream_t s) {
     if ((rc = ctx->XB.ensure((size_t)n3 * DPb * 4))) return rc;
     if ((rc = ctx->XS.ensure((size_t)n3 * sizeof(float)))) return rc;
     launch_prep_split_tiled(t.X64, t.mu, t.n, t.d, DPb, n3, std::ldexp(1.0, t.jx), (unsigned short*)ctx->XB.p, t.xinit_l2,
-                            (float*)ctx->XS.p, s);
+                            (float*)ctx->XS.p, s, t.perm);
   } else {
     if ((rc = ctx->XB.ensure((size_t)t.n_pad * (DPb + 4) * sizeof(float) + 1024))) return rc;
     launch_prep_split(t.X64, t.mu, t.n, t.d, DPb, t.n_pad, std::ldexp(1.0, t.jx), (unsigned short*)ctx->XB.p,
-                      2 * (DPb + 4), t.xinit_l2, t.xinit_l1, s);
+                      2 * (DPb + 4), t.xinit_l2, t.xinit_l1, s, t.perm);
   }
   HIP_TRY(hipGetLastError());
   ctx->DPb = DPb;
@@ -299,7 +346,7 @@ static int ensure_fp16(knn_ctx* ctx, hipStream_t s) {
   unsigned long long* st_d = (unsigned long long*)ctx->stats.p + 3;
   HIP_TRY(hipMemsetAsync(st_d, 0, 8, s));
   launch_prep_half_train(t.X64, t.mu, t.n, t.d, DPh, t.n_pad, t.jx,
-                         (unsigned short*)ctx->XH.p, t.xinit_l2, st_d, swz, s);
+                         (unsigned short*)ctx->XH.p, t.xinit_l2, st_d, swz, s, t.perm);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(ctx->h_stats + 3, st_d, 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
@@ -327,7 +374,7 @@ static int ensure_i8(knn_ctx* ctx, int kmetric, hipStream_t s) {
   unsigned* cmax = (unsigned*)((unsigned long long*)ctx->stats.p + 3);
   HIP_TRY(hipMemsetAsync(cmax, 0, 8, s));
   launch_prep_i8_train(t.X64, (const double*)ctx->i8_cent.p, t.n, t.d, DPi, t.n_pad, ctx->i8_s,
-                       (signed char*)ctx->XI.p, cmax, swz, s);
+                       (signed char*)ctx->XI.p, cmax, swz, s, t.perm);
   HIP_TRY(hipGetLastError());
   unsigned cm = 0;
   HIP_TRY(hipMemcpyAsync(&cm, cmax, sizeof cm, hipMemcpyDeviceToHost, s));
@@ -353,7 +400,7 @@ static int ensure_fp16_s3(knn_ctx* ctx, hipStream_t s) {
   unsigned long long* st_d = (unsigned long long*)ctx->stats.p + 3;
   HIP_TRY(hipMemsetAsync(st_d, 0, 8, s));
   launch_prep_half_tiled(t.X64, t.mu, t.n, t.d, DPs, n3, t.jx, 1.0, (unsigned short*)ctx->XT16.p,
-                         t.xinit_l2, (float*)ctx->XS16.p, nullptr, st_d, s);
+                         t.xinit_l2, (float*)ctx->XS16.p, nullptr, st_d, s, t.perm);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(ctx->h_stats + 3, st_d, 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
@@ -380,7 +427,8 @@ static int ensure_fp16_s3(knn_ctx* ctx, hipStream_t s) {
 // key "seed": 0 / -1 off, N = sample rows (experiments).
 
 static int64_t seed_rows(const knn_ctx* ctx) {
-  if (ctx->tune_seed <= 0) return 0;
+  // (the sample image takes train rows by stride: train order only)
+  if (ctx->tune_seed <= 0 || ctx->ord_P) return 0;
   const int64_t ns = std::min<int64_t>(ctx->tune_seed, ctx->train.n / 8) / 256 * 256;
   return ns < 4096 ? 0 : ns;
 }
@@ -831,12 +879,34 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   // marked void and goes to the exact rescan
   const double qscale = metric == KNN_METRIC_L2 ? -2.0 : 1.0;
   float* qvalid = (float*)ctx->qvalid.p;
+  // region order of the queries (resident kernels, metrics 4-6; knn_order.hip):
+  // operand row p = query qperm[p], sorted by region; each query tile's
+  // workgroups start their streams at the tile's region (qstart), and the
+  // merge finds query q's lists at qpos[q]
+  const int* qperm = nullptr;
+  const int* qpos = nullptr;
+  const int* qstart = nullptr;
+  if (ctx->ord_P > 0 && ctx->tune_order != 0 && !s3 && kmetric >= 4 && DP <= 256) {
+    if ((rc = ctx->ord_qkey.ensure((size_t)m * sizeof(int)))) return rc;
+    if ((rc = ctx->ord_bcnt.ensure((size_t)region_sort_blocks(m) * kRegionMax * sizeof(int)))) return rc;
+    if ((rc = ctx->ord_qperm.ensure((size_t)m * sizeof(int)))) return rc;
+    if ((rc = ctx->ord_qpos.ensure((size_t)m * sizeof(int)))) return rc;
+    if ((rc = ctx->ord_qstart.ensure((size_t)m * sizeof(int)))) return rc;
+    launch_region_assign(dQ, t.mu, m, t.d, 1, t.jx, (const float*)ctx->ord_cent.p, ctx->ord_P,
+                         (const int*)ctx->ord_rank.p, (int*)ctx->ord_qkey.p, s);
+    launch_region_sort((const int*)ctx->ord_qkey.p, m, (int*)ctx->ord_bcnt.p, (int*)ctx->ord_tot.p,
+                       (int*)ctx->ord_qperm.p, (int*)ctx->ord_qpos.p,
+                       (const int*)ctx->ord_rstart.p, (int*)ctx->ord_qstart.p, nullptr, s);
+    qperm = (const int*)ctx->ord_qperm.p;
+    qpos = (const int*)ctx->ord_qpos.p;
+    qstart = (const int*)ctx->ord_qstart.p;
+  }
   launch_query_check(dQ, t.mu, m, t.d, m_pad, qscale, t.jx,
                      kmetric >= 5 ? DBL_MAX : kmetric == 4 ? 65000.0 : std::ldexp(1.0, 100), qvalid,
                      s);
   if (kmetric >= 5)  // codes of the train set's grid; a query off it: valid 0 (rescan)
     launch_prep_i8_queries(dQ, (const double*)ctx->i8_cent.p, m, t.d, DP, m_pad, ctx->i8_s,
-                           (signed char*)ctx->Q32.p, qvalid, s);
+                           (signed char*)ctx->Q32.p, qvalid, s, qperm);
   else if (s3h)
     launch_prep_half_tiled(dQ, t.mu, m, t.d, DP, m_pad, t.jx, -2.0, (unsigned short*)ctx->Q32.p,
                            nullptr, nullptr, qvalid, nullptr, s);
@@ -845,7 +915,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
                             (unsigned short*)ctx->Q32.p, nullptr, nullptr, s);
   else if (kmetric == 4)
     launch_prep_half_queries(dQ, t.mu, m, t.d, DP, m_pad, t.jx, (unsigned short*)ctx->Q32.p,
-                             qvalid, s);
+                             qvalid, s, qperm);
   else if (kmetric == 2 || kmetric == 3)
     launch_prep_split(dQ, t.mu, m, t.d, DP, m_pad, std::ldexp(qscale, t.jx),
                       (unsigned short*)ctx->Q32.p, 2 * DP, nullptr, nullptr, s);
@@ -870,6 +940,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   cl.gthr = use_gthr ? (uint32_t*)ctx->gthr.p : nullptr;
   cl.gk = gk;
   cl.xsw = kmetric >= 5 ? ctx->i8_swz : ctx->xh_swz;
+  cl.qstart = qstart;
   // slots of groups without a split stay 0 (never the max)
   // (experiment, tuning "ablate" bit 5: keep the previous call's final
   // thresholds -- valid only for a repeat of the same queries; measures what
@@ -936,15 +1007,15 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
     t8.DP = DP;
     launch_merge_rerank(metric, (const float*)ctx->cand_v.p, (const int*)ctx->cand_i.p, NL, R, t8,
                         dQ, m, W, C, 0.0,
-                        ProxyScale{qvalid, 0.0, 1.0 / DP, false, (const double*)ctx->i8_cent.p},
+                        ProxyScale{qvalid, 0.0, 1.0 / DP, false, (const double*)ctx->i8_cent.p, qpos},
                         cl.gthr, sink,
                         (int*)ctx->rescan_q.p, (double*)ctx->rescan_tau.p, (int*)ctx->rescan_cnt.p,
                         sm, s);
   } else {
     launch_merge_rerank(metric, (const float*)ctx->cand_v.p, (const int*)ctx->cand_i.p, NL, R, t,
                         dQ, m, W, C, err_factor(kmetric, DP),
-                        kmetric == 4 ? ProxyScale{qvalid, 0x1p-14, 0x1p-28, true}
-                                     : ProxyScale{qvalid, 0x1p-125, 0x1p-124},
+                        kmetric == 4 ? ProxyScale{qvalid, 0x1p-14, 0x1p-28, true, nullptr, qpos}
+                                     : ProxyScale{qvalid, 0x1p-125, 0x1p-124, false, nullptr, qpos},
                         cl.gthr, sink, (int*)ctx->rescan_q.p, (double*)ctx->rescan_tau.p,
                         (int*)ctx->rescan_cnt.p, sm, s);
   }
@@ -1372,6 +1443,10 @@ int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value) {
   } else if (!strcmp(key, "seed")) {
     if (value < -1) return knn_fail(KNN_ERR_ARG, "seed must be 0 / -1 (off) or N = sample rows");
     ctx->tune_seed = value;
+  } else if (!strcmp(key, "order")) {
+    if (value < -1 || value > kRegionMax)
+      return knn_fail(KNN_ERR_ARG, "order must be -1 (auto), 0, 1 or 2..64 regions");
+    ctx->tune_order = (int)value;
   } else if (!strcmp(key, "ties")) {
     if (value < 0 || value > 2) return knn_fail(KNN_ERR_ARG, "ties must be 0, 1 or 2");
     ctx->tune_ties = (int)value;

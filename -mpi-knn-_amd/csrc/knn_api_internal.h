@@ -66,6 +66,12 @@ struct knn_ctx {
   int tune_ties = 1;           // reference tie order: 0 off, 1 vote-affecting ties, 2 all ties
   int tune_m16 = -1;           // bf16x3 on the 16x16x32 MFMA layout: -1 auto, 0 off, 1 on
   int64_t tune_seed = 0;       // seeded thresholds: 0 / -1 off, N sample rows (experiment)
+  // region order (knn_order.hip): -1 auto, 0 off, 1 on, N >= 2 that many
+  // regions.  The train layout is decided at set_train; a train set laid out
+  // by region still serves calls with 0 (queries in call order, streams
+  // starting at each split's first tile).
+  int tune_order = -1;
+  int ord_P = 0;               // regions of the current train layout (0: train order)
   // sample image of the seeding pre-pass (strided train rows in the image
   // format of kernel metric smp_kind at width smp_dp; 0 = not built)
   int smp_kind = 0, smp_dp = 0, smp_swz = -1;
@@ -86,6 +92,10 @@ struct knn_ctx {
   // value units d] (the latter the merge's mu for this pass); grid stats scratch
   DevBuf XI, i8_cent, i8_gs;
   DevBuf smp_x64, smp_xl2, smp_img, smp_scr, smp_v, smp_i;
+  // region order: centroids [P][d], chain ranks, region starts, image
+  // position <-> train row maps; k-means / sort scratch; per-call query order
+  DevBuf ord_cent, ord_rank, ord_rstart, ord_perm, ord_ipos, ord_key, ord_bcnt, ord_tot, ord_qkey,
+      ord_qperm, ord_qpos, ord_qstart;
   // per-classify workspace
   DevBuf Q64, Q32, qvalid, cand_v, cand_i, gthr, rescan_q, rescan_tau, rescan_cnt, fr_cnt, fr_buf,
       fr_q, fr_thr, slow_q, totals, lk, rescan_mask, rescan_nkeep;
@@ -101,7 +111,10 @@ struct knn_ctx {
     return {&X64_own, &lab_own, &X32,   &xl2,   &xl1,    &stats,  &XB,       &XS, &XI, &i8_cent, &i8_gs,
             &XH,      &XT16,    &XS16,  &mu,      &mu_part, &Q64, &Q32,    &qvalid, &cand_v,   &cand_i,
             &gthr,    &rescan_q, &rescan_tau, &rescan_cnt, &fr_cnt, &fr_buf, &fr_q, &fr_thr,
-            &slow_q,  &totals,  &lk, &mrg, &tie_q, &tie_ws, &o_lab, &o_idx, &o_dist, &o_flags, &nrm_part, &nrm_mm, &nrm_X};
+            &slow_q,  &totals,  &lk, &mrg, &tie_q, &tie_ws, &o_lab, &o_idx, &o_dist, &o_flags, &nrm_part, &nrm_mm, &nrm_X,
+            &rescan_mask, &rescan_nkeep, &smp_x64, &smp_xl2, &smp_img, &smp_scr, &smp_v, &smp_i,
+            &ord_cent, &ord_rank, &ord_rstart, &ord_perm, &ord_ipos, &ord_key, &ord_bcnt, &ord_tot,
+            &ord_qkey, &ord_qperm, &ord_qpos, &ord_qstart};
   }
 };
 

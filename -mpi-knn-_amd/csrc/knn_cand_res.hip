@@ -165,7 +165,7 @@ __global__ void __launch_bounds__(NW * 64)
 __attribute__((amdgpu_waves_per_eu(res_wpe<DP, R, METRIC>())))
 cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
             int n_qt, float* __restrict__ out_v, int* __restrict__ out_i, int abl,
-            uint32_t* gthr, int gk, int xsw) {
+            uint32_t* gthr, int gk, int xsw, const int* __restrict__ qstart) {
 #if !KNN_ABLATIONS
   abl = 0;  // (folds every ablation check below)
 #endif
@@ -348,6 +348,21 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   int x_ops = 0, x_age = -1;  // ops of the pending exchange, tiles since it
 
   const int my_nt = split < n_tiles ? (n_tiles - split + S - 1) / S : 0;
+  // Region order (knn_order.hip): the split's stream starts at its first tile
+  // at or after the start of the query tile's region (the query tile's own
+  // neighbourhood first, thresholds tight from the first tiles) and wraps.
+  // The split's set of tiles is unchanged.
+  int it0 = 0;
+  if (qstart && my_nt > 1) {
+    const int t0 = __builtin_amdgcn_readfirstlane(qstart[(int64_t)qt * (NW * QW)]) / (kTR * TPB);
+    it0 = t0 > split ? (t0 - split + S - 1) / S : 0;
+    if (it0 >= my_nt) it0 = my_nt - 1;
+  }
+  auto tile_at = [&](int i) {  // i < 2 my_nt
+    int r = i + it0;
+    if (r >= my_nt) r -= my_nt;
+    return split + r * S;
+  };
   constexpr bool PIPE = TEC && KNN_M4_PIPE && DP <= 192;  // DP 256: no registers to spare
   using AccT = std::conditional_t<I8A, i32x4, f32x4>;
   // PIPE: the previous sub-tile's accumulators; before the first sub-tile
@@ -408,12 +423,12 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   }
 #pragma unroll
   for (int p = 0; p < PD; ++p)
-    if (my_nt > p) KNN_ISSUE(split + p * S, p);
+    if (my_nt > p) KNN_ISSUE(tile_at(p), p);
 
   const bool g_hi = wv < NG % NW || NG % NW == 0;
   int cur = 0, nxt = PD;  // buffer of tile it, buffer that tile it+PD goes to
   for (int it = 0; it < my_nt; ++it) {
-    const int t = split + it * S;
+    const int t = tile_at(it);
     if constexpr (TEC) {
 #pragma unroll
       for (int b = 0; b < NQL; ++b) thr[b] = lval(L[b][R - 1]);  // for the exchange below
@@ -448,7 +463,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       __builtin_amdgcn_sched_barrier(0);
       // (abl bit 3: the same pieces, always of the split's first tile -- DMA
       // issue cost without the data stream; timing only)
-      if (it + PD < my_nt && !(abl & 1)) KNN_ISSUE((abl & 8) ? split : t + PD * S, nxt);
+      if (it + PD < my_nt && !(abl & 1)) KNN_ISSUE((abl & 8) ? tile_at(0) : tile_at(it + PD), nxt);
       if (gthr) {
         if (x_age == XPD) {
 #pragma unroll
@@ -854,7 +869,7 @@ static void launch_res(const CandLaunch& c, hipStream_t s) {
   hipLaunchKernelGGL((cand_kernel<DP, R, METRIC, NW>), dim3((unsigned)(c.n_qt * c.S)),
                      dim3(NW * 64), 0, s, c.X32, c.Q32, (int)(c.n_pad / (kTR * res_tpb<METRIC>())), c.S,
                      c.n_qt,
-                     c.out_v, c.out_i, c.ablate, c.gthr, c.gk, c.xsw);
+                     c.out_v, c.out_i, c.ablate, c.gthr, c.gk, c.xsw, c.qstart);
 }
 
 // Instantiated variants: R in {4, 8, 16}; METRIC 0/2 with NW in {4, 8};

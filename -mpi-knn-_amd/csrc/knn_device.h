@@ -102,6 +102,15 @@ __device__ __forceinline__ double exact_dist(const double* __restrict__ q,
 // fp-class test (is-inf-or-nan), and under -fno-honor-nans it then drops the
 // NaN half -- measured on the large-k path: a NaN query went through as
 // finite while -inf was caught.
+// train row of candidate-image row (position) p (region order)
+__device__ __forceinline__ int train_row(const TrainDev& t, int p) { return t.perm ? t.perm[p] : p; }
+
+// Source row of image row `row` under an optional permutation (region order,
+// knn_order.hip): perm[row] for real rows, the row itself otherwise.
+__device__ __forceinline__ int64_t src_row(const int* perm, int64_t row, int64_t n) {
+  return perm && row < n ? (int64_t)perm[row] : row;
+}
+
 __device__ __forceinline__ bool nonfinite_bits(double x) {
   long long b = __double_as_longlong(x);
   asm volatile("" : "+v"(b));

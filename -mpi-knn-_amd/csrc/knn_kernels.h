@@ -50,6 +50,12 @@ struct TrainDev {
   double x2max, x1max;   // max ||x - mu||_2^2, max ||x - mu||_1 over the train rows
   double dxmax;          // max ||fp16 row / 2^jx - (x - mu)||_2 of the fp16 copy (when built)
   int jx;                // candidate operands are 2^jx (x - mu) (knn_prep.hip)
+  // Region order (knn_order.hip): row p of every candidate image (X32, the
+  // fp16 / bf16 / int8 copies) is train row perm[p]; ipos is the inverse.
+  // Null: images in train order.  Candidate lists carry image positions; the
+  // merge and the rescan report train rows.
+  const int* perm = nullptr;  // [n]
+  const int* ipos = nullptr;  // [n]
 };
 
 int pad_dim(int d);                 // padded dim the candidate kernels run at
@@ -68,7 +74,8 @@ void launch_cand_s3(const unsigned short* XT, const float* XS, const unsigned sh
 // (train only, else null) receives seed_src[row] (+inf on pad rows)
 void launch_prep_split_tiled(const double* X64, const double* mu, int64_t n, int d, int DP,
                              int64_t n_pad, double scale, unsigned short* out,
-                             const float* seed_src, float* seed_out, hipStream_t s);
+                             const float* seed_src, float* seed_out, hipStream_t s,
+                             const int* perm = nullptr);
 // fp16 S3 kernel (DP > 256, DP % 32 == 0): XT/QT made by launch_prep_half_tiled
 // q16: the v_mfma_f32_16x16x32_f16 form (R = 8 quad lists: [m_pad][4S][8])
 // gthr / gk: the global threshold exchange of the q16 form (null / 0: none)
@@ -87,7 +94,7 @@ int pad_dim_fp16_s3(int d);         // padded dim of the fp16 S3 image (multiple
 void launch_prep_half_tiled(const double* X64, const double* mu, int64_t n, int d, int DP,
                             int64_t n_pad, int jx, double mult, unsigned short* out,
                             const float* seed_src, float* seed_out, const float* valid,
-                            unsigned long long* dx2max, hipStream_t s);
+                            unsigned long long* dx2max, hipStream_t s, const int* perm = nullptr);
 bool cand_supported(int DP);
 // train rows per tile of the candidate kernel serving (kernel metric, DP):
 // split s of a launch walks tiles s, s + S, ... (rows (r / tile) % S == s)
@@ -115,6 +122,11 @@ struct CandLaunch {
   int gk;          // what a list group publishes into gthr (see cand_kernel): 0 = the
                    // lists' R-th entries into split % 4, K = 1..4: the K-th smallest of
                    // the union of the query's lists in the workgroup into split % 8
+  // resident kernel, region order: qstart[p] = the image position where the
+  // region of the query at position p starts; each workgroup starts its
+  // split's stream at the first of its tiles at or after qstart[first
+  // query of the tile] (null: at the split's first tile)
+  const int* qstart = nullptr;
 };
 constexpr uint32_t kGthrInit = 0xFF800000u;  // order-preserving key of +inf
 constexpr int kGthrSlots = 8;                // slots per query in gthr
@@ -132,9 +144,10 @@ void launch_absmax(const double* X64, const double* mu, int64_t n, int d, unsign
                    unsigned long long* nonfinite, hipStream_t s);
 void launch_label_check(const int32_t* lab, int64_t n, int class_cnt, unsigned long long* bad,
                         hipStream_t s);
+// perm (every train image builder): image row p <- train row perm[p] (null: p)
 void launch_prep_train(const double* X64, const double* mu, int64_t n, int d, int DP,
                        int64_t n_pad, int jx, float* X32, float* xl2, float* xl1,
-                       unsigned long long* stats, hipStream_t s);
+                       unsigned long long* stats, hipStream_t s, const int* perm = nullptr);
 void launch_query_check(const double* Q64, const double* mu, int64_t m, int d, int64_t m_pad,
                         double scale, int jx, double limit, float* valid, hipStream_t s);
 void launch_prep_queries(const double* Q64, const double* mu, int64_t m, int d, int DP,
@@ -159,6 +172,9 @@ struct ProxyScale {
   // int8 pass: the per-dimension code centres (queries are coded
   // clamp(rint(q 2^s - cent), -128, 127); the merge measures the rounding)
   const double* i8c = nullptr;
+  // queries in region order: query q's lists and thresholds sit at position
+  // qpos[q] (null: at q)
+  const int* qpos = nullptr;
 };
 // Per-split certification (merge) and the targeted rescan: a query whose
 // bound fails only through some splits' lists (a list holding R of its top
@@ -263,9 +279,11 @@ void launch_grid_stats(const double* X64, int64_t n, int d, double* partial, dou
 // the 32x32x32 kernel's (its reads are conflict-free unswizzled)
 void launch_prep_i8_train(const double* X64, const double* cent, int64_t n, int d, int DP,
                           int64_t n_pad, int s, signed char* out, unsigned* codes_max, int swz,
-                          hipStream_t st);
+                          hipStream_t st, const int* perm = nullptr);
+// qperm (query operand builders): operand row p <- query qperm[p] (null: p)
 void launch_prep_i8_queries(const double* Q64, const double* cent, int64_t m, int d, int DP,
-                            int64_t m_pad, int s, signed char* out, float* valid, hipStream_t st);
+                            int64_t m_pad, int s, signed char* out, float* valid, hipStream_t st,
+                            const int* qperm = nullptr);
 int pad_dim_i8(int d);  // padded dim of the int8 kernel (a multiple of 64, <= 256), -1 if none
 int pad_dim_i8w(int d); // padded dim of the int8 32x32x32 kernel (metric 6), -1 if none
 // The reference's exact neighbour order on exact distance ties (knn_select.hip,
@@ -289,16 +307,35 @@ void launch_tie_order(int metric, const TrainDev& t, const double* Q64, const in
 // swz: store the payload chunks swizzled (xh_swz, knn_device.h)
 void launch_prep_half_train(const double* X64, const double* mu, int64_t n, int d, int DP,
                             int64_t n_pad, int jx, unsigned short* out, const float* xl2,
-                            unsigned long long* dx2max, int swz, hipStream_t s);
+                            unsigned long long* dx2max, int swz, hipStream_t s,
+                            const int* perm = nullptr);
 // mu <- mu rounded to a multiple of 2^-g (the centre then sits on any data
 // grid at least as coarse, so such data is exact in the fp16 operands)
 void launch_round_mu(double* mu, int d, int g, hipStream_t s);
 void launch_prep_half_queries(const double* Q64, const double* mu, int64_t m, int d, int DP,
                               int64_t m_pad, int jx, unsigned short* out, const float* valid,
-                              hipStream_t s);
+                              hipStream_t s, const int* qperm = nullptr);
 void launch_prep_split(const double* X64, const double* mu, int64_t n, int d, int DP,
                        int64_t n_pad, double scale, unsigned short* out, int row_shorts,
-                       const float* xl2, const float* xl1, hipStream_t s);
+                       const float* xl2, const float* xl1, hipStream_t s, const int* perm = nullptr);
+
+// Region order (knn_order.hip).  Features are the fp32 operands 2^jx (x - mu).
+constexpr int kRegionMax = 64;  // regions (k-means centroids) at most
+// out[r] = rank[nearest centroid of row r * stride] (rank null: the centroid)
+void launch_region_assign(const double* X, const double* mu, int64_t n, int d, int64_t stride,
+                          int jx, const float* cent, int P, const int* rank, int* out, hipStream_t s);
+// k-means over ns sample rows (row i = X row i * stride): cent [P][d],
+// assign [ns] scratch, rank [P] = each centroid's place in the greedy chain
+void launch_region_kmeans(const double* X, const double* mu, int64_t ns, int d, int64_t stride,
+                          int jx, int P, int iters, float* cent, int* assign, int* rank,
+                          hipStream_t s);
+// Stable counting sort of n keys in [0, kRegionMax): bcnt holds
+// region_sort_blocks(n) x kRegionMax ints, tot kRegionMax; outputs (nullable)
+// perm[pos] = i, ipos[i] = pos, qstart[pos] = rstart[key], bases[k] = the
+// first position of key k
+int64_t region_sort_blocks(int64_t n);
+void launch_region_sort(const int* key, int64_t n, int* bcnt, int* tot, int* perm, int* ipos,
+                        const int* rstart, int* qstart, int* bases, hipStream_t s);
 
 // Min-max normalisation (knn_normalize.hip, cpp:229-306).  R = rows per
 // grid sweep; `partial` holds 2*d*R doubles.  launch_minmax folds the set's

@@ -1,0 +1,323 @@
+// knn_order.hip -- the order in which the candidate pass streams the train
+// rows ("regions"), and the matching order of the queries.
+//
+// The candidate kernels filter each row against per-query thresholds that
+// tighten as the stream goes on; the rows a split sees before its thresholds
+// are tight are the ones that pay list insertions and the divergent slow
+// path of the selection.  Nothing in the result depends on
+// the order (the pass is certified and re-ranked exactly, ties by train
+// index), so the train image is laid out by region:
+//   1. k-means (Lloyd) on a strided sample of the rows, P <= 64 centroids;
+//   2. the centroids chained greedily (each next one the nearest unvisited),
+//      so regions adjacent in the chain are near each other;
+//   3. every row assigned to its nearest centroid and the rows stably
+//      counting-sorted by the chain rank of their region: image position
+//      p holds train row perm[p] (ipos is the inverse).
+// Per classify call the queries get the same treatment (assign, sort), and
+// each query tile's workgroups start their streams at the first tile of the
+// tile's region (cand_kernel, qstart): the first rows each split sees are
+// the query tile's own neighbourhood, and its thresholds are tight from the
+// first tiles on.  Everything here is deterministic (integer counts, fixed
+// summation orders), so the same train set always gets the same layout.
+#include "knn_device.h"
+#include "knn_kernels.h"
+
+namespace knnk {
+
+constexpr int kOrdDC = 32;  // dims per staged chunk of the assignment kernel
+
+// Nearest centroid of rows r = 0..n-1 (source row r * stride of X, as the
+// fp32 operands 2^jx (x - mu) of every candidate path -- any assignment is
+// valid, only locality matters).  Block = 64
+// rows x 4 waves; wave w scores centroids 16w .. 16w+15 for every row of the
+// block (lane = row), score_p = ||c_p||^2 - 2 x.c_p; the lowest score wins,
+// the lowest p on ties.  Centroids transposed in LDS ([d][64]: one 16-B
+// broadcast read per 4 centroids); out[r] = rank[p] (rank null: p).
+__global__ void __launch_bounds__(256)
+region_assign_kernel(const double* __restrict__ X, const double* __restrict__ mu, int64_t n, int d,
+                     int64_t stride, int jx, const float* __restrict__ cent, int P,
+                     const int* __restrict__ rank, int* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) float cT[256 * kRegionMax];
+  __shared__ float tile[64 * (kOrdDC + 1)];
+  __shared__ float cn[kRegionMax];
+  __shared__ float bs[4][64];
+  __shared__ int bp[4][64];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int e = tid; e < d * kRegionMax; e += 256) {
+    const int c = e / kRegionMax, p = e - c * kRegionMax;
+    cT[e] = p < P ? cent[(int64_t)p * d + c] : 0.0f;
+  }
+  __syncthreads();
+  if (tid < kRegionMax) {
+    float s = 0.0f;
+    for (int c = 0; c < d; ++c) s = __builtin_fmaf(cT[c * kRegionMax + tid], cT[c * kRegionMax + tid], s);
+    cn[tid] = tid < P ? s : KNN_INF_F;
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * 64;
+  float acc[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+  for (int c0 = 0; c0 < d; c0 += kOrdDC) {
+    __syncthreads();  // the previous chunk's reads of tile are done
+#pragma unroll
+    for (int u = 0; u < 64 * kOrdDC / 256; ++u) {
+      const int e = tid + 256 * u, rr = e / kOrdDC, cc = e - rr * kOrdDC;
+      float v = 0.0f;
+      if (r0 + rr < n && c0 + cc < d)
+        v = (float)__builtin_ldexp(X[(r0 + rr) * stride * d + c0 + cc] - mu[c0 + cc], jx);
+      tile[rr * (kOrdDC + 1) + cc] = v;
+    }
+    __syncthreads();
+    const int nc = min(kOrdDC, d - c0);
+    for (int cc = 0; cc < nc; ++cc) {
+      const float x = tile[lane * (kOrdDC + 1) + cc];
+      const float4* cr = (const float4*)(cT + (c0 + cc) * kRegionMax + 16 * wv);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float4 c4 = cr[u];
+        acc[4 * u] = __builtin_fmaf(x, c4.x, acc[4 * u]);
+        acc[4 * u + 1] = __builtin_fmaf(x, c4.y, acc[4 * u + 1]);
+        acc[4 * u + 2] = __builtin_fmaf(x, c4.z, acc[4 * u + 2]);
+        acc[4 * u + 3] = __builtin_fmaf(x, c4.w, acc[4 * u + 3]);
+      }
+    }
+  }
+  float best = KNN_INF_F;
+  int bpi = 0x7fffffff;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int p = 16 * wv + i;
+    const float s = cn[p] - 2.0f * acc[i];
+    if (p < P && (s < best || bpi == 0x7fffffff)) {
+      best = s;
+      bpi = p;
+    }
+  }
+  bs[wv][lane] = best;
+  bp[wv][lane] = bpi;
+  __syncthreads();
+  if (wv == 0 && r0 + lane < n) {
+    float b = bs[0][lane];
+    int p = bp[0][lane];
+    for (int w = 1; w < 4; ++w)
+      if (bp[w][lane] != 0x7fffffff && (p == 0x7fffffff || bs[w][lane] < b)) {
+        b = bs[w][lane];
+        p = bp[w][lane];
+      }
+    if (p == 0x7fffffff) p = 0;  // no finite score (a query beyond fp32 range)
+    out[r0 + lane] = rank ? rank[p] : p;
+  }
+}
+
+// Lloyd update: centroid p = mean of the sample rows assigned to it (fp64
+// sums in row order: deterministic); an empty centroid keeps its value.
+// Grid = P blocks, thread = dimension (d <= 256).
+__global__ void __launch_bounds__(256)
+region_update_kernel(const double* __restrict__ X, const double* __restrict__ mu, int64_t ns,
+                     int d, int64_t stride, int jx, const int* __restrict__ assign,
+                     float* __restrict__ cent) {
+  __shared__ int a[256];
+  const int p = blockIdx.x, c = threadIdx.x;
+  double s = 0.0;
+  int64_t cnt = 0;
+  for (int64_t i0 = 0; i0 < ns; i0 += 256) {
+    __syncthreads();
+    a[threadIdx.x] = i0 + threadIdx.x < ns ? assign[i0 + threadIdx.x] : -1;
+    __syncthreads();
+    const int nb = (int)min((int64_t)256, ns - i0);
+    for (int i = 0; i < nb; ++i)
+      if (a[i] == p) {
+        ++cnt;
+        if (c < d) s += __builtin_ldexp(X[(i0 + i) * stride * d + c] - mu[c], jx);
+      }
+  }
+  if (c < d && cnt > 0) cent[(int64_t)p * d + c] = (float)(s / (double)cnt);
+}
+
+// Initial centroids: sample rows p * ns / P (centred).
+__global__ void region_init_kernel(const double* __restrict__ X, const double* __restrict__ mu,
+                                   int64_t ns, int d, int64_t stride, int jx, int P,
+                                   float* __restrict__ cent) {
+  const int p = blockIdx.x;
+  const int64_t r = (int64_t)p * ns / P;
+  for (int c = threadIdx.x; c < d; c += blockDim.x)
+    cent[(int64_t)p * d + c] = (float)__builtin_ldexp(X[r * stride * d + c] - mu[c], jx);
+}
+
+// Greedy chain over the P centroids (one wave, lane = centroid): start at
+// the centroid farthest from centroid 0, then repeatedly the nearest
+// unvisited one; rank[p] = its position in the chain.
+__global__ void __launch_bounds__(64)
+region_chain_kernel(const float* __restrict__ cent, int P, int d, int* __restrict__ rank) {
+  const int p = threadIdx.x;
+  auto dist_to = [&](int cur) {
+    float s = KNN_INF_F;
+    if (p < P) {
+      s = 0.0f;
+      for (int c = 0; c < d; ++c) {
+        const float t = cent[(int64_t)p * d + c] - cent[(int64_t)cur * d + c];
+        s = __builtin_fmaf(t, t, s);
+      }
+    }
+    return s == s ? s : 3e38f;  // (NaN: far)
+  };
+  // argmax / argmin over the wave, lowest index on ties
+  auto pick = [&](float v, bool want_max) {
+    float best = v;
+    int bi = p;
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      const bool take = want_max ? (ov > best || (ov == best && oi < bi))
+                                 : (ov < best || (ov == best && oi < bi));
+      if (take) {
+        best = ov;
+        bi = oi;
+      }
+    }
+    return bi;
+  };
+  float d0 = dist_to(0);
+  int cur = pick(p < P ? d0 : -1.0f, true);
+  bool visited = false;
+  for (int step = 0; step < P; ++step) {
+    if (p == cur) {
+      visited = true;
+      rank[p] = step;
+    }
+    if (step + 1 == P) break;
+    const float dc = dist_to(cur);
+    cur = pick(visited || p >= P ? KNN_INF_F : dc, false);
+  }
+}
+
+// ------------------------------------------------------------ counting sort
+// Stable sort of n keys in [0, kRegionMax) (key < 0: not sorted), in
+// blocks of 1024 elements: per-block counts, per-key exclusive scans over
+// the blocks, then a scatter that ranks equal keys within a block in index
+// order (wave ballots on the key bits).
+constexpr int kSortB = 1024;
+
+__global__ void __launch_bounds__(kSortB)
+sort_hist_kernel(const int* __restrict__ key, int64_t n, int* __restrict__ bcnt) {
+  __shared__ int cnt[kRegionMax];
+  if (threadIdx.x < kRegionMax) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * kSortB + threadIdx.x;
+  if (i < n) {
+    const int k = key[i];
+    if (k >= 0) atomicAdd(&cnt[k], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x < kRegionMax) bcnt[(int64_t)blockIdx.x * kRegionMax + threadIdx.x] = cnt[threadIdx.x];
+}
+
+// Grid = kRegionMax blocks (one per key): bcnt[b][k] <- exclusive prefix over
+// blocks b, tot[k] <- the key's total.
+__global__ void __launch_bounds__(kSortB)
+sort_scan_kernel(int* __restrict__ bcnt, int64_t nb, int* __restrict__ tot) {
+  __shared__ int ws[kSortB / 64];
+  __shared__ int carry;
+  const int k = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) carry = 0;
+  for (int64_t b0 = 0; b0 < nb; b0 += kSortB) {
+    __syncthreads();
+    const int64_t b = b0 + tid;
+    const int v = b < nb ? bcnt[b * kRegionMax + k] : 0;
+    // inclusive scan within the wave
+    int x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) ws[wv] = x;
+    __syncthreads();
+    int before = carry;
+    for (int w = 0; w < wv; ++w) before += ws[w];
+    if (b < nb) bcnt[b * kRegionMax + k] = before + x - v;
+    __syncthreads();
+    if (tid == kSortB - 1) carry = before + x;
+  }
+  __syncthreads();
+  if (tid == 0) tot[k] = carry;
+}
+
+// pos = (keys before k in total) + (key k in earlier blocks) + (key k
+// earlier in this block).  Outputs (each nullable): perm[pos] = i,
+// ipos[i] = pos, qstart[pos] = rstart[k]; bases (block 0) = the exclusive
+// prefix of tot (the start position of each key).
+__global__ void __launch_bounds__(kSortB)
+sort_scatter_kernel(const int* __restrict__ key, int64_t n, const int* __restrict__ bcnt,
+                    const int* __restrict__ tot, int* __restrict__ perm, int* __restrict__ ipos,
+                    const int* __restrict__ rstart, int* __restrict__ qstart, int* __restrict__ bases) {
+  __shared__ int base[kRegionMax];
+  __shared__ int wc[kSortB / 64][kRegionMax];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid < 64) {
+    const int v = tid < kRegionMax ? tot[tid] : 0;
+    int x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (tid < kRegionMax) {
+      base[tid] = x - v;
+      if (bases && blockIdx.x == 0) bases[tid] = x - v;
+    }
+  }
+  for (int e = tid; e < (kSortB / 64) * kRegionMax; e += kSortB) (&wc[0][0])[e] = 0;
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * kSortB + tid;
+  const int k = i < n ? key[i] : -1;
+  const bool valid = k >= 0;
+  unsigned long long m = __ballot(valid);
+#pragma unroll
+  for (int b = 0; b < 6; ++b) {
+    const bool bit = valid && ((k >> b) & 1);
+    const unsigned long long bal = __ballot(bit);
+    m &= bit ? bal : ~bal;
+  }
+  const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+  if (valid && r == 0) wc[wv][k] = __popcll(m);
+  __syncthreads();
+  if (!valid) return;
+  int pos = base[k] + bcnt[(int64_t)blockIdx.x * kRegionMax + k] + r;
+  for (int w = 0; w < wv; ++w) pos += wc[w][k];
+  if (perm) perm[pos] = (int)i;
+  if (ipos) ipos[i] = pos;
+  if (qstart) qstart[pos] = rstart[k];
+}
+
+int64_t region_sort_blocks(int64_t n) { return (n + kSortB - 1) / kSortB; }
+
+void launch_region_assign(const double* X, const double* mu, int64_t n, int d, int64_t stride,
+                          int jx, const float* cent, int P, const int* rank, int* out, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(region_assign_kernel, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, s, X, mu,
+                     n, d, stride, jx, cent, P, rank, out);
+}
+
+void launch_region_kmeans(const double* X, const double* mu, int64_t ns, int d, int64_t stride,
+                          int jx, int P, int iters, float* cent, int* assign, int* rank,
+                          hipStream_t s) {
+  hipLaunchKernelGGL(region_init_kernel, dim3(P), dim3(256), 0, s, X, mu, ns, d, stride, jx, P,
+                     cent);
+  for (int it = 0; it < iters; ++it) {
+    launch_region_assign(X, mu, ns, d, stride, jx, cent, P, nullptr, assign, s);
+    hipLaunchKernelGGL(region_update_kernel, dim3(P), dim3(256), 0, s, X, mu, ns, d, stride, jx,
+                       assign, cent);
+  }
+  hipLaunchKernelGGL(region_chain_kernel, dim3(1), dim3(64), 0, s, cent, P, d, rank);
+}
+
+void launch_region_sort(const int* key, int64_t n, int* bcnt, int* tot, int* perm, int* ipos,
+                        const int* rstart, int* qstart, int* bases, hipStream_t s) {
+  if (n <= 0) return;
+  const int64_t nb = region_sort_blocks(n);
+  hipLaunchKernelGGL(sort_hist_kernel, dim3((unsigned)nb), dim3(kSortB), 0, s, key, n, bcnt);
+  hipLaunchKernelGGL(sort_scan_kernel, dim3(kRegionMax), dim3(kSortB), 0, s, bcnt, nb, tot);
+  hipLaunchKernelGGL(sort_scatter_kernel, dim3((unsigned)nb), dim3(kSortB), 0, s, key, n, bcnt, tot,
+                     perm, ipos, rstart, qstart, bases);
+}
+
+}  // namespace knnk

@@ -120,17 +120,19 @@ void launch_label_check(const int32_t* lab, int64_t n, int class_cnt, unsigned l
 __global__ void __launch_bounds__(256)
 prep_train_kernel(const double* __restrict__ X64, const double* __restrict__ mu, int64_t n, int d,
                   int DP, int64_t n_pad, int jx, float* __restrict__ X32, float* __restrict__ xl2,
-                  float* __restrict__ xl1, unsigned long long* __restrict__ stats) {
+                  float* __restrict__ xl1, unsigned long long* __restrict__ stats,
+                  const int* __restrict__ perm) {
   const int RSF = DP + 4;  // padded row: [x32 (DP) | ||x32||^2, l1 seed, 0, 0]
   const int lane = threadIdx.x & 63;
   const int64_t wstride = (int64_t)gridDim.x * 4;
   double m2 = 0.0, m1 = 0.0;
   for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n_pad; row += wstride) {
     double s32 = 0.0, s64 = 0.0, a64 = 0.0;
+    const int64_t src = src_row(perm, row, n);
     for (int c = lane; c < DP; c += 64) {
       float v = 0.0f;
       if (row < n && c < d) {
-        const double x = X64[row * d + c] - mu[c];
+        const double x = X64[src * d + c] - mu[c];
         v = (float)__builtin_ldexp(x, jx);
         s64 += x * x;
         a64 += __builtin_fabs(x);
@@ -162,11 +164,11 @@ prep_train_kernel(const double* __restrict__ X64, const double* __restrict__ mu,
 
 void launch_prep_train(const double* X64, const double* mu, int64_t n, int d, int DP,
                        int64_t n_pad, int jx, float* X32, float* xl2, float* xl1,
-                       unsigned long long* stats, hipStream_t s) {
+                       unsigned long long* stats, hipStream_t s, const int* perm) {
   int64_t blocks = (n_pad + 3) / 4;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(prep_train_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X64, mu, n, d,
-                     DP, n_pad, jx, X32, xl2, xl1, stats);
+                     DP, n_pad, jx, X32, xl2, xl1, stats, perm);
 }
 
 // Per query: valid[row] = 1 when every |scale * 2^jx (q_i - mu_i)| stays below
@@ -226,7 +228,8 @@ void launch_prep_queries(const double* Q64, const double* mu, int64_t m, int d, 
 __global__ void __launch_bounds__(256)
 prep_split_kernel(const double* __restrict__ X64, const double* __restrict__ mu, int64_t n, int d,
                   int DP, int64_t n_pad, double scale, unsigned short* __restrict__ out, int row_shorts,
-                  const float* __restrict__ xl2, const float* __restrict__ xl1) {
+                  const float* __restrict__ xl2, const float* __restrict__ xl1,
+                  const int* __restrict__ perm) {
   // row r of `out` (row_shorts 16-bit words) = [hi(DP) | lo(DP) | seeds...]
   const int64_t total = n_pad * DP;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
@@ -234,7 +237,7 @@ prep_split_kernel(const double* __restrict__ X64, const double* __restrict__ mu,
     const int64_t row = e / DP;
     const int c = (int)(e - row * DP);
     unsigned short hi = 0, lo = 0;
-    if (row < n && c < d) split_bf16(scale * (X64[row * d + c] - mu[c]), hi, lo);
+    if (row < n && c < d) split_bf16(scale * (X64[src_row(perm, row, n) * d + c] - mu[c]), hi, lo);
     out[row * row_shorts + c] = hi;
     out[row * row_shorts + DP + c] = lo;
     if (xl2 && c < 4) {  // train rows: the padded row's seed floats
@@ -246,11 +249,11 @@ prep_split_kernel(const double* __restrict__ X64, const double* __restrict__ mu,
 
 void launch_prep_split(const double* X64, const double* mu, int64_t n, int d, int DP,
                        int64_t n_pad, double scale, unsigned short* out, int row_shorts,
-                       const float* xl2, const float* xl1, hipStream_t s) {
+                       const float* xl2, const float* xl1, hipStream_t s, const int* perm) {
   int64_t blocks = (n_pad * DP + 255) / 256;
   if (blocks > 16384) blocks = 16384;
   hipLaunchKernelGGL(prep_split_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X64, mu, n, d, DP,
-                     n_pad, scale, out, row_shorts, xl2, xl1);
+                     n_pad, scale, out, row_shorts, xl2, xl1, perm);
 }
 
 // ---------------------------------- fp16 images (kernel metric 4, d <= 256)
@@ -262,7 +265,7 @@ __global__ void __launch_bounds__(256)
 prep_half_train_kernel(const double* __restrict__ X64, const double* __restrict__ mu, int64_t n,
                        int d, int DP, int64_t n_pad, int jx, unsigned short* __restrict__ out,
                        const float* __restrict__ xl2, unsigned long long* __restrict__ dx2max,
-                       int swz) {
+                       int swz, const int* __restrict__ perm) {
   // one wave per row; the row's representation error ||h / 2^jx - (x - mu)||^2
   // is measured in fp64 (h / 2^jx - x is exact: Sterbenz, or h = 0)
   const int row_shorts = DP + 8;
@@ -273,10 +276,11 @@ prep_half_train_kernel(const double* __restrict__ X64, const double* __restrict_
   for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n_pad; row += wstride) {
     double e2 = 0.0;
     const int cx = swz ? xh_swz((int)(row & 15)) << 3 : 0;
+    const int64_t src = src_row(perm, row, n);
     for (int c = lane; c < DP; c += 64) {
       _Float16 h = (_Float16)0.0f;
       if (row < n && c < d) {
-        const double x = X64[row * d + c] - mu[c];
+        const double x = X64[src * d + c] - mu[c];
         h = f16_operand(x, jx);
         const double e = (double)h * sinv - x;
         e2 += e * e;
@@ -297,11 +301,11 @@ prep_half_train_kernel(const double* __restrict__ X64, const double* __restrict_
 
 void launch_prep_half_train(const double* X64, const double* mu, int64_t n, int d, int DP,
                             int64_t n_pad, int jx, unsigned short* out, const float* xl2,
-                            unsigned long long* dx2max, int swz, hipStream_t s) {
+                            unsigned long long* dx2max, int swz, hipStream_t s, const int* perm) {
   int64_t blocks = (n_pad + 3) / 4;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(prep_half_train_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X64, mu, n, d,
-                     DP, n_pad, jx, out, xl2, dx2max, swz);
+                     DP, n_pad, jx, out, xl2, dx2max, swz, perm);
 }
 
 __global__ void round_mu_kernel(double* mu, int d, int g) {
@@ -321,26 +325,27 @@ void launch_round_mu(double* mu, int d, int g, hipStream_t s) {
 __global__ void __launch_bounds__(256)
 prep_half_queries_kernel(const double* __restrict__ Q64, const double* __restrict__ mu, int64_t m,
                          int d, int DP, int64_t m_pad, int jx, unsigned short* __restrict__ out,
-                         const float* __restrict__ valid) {
+                         const float* __restrict__ valid, const int* __restrict__ qperm) {
   const int64_t total = m_pad * DP;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * 256) {
     const int64_t row = e / DP;
     const int c = (int)(e - row * DP);
     _Float16 h = (_Float16)0.0f;
-    if (row < m && c < d && valid[row] > 0.0f)
-      h = f16_operand(-2.0 * (Q64[row * d + c] - mu[c]), jx);
+    const int64_t q = src_row(qperm, row, m);
+    if (row < m && c < d && valid[q] > 0.0f)
+      h = f16_operand(-2.0 * (Q64[q * d + c] - mu[c]), jx);
     out[e] = __builtin_bit_cast(unsigned short, h);
   }
 }
 
 void launch_prep_half_queries(const double* Q64, const double* mu, int64_t m, int d, int DP,
                               int64_t m_pad, int jx, unsigned short* out, const float* valid,
-                              hipStream_t s) {
+                              hipStream_t s, const int* qperm) {
   int64_t blocks = (m_pad * DP + 255) / 256;
   if (blocks > 16384) blocks = 16384;
   hipLaunchKernelGGL(prep_half_queries_kernel, dim3((unsigned)blocks), dim3(256), 0, s, Q64, mu, m,
-                     d, DP, m_pad, jx, out, valid);
+                     d, DP, m_pad, jx, out, valid, qperm);
 }
 
 // ---------------------------------- int8 images (kernel metric 5, d <= 256)
@@ -415,7 +420,7 @@ void launch_grid_stats(const double* X64, int64_t n, int d, double* partial, dou
 __global__ void __launch_bounds__(256)
 prep_i8_train_kernel(const double* __restrict__ X64, const double* __restrict__ cent, int64_t n,
                      int d, int DP, int64_t n_pad, int s, signed char* __restrict__ out,
-                     unsigned* __restrict__ codes_max, int swz) {
+                     unsigned* __restrict__ codes_max, int swz, const int* __restrict__ perm) {
   const int row_bytes = DP + 16;
   const int lane = threadIdx.x & 63;
   const int64_t wstride = (int64_t)gridDim.x * 4;
@@ -423,10 +428,11 @@ prep_i8_train_kernel(const double* __restrict__ X64, const double* __restrict__ 
   for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n_pad; row += wstride) {
     int q2 = 0;
     const int cx = swz ? xh_swz((int)(row & 15)) << 4 : 0;
+    const int64_t src = src_row(perm, row, n);
     for (int c = lane; c < DP; c += 64) {
       int k = 0;
       if (row < n && c < d) {
-        k = (int)__builtin_rint(__builtin_ldexp(X64[row * d + c], s) - cent[c]);
+        k = (int)__builtin_rint(__builtin_ldexp(X64[src * d + c], s) - cent[c]);
         q2 += k * k;
       }
       out[row * row_bytes + (c ^ cx)] = (signed char)k;
@@ -443,11 +449,11 @@ prep_i8_train_kernel(const double* __restrict__ X64, const double* __restrict__ 
 
 void launch_prep_i8_train(const double* X64, const double* cent, int64_t n, int d, int DP,
                           int64_t n_pad, int s, signed char* out, unsigned* codes_max, int swz,
-                          hipStream_t st) {
+                          hipStream_t st, const int* perm) {
   int64_t blocks = (n_pad + 3) / 4;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(prep_i8_train_kernel, dim3((unsigned)blocks), dim3(256), 0, st, X64, cent, n,
-                     d, DP, n_pad, s, out, codes_max, swz);
+                     d, DP, n_pad, s, out, codes_max, swz, perm);
 }
 
 // Query rows: int8 codes clamp(rint(q 2^s - c_i), -128, 127) (DP bytes,
@@ -458,15 +464,16 @@ void launch_prep_i8_train(const double* X64, const double* cent, int64_t n, int 
 __global__ void __launch_bounds__(256)
 prep_i8_queries_kernel(const double* __restrict__ Q64, const double* __restrict__ cent, int64_t m,
                        int d, int DP, int64_t m_pad, int s, signed char* __restrict__ out,
-                       float* __restrict__ valid) {
+                       float* __restrict__ valid, const int* __restrict__ qperm) {
   const int lane = threadIdx.x & 63;
   const int64_t wstride = (int64_t)gridDim.x * 4;
   for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < m_pad; row += wstride) {
-    const bool use = row < m && valid[row] > 0.0f;
+    const int64_t q = src_row(qperm, row, m);
+    const bool use = row < m && valid[q] > 0.0f;
     for (int c = lane; c < DP; c += 64) {
       int k = 0;
       if (use && c < d) {
-        const double y = __builtin_ldexp(Q64[row * d + c], s) - cent[c];
+        const double y = __builtin_ldexp(Q64[q * d + c], s) - cent[c];
         k = (int)__builtin_fmin(__builtin_fmax(__builtin_rint(y), -128.0), 127.0);
       }
       out[row * DP + c] = (signed char)k;
@@ -475,11 +482,12 @@ prep_i8_queries_kernel(const double* __restrict__ Q64, const double* __restrict_
 }
 
 void launch_prep_i8_queries(const double* Q64, const double* cent, int64_t m, int d, int DP,
-                            int64_t m_pad, int s, signed char* out, float* valid, hipStream_t st) {
+                            int64_t m_pad, int s, signed char* out, float* valid, hipStream_t st,
+                            const int* qperm) {
   int64_t blocks = (m_pad + 3) / 4;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(prep_i8_queries_kernel, dim3((unsigned)blocks), dim3(256), 0, st, Q64, cent, m,
-                     d, DP, m_pad, s, out, valid);
+                     d, DP, m_pad, s, out, valid, qperm);
 }
 
 __global__ void fill_i32_kernel(int32_t* p, int64_t n, int32_t v) {
@@ -555,7 +563,7 @@ prep_half_tiled_kernel(const double* __restrict__ X64, const double* __restrict_
                        int d, int DP, int64_t n_pad, int jx, double mult,
                        unsigned short* __restrict__ out, const float* __restrict__ seed_src,
                        float* __restrict__ seed_out, const float* __restrict__ valid,
-                       unsigned long long* __restrict__ dx2max) {
+                       unsigned long long* __restrict__ dx2max, const int* __restrict__ perm) {
   const int lane = threadIdx.x & 63;
   const int64_t wstride = (int64_t)gridDim.x * 4;
   const double sinv = __builtin_ldexp(1.0, -jx);
@@ -565,6 +573,7 @@ prep_half_tiled_kernel(const double* __restrict__ X64, const double* __restrict_
     const bool live = row < n && (!valid || valid[row] > 0.0f);
     const int64_t tile = row / kS3R;
     const int r = (int)(row - tile * kS3R);
+    const int64_t src = src_row(perm, row, n);
     double e2 = 0.0;
     for (int g = lane; g < G; g += 64) {
       unsigned short hv[8];
@@ -573,7 +582,7 @@ prep_half_tiled_kernel(const double* __restrict__ X64, const double* __restrict_
         const int col = 8 * g + u;
         _Float16 h = (_Float16)0.0f;
         if (live && col < d) {
-          const double x = X64[row * d + col] - mu[col];
+          const double x = X64[src * d + col] - mu[col];
           h = f16_operand(mult * x, jx);
           if (dx2max) {
             const double e = (double)h * sinv - x;
@@ -600,11 +609,11 @@ prep_half_tiled_kernel(const double* __restrict__ X64, const double* __restrict_
 void launch_prep_half_tiled(const double* X64, const double* mu, int64_t n, int d, int DP,
                             int64_t n_pad, int jx, double mult, unsigned short* out,
                             const float* seed_src, float* seed_out, const float* valid,
-                            unsigned long long* dx2max, hipStream_t s) {
+                            unsigned long long* dx2max, hipStream_t s, const int* perm) {
   int64_t blocks = (n_pad + 3) / 4;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(prep_half_tiled_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X64, mu, n, d,
-                     DP, n_pad, jx, mult, out, seed_src, seed_out, valid, dx2max);
+                     DP, n_pad, jx, mult, out, seed_src, seed_out, valid, dx2max, perm);
 }
 
 // ------------------------------- S3 images (bf16x3, DP > 256; knn_cand.hip)
@@ -613,7 +622,8 @@ void launch_prep_half_tiled(const double* X64, const double* mu, int64_t n, int 
 __global__ void __launch_bounds__(256)
 prep_split_tiled_kernel(const double* __restrict__ X64, const double* __restrict__ mu, int64_t n,
                         int d, int DP, int64_t n_pad, double scale, unsigned short* __restrict__ out,
-                        const float* __restrict__ seed_src, float* __restrict__ seed_out) {
+                        const float* __restrict__ seed_src, float* __restrict__ seed_out,
+                        const int* __restrict__ perm) {
   const int G = DP / 8;  // 8-dim groups per row
   const int nch = DP / kS3DC;
   const int64_t total = n_pad * G;
@@ -626,7 +636,8 @@ prep_split_tiled_kernel(const double* __restrict__ X64, const double* __restrict
     for (int u = 0; u < 8; ++u) {
       const int col = 8 * g + u;
       hi[u] = lo[u] = 0;
-      if (row < n && col < d) split_bf16(scale * (X64[row * d + col] - mu[col]), hi[u], lo[u]);
+      if (row < n && col < d)
+        split_bf16(scale * (X64[src_row(perm, row, n) * d + col] - mu[col]), hi[u], lo[u]);
     }
     const int64_t tile = row / kS3R;
     const int r = (int)(row - tile * kS3R);
@@ -645,11 +656,12 @@ prep_split_tiled_kernel(const double* __restrict__ X64, const double* __restrict
 
 void launch_prep_split_tiled(const double* X64, const double* mu, int64_t n, int d, int DP,
                              int64_t n_pad, double scale, unsigned short* out,
-                             const float* seed_src, float* seed_out, hipStream_t s) {
+                             const float* seed_src, float* seed_out, hipStream_t s,
+                             const int* perm) {
   int64_t blocks = (n_pad * (DP / 8) + 255) / 256;
   if (blocks > 16384) blocks = 16384;
   hipLaunchKernelGGL(prep_split_tiled_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X64, mu, n, d,
-                     DP, n_pad, scale, out, seed_src, seed_out);
+                     DP, n_pad, scale, out, seed_src, seed_out, perm);
 }
 
 }  // namespace knnk

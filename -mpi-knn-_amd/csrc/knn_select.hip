@@ -316,8 +316,10 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
     const bool void_q = !(vq > 0.0f);
     const bool nonfinite = vq < 0.0f;
     // union in registers; min over full lists of their R-th (worst kept) entry
-    const float* lv = cv + q * U;
-    const int* li = ci + q * U;
+    // (queries in region order: the query's lists sit at its position)
+    const int64_t qp = ps.qpos ? ps.qpos[q] : q;
+    const float* lv = cv + qp * U;
+    const int* li = ci + qp * U;
     float v[EPL];
     int id[EPL];
     float mlr = KNN_INF_F;
@@ -361,7 +363,7 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
       const unsigned long long mk = __ballot(sel);
       if (sel) {
         const int pos = cn + lanes_below(mk);
-        if (pos < Cmax) di[pos] = id[e];
+        if (pos < Cmax) di[pos] = train_row(t, id[e]);
       }
       cn += __popcll(mk);
     }
@@ -389,7 +391,7 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
           const unsigned long long mk = __ballot(sel);
           if (sel) {
             const int pos = cn + lanes_below(mk);
-            if (pos < Cmax) di[pos] = id[e];
+            if (pos < Cmax) di[pos] = train_row(t, id[e]);
           }
           cn += __popcll(mk);
         }
@@ -401,7 +403,7 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
     // (cand_kernel): rows it dropped have proxy >= its final value
     float tq = KNN_INF_F;
     if (gthr) {
-      const uint32_t* g = gthr + q * kGthrSlots;
+      const uint32_t* g = gthr + qp * kGthrSlots;
       uint32_t mk = g[0];
 #pragma unroll
       for (int e = 1; e < kGthrSlots; ++e) mk = max(mk, g[e]);
@@ -482,8 +484,8 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
           if (mk != ~0ull) {
             const double tau = dk[W - 1];
             for (int i = 0; i < cn; ++i) {
-              const int r = di[i];
-              const int sp = (int)(((int64_t)r / sm.trows) % sm.S);
+              const int r = di[i];  // (a train row; its split by its image position)
+              const int sp = (int)(((int64_t)(t.ipos ? t.ipos[r] : r) / sm.trows) % sm.S);
               if (dk[i] <= tau && !((mk >> sp) & 1)) sm.keep[(int64_t)f * kRescanCap + nk++] = r;
             }
           }
@@ -626,12 +628,14 @@ rescan_prep_kernel(TrainDev t, const double* __restrict__ Q64, const int* __rest
   }
 }
 
-// Appends row `row` to query s's list if its proxy passes.
+// Appends image row `row` (as its train row) to query s's list if its proxy
+// passes (pad rows never do: +inf seeds).
 __device__ __forceinline__ void rescan_append(float acc, float th, int s, int64_t row,
-                                              int* __restrict__ fcnt, int* __restrict__ buf) {
+                                              const TrainDev& t, int* __restrict__ fcnt,
+                                              int* __restrict__ buf) {
   if (acc <= th) {
     const int pos = atomicAdd(&fcnt[s], 1);
-    if (pos < kRescanCap) buf[(int64_t)s * kRescanCap + pos] = (int)row;
+    if (pos < kRescanCap) buf[(int64_t)s * kRescanCap + pos] = train_row(t, (int)row);
   }
 }
 
@@ -733,7 +737,7 @@ rescan_filter_kernel(TrainDev t, const float* __restrict__ qf, const float* __re
 #pragma unroll
       for (int qi = 0; qi < FQ; ++qi)
         if (qi < nfg && ((mask_s[qi] >> wsp) & 1))
-          rescan_append(acc[qi], thr_s[qi], g0 + qi, row0 + lane, fcnt, buf);
+          rescan_append(acc[qi], thr_s[qi], g0 + qi, row0 + lane, t, fcnt, buf);
     }
   }
   }  // row blocks
@@ -827,7 +831,7 @@ rescan_filter_wide_kernel(TrainDev t, const float* __restrict__ qf, const float*
 #pragma unroll
       for (int qi = 0; qi < FQ; ++qi)
         if (qi < nfg && ((mask_s[qi] >> bsp) & 1))
-          rescan_append(acc[qi], thr_s[qi], g0 + qi, row, fcnt, buf);
+          rescan_append(acc[qi], thr_s[qi], g0 + qi, row, t, fcnt, buf);
     }
   }
   }  // row blocks

@@ -299,7 +299,8 @@ class Classifier:
 
     def set_tuning(self, key, value):
         """Experiment overrides (knn_amd.h): "R", "S", "nw", "ablate", "fp16",
-        "mfma16", "i8", "gk", "s3q", "xhswz"; 0 (or -1 where stated) = automatic."""
+        "mfma16", "i8", "i8w", "gk", "s3q", "xhswz", "ties", "seed", "order"
+        ("order" before set_train); 0 (or -1 where stated) = automatic."""
         _check(lib().knn_set_tuning(self._h, key.encode(), int(value)))
 
     def last_candidate_path(self):

@@ -267,7 +267,12 @@ const char* knn_last_kernel_name(knn_ctx* ctx);
  * queries whose label it can change, 2 every query with a tie in its top k);
  * "seed" (experiment: seeded global thresholds of the fp16 / int8 resident
  * kernels from a pre-pass over N strided train rows; 0 / -1 off, the
- * default -- measured slower; results stay exact). */
+ * default -- measured slower; results stay exact); "order" (region order of
+ * the train images, read by knn_set_train*: -1 auto -- on at n >= 131072,
+ * d <= 256, one region per 32K rows up to 64 -- 0 off, 1 on, 2..64 that
+ * many regions; queries of the resident fp16 / int8 kernels are then sorted
+ * by region and each query tile's stream starts at its region; results stay
+ * exact). */
 int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value);
 
 /* Synchronise the context's stream. */

@@ -34,7 +34,8 @@ def knn():
     return mod
 
 
-@pytest.fixture(scope="module", params=["auto", "fp32", "m16", "fp16", "fp16w", "i8", "i8w"])
+@pytest.fixture(scope="module",
+                params=["auto", "fp32", "m16", "fp16", "fp16w", "i8", "i8w", "ord", "ordh"])
 def clf(knn, request):
     """Every parity test runs with the default candidate path (AUTO: int8 for
     integer-coded data and fp16 otherwise for batches of >= 4096 queries at
@@ -44,12 +45,16 @@ def clf(knn, request):
     kernel on 32x32x16 above 256 dims, the resident kernel publishing list
     thresholds, gk = 0), and with the int8 path forced wherever the data are
     integer-coded, on its AUTO kernel (i8) and on v_mfma_i32_32x32x32_i8 at
-    every width (i8w); other data take the AUTO path."""
+    every width (i8w); other data take the AUTO path.  ord / ordh: the train
+    images in region order (tuning "order" = 4 regions, knn_order.hip) with
+    the AUTO path and with fp16 forced: queries sorted by region, streams
+    starting at each query tile's region, lists mapped back to train rows."""
     c = knn.Classifier(0)
     c.set_precision({"auto": knn.PRECISION_AUTO, "fp32": knn.PRECISION_FP32,
                      "m16": knn.PRECISION_BF16X3, "fp16": knn.PRECISION_FP16,
                      "fp16w": knn.PRECISION_FP16, "i8": knn.PRECISION_AUTO,
-                     "i8w": knn.PRECISION_AUTO}[request.param])
+                     "i8w": knn.PRECISION_AUTO, "ord": knn.PRECISION_AUTO,
+                     "ordh": knn.PRECISION_FP16}[request.param])
     c.set_tuning("mfma16", 1 if request.param == "m16" else -1)
     if request.param in ("i8", "i8w"):
         c.set_tuning("i8", 1)
@@ -58,6 +63,8 @@ def clf(knn, request):
     if request.param == "fp16w":
         c.set_tuning("s3q", 0)
         c.set_tuning("gk", 0)
+    # (the train layout is decided at set_train: every case's own)
+    c.set_tuning("order", 4 if request.param in ("ord", "ordh") else 0)
     yield c
     c.close()
 
@@ -332,14 +339,17 @@ def test_int8_off_grid_queries(knn):
     c.close()
 
 
+@pytest.mark.parametrize("order", [0, 4])
 @pytest.mark.parametrize("path", ["i8", "i8w", "fp16", "s3"])
-def test_targeted_rescan(knn, path):
+def test_targeted_rescan(knn, path, order):
     """Per-split certification: with few splits (tuning S = 2, 3) a lane list
     often holds R of a query's top W, so its bound fails; the merge then
     flags only the splits whose own bound fails, hands the re-ranked rows of
     the others to the rescan, and the rescan scans just the flagged splits'
     rows (knn_select.hip).  Exact answers against the oracle on the int8
-    (grid data), fp16 (continuous data) and fp16 S3 (d = 300) paths."""
+    (grid data), fp16 (continuous data) and fp16 S3 (d = 300) paths, with the
+    train images in train order and in region order (order = 4: a split's
+    rows are then image positions, mapped back to train rows)."""
     rng = np.random.default_rng(123)
     if path in ("i8", "i8w"):
         tr, lab, te = _grid_codes(rng, 20000, 600, 64 if path == "i8" else 96, 6)
@@ -359,6 +369,7 @@ def test_targeted_rescan(knn, path):
         else:
             c.set_precision(knn.PRECISION_FP16)
         c.set_tuning("S", S)
+        c.set_tuning("order", order)
         run_case(c, knn, tr, lab, te, k, 0, 6)
         assert c.last_candidate_path() == {"i8": 5, "i8w": 6}.get(path, 4)
         assert c.last_geometry()["splits"] == S

@@ -30,12 +30,15 @@ def main():
     ap.add_argument("--d", type=int, default=128)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--data", default="grid", choices=("grid", "continuous"))
+    ap.add_argument("--order", type=int, default=-1,
+                    help="region order of the train layout (tuning key 'order', set before set_train)")
     ap.add_argument("variants", nargs="*", default=["auto:0:0", "auto:4:0", "auto:8:0", "fp32:0:0"])
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     knn = bench.load_knn()
     X, lab, Q, _ = bench.synth(a.n, a.m, a.d, 10, 1234, 5678, dev, data=a.data)
     clf = knn.Classifier(0)
+    clf.set_tuning("order", a.order)
     clf.set_train_device(X.data_ptr(), lab.data_ptr(), a.n, a.d, 10, keep=(X, lab))
     clf.set_timing(True)
     out = torch.empty(a.m, dtype=torch.int32, device=dev)
