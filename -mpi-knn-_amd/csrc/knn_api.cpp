@@ -175,13 +175,22 @@ static int detect_i8(knn_ctx* ctx, const double* dX, int64_t n, int d) {
 }
 
 // Region order of the train images (knn_order.hip): regions for n rows (0:
-// train order).  Auto: one region per 32K rows, at least 4 and at most 64
-// (a region then spans >= 128 tiles of 256 rows: several per split of a
-// 38-split launch), only where the resident kernels run (d <= 256).
+// train order).  Only where the resident kernels run (d <= 256).  Auto: 64
+// regions (at most one per 16K rows) where the candidate image fits the
+// 256 MB MALL with room to spare: with the order, a split's query tiles
+// start their streams at different rows and no longer share the staged
+// tiles in L2, so a larger image is re-read from HBM -- the 12.5M x 96
+// shard ran 12.11 -> 13.87 ms, cfg2 1.342 -> 1.266 ms (profiles/ab_log.md
+// r4i).  1: on at any size, 2..64: that many regions.
+constexpr int64_t kOrderMaxImage = 192ll << 20;
 static int region_count(const knn_ctx* ctx, int64_t n, int d) {
   if (ctx->tune_order == 0 || pad_dim_fp16(d) <= 0) return 0;
-  int P = (int)std::min<int64_t>(kRegionMax, n / 32768);
-  if (ctx->tune_order < 0) return P >= 4 ? P : 0;
+  int P = (int)std::min<int64_t>(kRegionMax, n / 16384);
+  if (ctx->tune_order < 0) {
+    const int64_t img = ctx->i8_ok && pad_dim_i8(d) > 0 ? n * (pad_dim_i8(d) + 16)
+                                                        : n * (2 * (int64_t)pad_dim_fp16(d) + 16);
+    return P >= 8 && img <= kOrderMaxImage ? P : 0;
+  }
   if (ctx->tune_order >= 2) P = (int)std::min<int64_t>(ctx->tune_order, kRegionMax);
   P = (int)std::min<int64_t>(P, n / 256);
   return P >= 2 ? P : 0;
@@ -196,6 +205,7 @@ static int build_order(knn_ctx* ctx, const double* dX, const double* mu, int64_t
   const int64_t nb = region_sort_blocks(n);
   int rc;
   if ((rc = ctx->ord_cent.ensure((size_t)kRegionMax * d * sizeof(float)))) return rc;
+  if ((rc = ctx->ord_cnorm.ensure(kRegionMax * sizeof(float)))) return rc;
   if ((rc = ctx->ord_rank.ensure(kRegionMax * sizeof(int)))) return rc;
   if ((rc = ctx->ord_rstart.ensure(kRegionMax * sizeof(int)))) return rc;
   if ((rc = ctx->ord_tot.ensure(kRegionMax * sizeof(int)))) return rc;
@@ -206,8 +216,10 @@ static int build_order(knn_ctx* ctx, const double* dX, const double* mu, int64_t
   float* cent = (float*)ctx->ord_cent.p;
   int* rank = (int*)ctx->ord_rank.p;
   int* key = (int*)ctx->ord_key.p;
-  launch_region_kmeans(dX, mu, ns, d, stride, jx, P, 8, cent, key, rank, ctx->stream);
-  launch_region_assign(dX, mu, n, d, 1, jx, cent, P, rank, key, ctx->stream);
+  launch_region_kmeans(dX, mu, ns, d, stride, jx, P, 8, cent, key, rank, (float*)ctx->ord_cnorm.p,
+                       ctx->stream);
+  launch_region_assign(dX, mu, n, d, 1, jx, cent, P, rank, key, ctx->stream,
+                       (const float*)ctx->ord_cnorm.p);
   launch_region_sort(key, n, (int*)ctx->ord_bcnt.p, (int*)ctx->ord_tot.p, (int*)ctx->ord_perm.p,
                      (int*)ctx->ord_ipos.p, nullptr, nullptr, (int*)ctx->ord_rstart.p, ctx->stream);
   HIP_TRY(hipGetLastError());
@@ -629,9 +641,10 @@ static void choose_geometry(knn_ctx* ctx, int metric, bool streamed, int DP, int
     // S3: prefer a split count that lets the XCD's concurrent workgroups
     // share staged chunks (s3_map; gq 4 over 2 over none) within the same fill
     if (streamed && DP > 256) {
-      int bq = s3_group(n_qt, bS);
-      for (int S = bS + 1; S <= S_hi && bq < 4; S++)
-        if (eff_of(S) >= best - 0.02 && s3_group(n_qt, S) > bq) { bS = S; bq = s3_group(n_qt, S); }
+      const int gmax = ctx->tune_s3gq > 0 ? ctx->tune_s3gq : kS3GqMax;
+      int bq = s3_group(n_qt, bS, gmax);
+      for (int S = bS + 1; S <= S_hi && bq < gmax; S++)
+        if (eff_of(S) >= best - 0.02 && s3_group(n_qt, S, gmax) > bq) { bS = S; bq = s3_group(n_qt, S, gmax); }
     }
     if (ctx->tune_S) bS = std::min(ctx->tune_S, S_hi);
     bestS = bS;
@@ -892,11 +905,12 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
     if ((rc = ctx->ord_qperm.ensure((size_t)m * sizeof(int)))) return rc;
     if ((rc = ctx->ord_qpos.ensure((size_t)m * sizeof(int)))) return rc;
     if ((rc = ctx->ord_qstart.ensure((size_t)m * sizeof(int)))) return rc;
-    launch_region_assign(dQ, t.mu, m, t.d, 1, t.jx, (const float*)ctx->ord_cent.p, ctx->ord_P,
-                         (const int*)ctx->ord_rank.p, (int*)ctx->ord_qkey.p, s);
-    launch_region_sort((const int*)ctx->ord_qkey.p, m, (int*)ctx->ord_bcnt.p, (int*)ctx->ord_tot.p,
-                       (int*)ctx->ord_qperm.p, (int*)ctx->ord_qpos.p,
-                       (const int*)ctx->ord_rstart.p, (int*)ctx->ord_qstart.p, nullptr, s);
+    launch_region_sort_queries(dQ, t.mu, m, t.d, t.jx, (const float*)ctx->ord_cent.p,
+                               (const float*)ctx->ord_cnorm.p, ctx->ord_P,
+                               (const int*)ctx->ord_rank.p, (const int*)ctx->ord_rstart.p,
+                               std::min(ctx->tune_ophase, ctx->ord_P), (int*)ctx->ord_bcnt.p,
+                               (int*)ctx->ord_tot.p, (int*)ctx->ord_qkey.p, (int*)ctx->ord_qperm.p,
+                               (int*)ctx->ord_qpos.p, (int*)ctx->ord_qstart.p, s);
     qperm = (const int*)ctx->ord_qperm.p;
     qpos = (const int*)ctx->ord_qpos.p;
     qstart = (const int*)ctx->ord_qstart.p;
@@ -975,11 +989,11 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   if (s3h)
     launch_cand_s3h((const unsigned short*)ctx->XT16.p, (const float*)ctx->XS16.p,
                     (const unsigned short*)ctx->Q32.p, DP, n_pad3, R, S, n_qt, cl.out_v, cl.out_i,
-                    cl.ablate, s3q, cl.gthr, gk, s);
+                    cl.ablate, s3q, cl.gthr, gk, s, ctx->tune_s3gq > 0 ? ctx->tune_s3gq : kS3GqMax);
   else if (s3)
     launch_cand_s3((const unsigned short*)ctx->XB.p, (const float*)ctx->XS.p,
                    (const unsigned short*)ctx->Q32.p, DP, n_pad3, R, S, n_qt, cl.out_v, cl.out_i,
-                   cl.ablate, s);
+                   cl.ablate, s, ctx->tune_s3gq > 0 ? ctx->tune_s3gq : kS3GqMax);
   else if (!launch_cand(cl, s))
     return knn_fail(KNN_ERR_ARG, "no candidate kernel for this geometry (tuning overrides?)");
   HIP_TRY(hipGetLastError());
@@ -1443,6 +1457,13 @@ int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value) {
   } else if (!strcmp(key, "seed")) {
     if (value < -1) return knn_fail(KNN_ERR_ARG, "seed must be 0 / -1 (off) or N = sample rows");
     ctx->tune_seed = value;
+  } else if (!strcmp(key, "s3gq")) {
+    if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8 && value != 16 && value != 32)
+      return knn_fail(KNN_ERR_ARG, "s3gq must be 0 (auto) or 1, 2, 4, 8, 16, 32");
+    ctx->tune_s3gq = (int)value;
+  } else if (!strcmp(key, "ophase")) {
+    if (value < 0 || value > kRegionMax) return knn_fail(KNN_ERR_ARG, "ophase must be 0..64");
+    ctx->tune_ophase = (int)value;
   } else if (!strcmp(key, "order")) {
     if (value < -1 || value > kRegionMax)
       return knn_fail(KNN_ERR_ARG, "order must be -1 (auto), 0, 1 or 2..64 regions");

@@ -249,7 +249,7 @@ __device__ __forceinline__ void s3_wait_barrier(int n) {
 }
 
 // Workgroup -> (query tile, split) of the S3 kernel.  gq = 0: XCD-contiguous
-// ranges (xcd_remap), splits outer.  gq in {1, 2, 4} (n_qt % gq == 0 and
+// ranges (xcd_remap), splits outer.  gq in {1, 2, 4, 8, 16, 32} (n_qt % gq == 0 and
 // S % (32 / gq) == 0): the 32 workgroups an XCD runs at once (one per CU,
 // workgroup w on XCD w % 8) form one group of gq query tiles x 32/gq splits,
 // so each step's staged chunks are shared in the XCD's L2 -- a row chunk by
@@ -615,17 +615,19 @@ int s3h_blocks_per_cu(int R) {
                 : occupancy_of(cand_s3_kernel<16, true, false>, 512);
 }
 
-// the S3 grouping (s3_map) that n_qt and S admit: 4, 2, 1, else 0
-int s3_group(int n_qt, int S) {
-  for (int gq : {4, 2, 1})
-    if (n_qt % gq == 0 && S % (32 / gq) == 0) return gq;
+// the S3 grouping (s3_map) that n_qt and S admit, the largest up to gq_max
+// (a row chunk then serves gq workgroups of the XCD, a query chunk 32 / gq):
+// 32, 16, 8, 4, 2, 1, else 0
+int s3_group(int n_qt, int S, int gq_max) {
+  for (int gq : {32, 16, 8, 4, 2, 1})
+    if (gq <= gq_max && n_qt % gq == 0 && S % (32 / gq) == 0) return gq;
   return 0;
 }
 
 void launch_cand_s3(const unsigned short* XT, const float* XS, const unsigned short* QT, int DP,
                     int64_t n_pad, int R, int S, int n_qt, float* out_v, int* out_i, int ablate,
-                    hipStream_t s) {
-  const int gq = s3_group(n_qt, S);
+                    hipStream_t s, int gq_max) {
+  const int gq = s3_group(n_qt, S, gq_max);
   const int nch = DP / kS3DC;
   const int n_tiles = (int)(n_pad / kS3R);
   if (R == 8)
@@ -638,8 +640,8 @@ void launch_cand_s3(const unsigned short* XT, const float* XS, const unsigned sh
 
 void launch_cand_s3h(const unsigned short* XT, const float* XS, const unsigned short* QT, int DP,
                      int64_t n_pad, int R, int S, int n_qt, float* out_v, int* out_i, int ablate,
-                     bool q16, uint32_t* gthr, int gk, hipStream_t s) {
-  const int gq = s3_group(n_qt, S);
+                     bool q16, uint32_t* gthr, int gk, hipStream_t s, int gq_max) {
+  const int gq = s3_group(n_qt, S, gq_max);
   const int nch = DP / 32;
   const int n_tiles = (int)(n_pad / kS3R);
   const dim3 g((unsigned)(n_qt * S)), b(512);

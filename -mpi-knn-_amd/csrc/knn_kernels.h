@@ -63,13 +63,15 @@ int pad_dim_bf16x3(int d);          // padded dim of the bf16x3 kernel, -1 if un
 int pad_dim_fp16(int d);            // padded dim of the fp16 kernel (metric 4), -1 if unsupported
 bool bf16x3_streamed(int DP);       // bf16x3 at this DP runs the S3 stream kernel
 constexpr int kS3Rows = 256;        // S3 kernel: train rows per tile = queries per workgroup
+constexpr int kS3GqMax = 4;         // S3: default largest XCD grouping of query tiles (s3_group)
 int s3_blocks_per_cu(int R);
 // S3 kernel (bf16x3, DP > 256): XT/QT are tile-chunk images made by
 // launch_prep_split_tiled, XS the per-row seeds [n_pad]; n_pad and m_pad are
 // multiples of kS3Rows.
+// gq_max: the largest XCD grouping of query tiles to use (s3_group)
 void launch_cand_s3(const unsigned short* XT, const float* XS, const unsigned short* QT, int DP,
                     int64_t n_pad, int R, int S, int n_qt, float* out_v, int* out_i, int ablate,
-                    hipStream_t s);
+                    hipStream_t s, int gq_max = kS3GqMax);
 // fp64 rows -> bf16 hi/lo tile-chunk images of scale*x (S3 layout); seed_out
 // (train only, else null) receives seed_src[row] (+inf on pad rows)
 void launch_prep_split_tiled(const double* X64, const double* mu, int64_t n, int d, int DP,
@@ -81,11 +83,11 @@ void launch_prep_split_tiled(const double* X64, const double* mu, int64_t n, int
 // gthr / gk: the global threshold exchange of the q16 form (null / 0: none)
 void launch_cand_s3h(const unsigned short* XT, const float* XS, const unsigned short* QT, int DP,
                      int64_t n_pad, int R, int S, int n_qt, float* out_v, int* out_i, int ablate,
-                     bool q16, uint32_t* gthr, int gk, hipStream_t s);
+                     bool q16, uint32_t* gthr, int gk, hipStream_t s, int gq_max = kS3GqMax);
 int s3h_blocks_per_cu(int R);
 int s3q_blocks_per_cu();
 // S3 workgroup grouping for n_qt query tiles and S splits (knn_cand.hip, s3_map)
-int s3_group(int n_qt, int S);
+int s3_group(int n_qt, int S, int gq_max = kS3GqMax);
 int pad_dim_fp16_s3(int d);         // padded dim of the fp16 S3 image (multiple of 32, > 256)
 // fp64 rows -> fp16 S3 tile-chunk images of mult * 2^jx (x - mu) (knn_prep.hip);
 // train: seed_out[row] = seed_src[row] (+inf on pad rows) and the running max
@@ -322,20 +324,32 @@ void launch_prep_split(const double* X64, const double* mu, int64_t n, int d, in
 // Region order (knn_order.hip).  Features are the fp32 operands 2^jx (x - mu).
 constexpr int kRegionMax = 64;  // regions (k-means centroids) at most
 // out[r] = rank[nearest centroid of row r * stride] (rank null: the centroid)
+// cnorm (nullable): the centroids' squared norms; bcnt (nullable, zeroed):
+// per-1024-row-block key counts
 void launch_region_assign(const double* X, const double* mu, int64_t n, int d, int64_t stride,
-                          int jx, const float* cent, int P, const int* rank, int* out, hipStream_t s);
+                          int jx, const float* cent, int P, const int* rank, int* out, hipStream_t s,
+                          const float* cnorm = nullptr, int* bcnt = nullptr);
 // k-means over ns sample rows (row i = X row i * stride): cent [P][d],
-// assign [ns] scratch, rank [P] = each centroid's place in the greedy chain
+// assign [ns] scratch, rank [P] = each centroid's place in the greedy chain,
+// cnorm [kRegionMax] the final centroids' squared norms
 void launch_region_kmeans(const double* X, const double* mu, int64_t ns, int d, int64_t stride,
                           int jx, int P, int iters, float* cent, int* assign, int* rank,
-                          hipStream_t s);
+                          float* cnorm, hipStream_t s);
 // Stable counting sort of n keys in [0, kRegionMax): bcnt holds
 // region_sort_blocks(n) x kRegionMax ints, tot kRegionMax; outputs (nullable)
-// perm[pos] = i, ipos[i] = pos, qstart[pos] = rstart[key], bases[k] = the
-// first position of key k
+// perm[pos] = i, ipos[i] = pos, qstart[pos] = rstart[key] (phases > 0: of
+// the first key of the key's group, P keys in `phases` groups), bases[k] =
+// the first position of key k
 int64_t region_sort_blocks(int64_t n);
 void launch_region_sort(const int* key, int64_t n, int* bcnt, int* tot, int* perm, int* ipos,
-                        const int* rstart, int* qstart, int* bases, hipStream_t s);
+                        const int* rstart, int* qstart, int* bases, hipStream_t s, int P = 1,
+                        int phases = 0);
+// Per call: queries assigned to regions and counting-sorted (qperm / qpos /
+// qstart as above); bcnt region_sort_blocks(m) x kRegionMax ints
+void launch_region_sort_queries(const double* Q, const double* mu, int64_t m, int d, int jx,
+                                const float* cent, const float* cnorm, int P, const int* rank,
+                                const int* rstart, int phases, int* bcnt, int* tot, int* qkey,
+                                int* qperm, int* qpos, int* qstart, hipStream_t s);
 
 // Min-max normalisation (knn_normalize.hip, cpp:229-306).  R = rows per
 // grid sweep; `partial` holds 2*d*R doubles.  launch_minmax folds the set's

@@ -33,10 +33,14 @@ constexpr int kOrdDC = 32;  // dims per staged chunk of the assignment kernel
 // block (lane = row), score_p = ||c_p||^2 - 2 x.c_p; the lowest score wins,
 // the lowest p on ties.  Centroids transposed in LDS ([d][64]: one 16-B
 // broadcast read per 4 centroids); out[r] = rank[p] (rank null: p).
+// cnorm (nullable): the centroids' ||c||^2 (+inf past P), else computed here.
+// bcnt (nullable, zeroed): per 1024-row block, the count of each output key
+// (the histogram of the counting sort, launch_region_sort_queries).
 __global__ void __launch_bounds__(256)
 region_assign_kernel(const double* __restrict__ X, const double* __restrict__ mu, int64_t n, int d,
                      int64_t stride, int jx, const float* __restrict__ cent, int P,
-                     const int* __restrict__ rank, int* __restrict__ out) {
+                     const int* __restrict__ rank, int* __restrict__ out,
+                     const float* __restrict__ cnorm, int* __restrict__ bcnt) {
   __shared__ __attribute__((aligned(16))) float cT[256 * kRegionMax];
   __shared__ float tile[64 * (kOrdDC + 1)];
   __shared__ float cn[kRegionMax];
@@ -50,7 +54,9 @@ region_assign_kernel(const double* __restrict__ X, const double* __restrict__ mu
   __syncthreads();
   if (tid < kRegionMax) {
     float s = 0.0f;
-    for (int c = 0; c < d; ++c) s = __builtin_fmaf(cT[c * kRegionMax + tid], cT[c * kRegionMax + tid], s);
+    if (cnorm) s = cnorm[tid];
+    else
+      for (int c = 0; c < d; ++c) s = __builtin_fmaf(cT[c * kRegionMax + tid], cT[c * kRegionMax + tid], s);
     cn[tid] = tid < P ? s : KNN_INF_F;
   }
   const int64_t r0 = (int64_t)blockIdx.x * 64;
@@ -105,7 +111,9 @@ region_assign_kernel(const double* __restrict__ X, const double* __restrict__ mu
         p = bp[w][lane];
       }
     if (p == 0x7fffffff) p = 0;  // no finite score (a query beyond fp32 range)
-    out[r0 + lane] = rank ? rank[p] : p;
+    const int key = rank ? rank[p] : p;
+    out[r0 + lane] = key;
+    if (bcnt) atomicAdd(&bcnt[((r0 + lane) >> 10) * kRegionMax + key], 1);
   }
 }
 
@@ -146,10 +154,18 @@ __global__ void region_init_kernel(const double* __restrict__ X, const double* _
 
 // Greedy chain over the P centroids (one wave, lane = centroid): start at
 // the centroid farthest from centroid 0, then repeatedly the nearest
-// unvisited one; rank[p] = its position in the chain.
+// unvisited one; rank[p] = its position in the chain.  cnorm[p] = ||c_p||^2
+// (+inf past P), in the assignment kernel's summation order.
 __global__ void __launch_bounds__(64)
-region_chain_kernel(const float* __restrict__ cent, int P, int d, int* __restrict__ rank) {
+region_chain_kernel(const float* __restrict__ cent, int P, int d, int* __restrict__ rank,
+                    float* __restrict__ cnorm) {
   const int p = threadIdx.x;
+  {
+    float s = 0.0f;
+    if (p < P)
+      for (int c = 0; c < d; ++c) s = __builtin_fmaf(cent[(int64_t)p * d + c], cent[(int64_t)p * d + c], s);
+    cnorm[p] = p < P ? s : KNN_INF_F;
+  }
   auto dist_to = [&](int cur) {
     float s = KNN_INF_F;
     if (p < P) {
@@ -243,18 +259,38 @@ sort_scan_kernel(int* __restrict__ bcnt, int64_t nb, int* __restrict__ tot) {
 }
 
 // pos = (keys before k in total) + (key k in earlier blocks) + (key k
-// earlier in this block).  Outputs (each nullable): perm[pos] = i,
-// ipos[i] = pos, qstart[pos] = rstart[k]; bases (block 0) = the exclusive
-// prefix of tot (the start position of each key).
+// earlier in this block).  inl > 0: bcnt holds the blocks' plain counts
+// (nb = inl blocks, the query sort): each block sums the earlier blocks'
+// counts and the totals itself instead of reading sort_scan_kernel's
+// prefixes.  Outputs (each nullable): perm[pos] = i,
+// ipos[i] = pos, qstart[pos] = rstart[k] (phases > 0: rstart of the first
+// key of k's group, keys split into `phases` groups of P / phases: query
+// tiles of one group share their streams' start); bases (block 0) = the
+// exclusive prefix of tot (the start position of each key).
 __global__ void __launch_bounds__(kSortB)
 sort_scatter_kernel(const int* __restrict__ key, int64_t n, const int* __restrict__ bcnt,
                     const int* __restrict__ tot, int* __restrict__ perm, int* __restrict__ ipos,
-                    const int* __restrict__ rstart, int* __restrict__ qstart, int* __restrict__ bases) {
+                    const int* __restrict__ rstart, int* __restrict__ qstart, int* __restrict__ bases,
+                    int P, int phases, int inl) {
   __shared__ int base[kRegionMax];
+  __shared__ int boff[kRegionMax];
   __shared__ int wc[kSortB / 64][kRegionMax];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (tid < 64) {
-    const int v = tid < kRegionMax ? tot[tid] : 0;
+    int v;
+    if (inl > 0) {
+      int before = 0, all = 0;
+      for (int b = 0; b < inl; ++b) {
+        const int c = bcnt[(int64_t)b * kRegionMax + tid];
+        all += c;
+        if (b < (int)blockIdx.x) before += c;
+      }
+      boff[tid] = before;
+      v = all;
+    } else {
+      v = tot[tid];
+      boff[tid] = bcnt[(int64_t)blockIdx.x * kRegionMax + tid];
+    }
     int x = v;
     for (int o = 1; o < 64; o <<= 1) {
       const int y = __shfl_up(x, o, 64);
@@ -281,25 +317,26 @@ sort_scatter_kernel(const int* __restrict__ key, int64_t n, const int* __restric
   if (valid && r == 0) wc[wv][k] = __popcll(m);
   __syncthreads();
   if (!valid) return;
-  int pos = base[k] + bcnt[(int64_t)blockIdx.x * kRegionMax + k] + r;
+  int pos = base[k] + boff[k] + r;
   for (int w = 0; w < wv; ++w) pos += wc[w][k];
   if (perm) perm[pos] = (int)i;
   if (ipos) ipos[i] = pos;
-  if (qstart) qstart[pos] = rstart[k];
+  if (qstart) qstart[pos] = rstart[phases > 0 ? ((k * phases / P) * P + phases - 1) / phases : k];
 }
 
 int64_t region_sort_blocks(int64_t n) { return (n + kSortB - 1) / kSortB; }
 
 void launch_region_assign(const double* X, const double* mu, int64_t n, int d, int64_t stride,
-                          int jx, const float* cent, int P, const int* rank, int* out, hipStream_t s) {
+                          int jx, const float* cent, int P, const int* rank, int* out, hipStream_t s,
+                          const float* cnorm, int* bcnt) {
   if (n <= 0) return;
   hipLaunchKernelGGL(region_assign_kernel, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, s, X, mu,
-                     n, d, stride, jx, cent, P, rank, out);
+                     n, d, stride, jx, cent, P, rank, out, cnorm, bcnt);
 }
 
 void launch_region_kmeans(const double* X, const double* mu, int64_t ns, int d, int64_t stride,
                           int jx, int P, int iters, float* cent, int* assign, int* rank,
-                          hipStream_t s) {
+                          float* cnorm, hipStream_t s) {
   hipLaunchKernelGGL(region_init_kernel, dim3(P), dim3(256), 0, s, X, mu, ns, d, stride, jx, P,
                      cent);
   for (int it = 0; it < iters; ++it) {
@@ -307,17 +344,38 @@ void launch_region_kmeans(const double* X, const double* mu, int64_t ns, int d, 
     hipLaunchKernelGGL(region_update_kernel, dim3(P), dim3(256), 0, s, X, mu, ns, d, stride, jx,
                        assign, cent);
   }
-  hipLaunchKernelGGL(region_chain_kernel, dim3(1), dim3(64), 0, s, cent, P, d, rank);
+  hipLaunchKernelGGL(region_chain_kernel, dim3(1), dim3(64), 0, s, cent, P, d, rank, cnorm);
 }
 
 void launch_region_sort(const int* key, int64_t n, int* bcnt, int* tot, int* perm, int* ipos,
-                        const int* rstart, int* qstart, int* bases, hipStream_t s) {
+                        const int* rstart, int* qstart, int* bases, hipStream_t s, int P,
+                        int phases) {
   if (n <= 0) return;
   const int64_t nb = region_sort_blocks(n);
   hipLaunchKernelGGL(sort_hist_kernel, dim3((unsigned)nb), dim3(kSortB), 0, s, key, n, bcnt);
   hipLaunchKernelGGL(sort_scan_kernel, dim3(kRegionMax), dim3(kSortB), 0, s, bcnt, nb, tot);
   hipLaunchKernelGGL(sort_scatter_kernel, dim3((unsigned)nb), dim3(kSortB), 0, s, key, n, bcnt, tot,
-                     perm, ipos, rstart, qstart, bases);
+                     perm, ipos, rstart, qstart, bases, P, phases, 0);
+}
+
+// The per-call query order: assignment with the sort's histogram fused in,
+// then the scatter (which sums the block counts itself up to 64 blocks, i.e.
+// 64K queries; beyond, the scan kernel runs between).
+void launch_region_sort_queries(const double* Q, const double* mu, int64_t m, int d, int jx,
+                                const float* cent, const float* cnorm, int P, const int* rank,
+                                const int* rstart, int phases, int* bcnt, int* tot, int* qkey,
+                                int* qperm, int* qpos, int* qstart, hipStream_t s) {
+  if (m <= 0) return;
+  const int64_t nb = region_sort_blocks(m);
+  launch_fill_i32(bcnt, nb * kRegionMax, 0, s);
+  launch_region_assign(Q, mu, m, d, 1, jx, cent, P, rank, qkey, s, cnorm, bcnt);
+  int inl = (int)nb;
+  if (nb > 64) {
+    hipLaunchKernelGGL(sort_scan_kernel, dim3(kRegionMax), dim3(kSortB), 0, s, bcnt, nb, tot);
+    inl = 0;
+  }
+  hipLaunchKernelGGL(sort_scatter_kernel, dim3((unsigned)nb), dim3(kSortB), 0, s, qkey, m, bcnt, tot,
+                     qperm, qpos, rstart, qstart, nullptr, P, phases, inl);
 }
 
 }  // namespace knnk

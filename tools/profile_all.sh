@@ -5,7 +5,7 @@
 #          HBM section; each pass its own run, --kernel-trace only)
 #   api    rocprofv3 --hip-trace of a short cfg2 bench: the HIP calls made
 #          inside the timed knn_classify_device loop (no stream syncs)
-# Usage: TAG=r2 tools/profile_all.sh [stats] [pmc] [api] [cfg4] [cfg5]
+# Usage: TAG=r2 tools/profile_all.sh [stats] [pmc] [api] [cfg4] [cfg4s] [cfg5]
 # Outputs under gpurun_out/prof_$TAG/; tools/profiles_commit.py turns them
 # into the committed profiles/ files.  Every GPU step has its own time limit
 # and a failing step ends the script.
@@ -19,6 +19,8 @@ declare -A WL
 WL[cfg2]="--steps 10 --warmup 2"
 WL[cfg4]="--steps 3 --warmup 1 --mode train --n-train 100000000 --dim 96 --queries 10000"
 WL[cfg5]="--steps 4 --warmup 1 --dim 960 --k 100"
+# configs[3] at the 8-GPU shard size (100M / 8 rows per rank)
+WL[cfg4s]="--steps 5 --warmup 1 --mode train --n-train 12500000 --dim 96 --queries 10000"
 run() {  # run <name> <limit> <cmd...>
   local name=$1 lim=$2; shift 2
   echo "== $name"
@@ -29,7 +31,7 @@ run() {  # run <name> <limit> <cmd...>
   [ $rc -eq 0 ] || exit $rc
 }
 cfgs="cfg2"
-for a in "$@"; do case $a in cfg4|cfg5) cfgs="$cfgs $a" ;; esac; done
+for a in "$@"; do case $a in cfg4|cfg5|cfg4s) cfgs="$cfgs $a" ;; esac; done
 for a in "$@"; do
   case $a in
     stats)

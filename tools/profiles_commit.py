@@ -35,6 +35,7 @@ WORKLOADS = {
     "cfg2": dict(steps=10, warmup=2, n_train=1_000_000, queries=10_000, dim=128, k=10),
     "cfg4": dict(steps=3, warmup=1, n_train=100_000_000, queries=10_000, dim=96, k=10),
     "cfg5": dict(steps=4, warmup=1, n_train=1_000_000, queries=10_000, dim=960, k=100),
+    "cfg4s": dict(steps=5, warmup=1, n_train=12_500_000, queries=10_000, dim=96, k=10),
 }
 
 
