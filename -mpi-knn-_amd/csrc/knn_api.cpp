@@ -176,20 +176,21 @@ static int detect_i8(knn_ctx* ctx, const double* dX, int64_t n, int d) {
 
 // Region order of the train images (knn_order.hip): regions for n rows (0:
 // train order).  Only where the resident kernels run (d <= 256).  Auto: 64
-// regions (at most one per 16K rows) where the candidate image fits the
-// 256 MB MALL with room to spare: with the order, a split's query tiles
-// start their streams at different rows and no longer share the staged
-// tiles in L2, so a larger image is re-read from HBM -- the 12.5M x 96
-// shard ran 12.11 -> 13.87 ms, cfg2 1.342 -> 1.266 ms (profiles/ab_log.md
-// r4i).  1: on at any size, 2..64: that many regions.
+// regions (at most one per 16K rows) for integer-coded train sets (the int8
+// pass) whose image fits the 256 MB MALL with room to spare.  With the
+// order, a split's query tiles start their streams at different rows and no
+// longer share the staged tiles in L2, so a larger image is re-read from
+// HBM: the 12.5M x 96 shard ran 12.11 -> 13.87 ms, cfg2 1.342 -> 1.266 ms,
+// 1M x 128 x 100K queries 13.16 -> 11.47 ms; the fp16 pass on continuous
+// data gained nothing (2.343 / 2.342 ms; profiles/ab_log.md r4i, r4j).
+// 1: on at any size, 2..64: that many regions.
 constexpr int64_t kOrderMaxImage = 192ll << 20;
 static int region_count(const knn_ctx* ctx, int64_t n, int d) {
   if (ctx->tune_order == 0 || pad_dim_fp16(d) <= 0) return 0;
   int P = (int)std::min<int64_t>(kRegionMax, n / 16384);
   if (ctx->tune_order < 0) {
-    const int64_t img = ctx->i8_ok && pad_dim_i8(d) > 0 ? n * (pad_dim_i8(d) + 16)
-                                                        : n * (2 * (int64_t)pad_dim_fp16(d) + 16);
-    return P >= 8 && img <= kOrderMaxImage ? P : 0;
+    const bool i8 = ctx->i8_ok && pad_dim_i8(d) > 0;
+    return i8 && P >= 8 && n * (pad_dim_i8(d) + 16) <= kOrderMaxImage ? P : 0;
   }
   if (ctx->tune_order >= 2) P = (int)std::min<int64_t>(ctx->tune_order, kRegionMax);
   P = (int)std::min<int64_t>(P, n / 256);
@@ -206,6 +207,7 @@ static int build_order(knn_ctx* ctx, const double* dX, const double* mu, int64_t
   int rc;
   if ((rc = ctx->ord_cent.ensure((size_t)kRegionMax * d * sizeof(float)))) return rc;
   if ((rc = ctx->ord_cnorm.ensure(kRegionMax * sizeof(float)))) return rc;
+  if ((rc = ctx->ord_centT.ensure((size_t)kRegionMax * d * sizeof(float)))) return rc;
   if ((rc = ctx->ord_rank.ensure(kRegionMax * sizeof(int)))) return rc;
   if ((rc = ctx->ord_rstart.ensure(kRegionMax * sizeof(int)))) return rc;
   if ((rc = ctx->ord_tot.ensure(kRegionMax * sizeof(int)))) return rc;
@@ -217,9 +219,9 @@ static int build_order(knn_ctx* ctx, const double* dX, const double* mu, int64_t
   int* rank = (int*)ctx->ord_rank.p;
   int* key = (int*)ctx->ord_key.p;
   launch_region_kmeans(dX, mu, ns, d, stride, jx, P, 8, cent, key, rank, (float*)ctx->ord_cnorm.p,
-                       ctx->stream);
+                       (float*)ctx->ord_centT.p, ctx->stream);
   launch_region_assign(dX, mu, n, d, 1, jx, cent, P, rank, key, ctx->stream,
-                       (const float*)ctx->ord_cnorm.p);
+                       (const float*)ctx->ord_cnorm.p, (const float*)ctx->ord_centT.p);
   launch_region_sort(key, n, (int*)ctx->ord_bcnt.p, (int*)ctx->ord_tot.p, (int*)ctx->ord_perm.p,
                      (int*)ctx->ord_ipos.p, nullptr, nullptr, (int*)ctx->ord_rstart.p, ctx->stream);
   HIP_TRY(hipGetLastError());
@@ -906,7 +908,8 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
     if ((rc = ctx->ord_qpos.ensure((size_t)m * sizeof(int)))) return rc;
     if ((rc = ctx->ord_qstart.ensure((size_t)m * sizeof(int)))) return rc;
     launch_region_sort_queries(dQ, t.mu, m, t.d, t.jx, (const float*)ctx->ord_cent.p,
-                               (const float*)ctx->ord_cnorm.p, ctx->ord_P,
+                               (const float*)ctx->ord_cnorm.p, (const float*)ctx->ord_centT.p,
+                               ctx->ord_P,
                                (const int*)ctx->ord_rank.p, (const int*)ctx->ord_rstart.p,
                                std::min(ctx->tune_ophase, ctx->ord_P), (int*)ctx->ord_bcnt.p,
                                (int*)ctx->ord_tot.p, (int*)ctx->ord_qkey.p, (int*)ctx->ord_qperm.p,

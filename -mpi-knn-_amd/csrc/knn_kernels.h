@@ -328,13 +328,15 @@ constexpr int kRegionMax = 64;  // regions (k-means centroids) at most
 // per-1024-row-block key counts
 void launch_region_assign(const double* X, const double* mu, int64_t n, int d, int64_t stride,
                           int jx, const float* cent, int P, const int* rank, int* out, hipStream_t s,
-                          const float* cnorm = nullptr, int* bcnt = nullptr);
+                          const float* cnorm = nullptr, const float* centT = nullptr,
+                          int* bcnt = nullptr);
 // k-means over ns sample rows (row i = X row i * stride): cent [P][d],
 // assign [ns] scratch, rank [P] = each centroid's place in the greedy chain,
-// cnorm [kRegionMax] the final centroids' squared norms
+// cnorm [kRegionMax] the final centroids' squared norms, centT [d][kRegionMax]
+// the final centroids transposed (zero past P)
 void launch_region_kmeans(const double* X, const double* mu, int64_t ns, int d, int64_t stride,
                           int jx, int P, int iters, float* cent, int* assign, int* rank,
-                          float* cnorm, hipStream_t s);
+                          float* cnorm, float* centT, hipStream_t s);
 // Stable counting sort of n keys in [0, kRegionMax): bcnt holds
 // region_sort_blocks(n) x kRegionMax ints, tot kRegionMax; outputs (nullable)
 // perm[pos] = i, ipos[i] = pos, qstart[pos] = rstart[key] (phases > 0: of
@@ -347,7 +349,8 @@ void launch_region_sort(const int* key, int64_t n, int* bcnt, int* tot, int* per
 // Per call: queries assigned to regions and counting-sorted (qperm / qpos /
 // qstart as above); bcnt region_sort_blocks(m) x kRegionMax ints
 void launch_region_sort_queries(const double* Q, const double* mu, int64_t m, int d, int jx,
-                                const float* cent, const float* cnorm, int P, const int* rank,
+                                const float* cent, const float* cnorm, const float* centT, int P,
+                                const int* rank,
                                 const int* rstart, int phases, int* bcnt, int* tot, int* qkey,
                                 int* qperm, int* qpos, int* qstart, hipStream_t s);
 

@@ -33,23 +33,31 @@ constexpr int kOrdDC = 32;  // dims per staged chunk of the assignment kernel
 // block (lane = row), score_p = ||c_p||^2 - 2 x.c_p; the lowest score wins,
 // the lowest p on ties.  Centroids transposed in LDS ([d][64]: one 16-B
 // broadcast read per 4 centroids); out[r] = rank[p] (rank null: p).
-// cnorm (nullable): the centroids' ||c||^2 (+inf past P), else computed here.
+// cnorm (nullable): the centroids' ||c||^2 (+inf past P), else computed here;
+// centT (nullable, with cnorm): the centroids already transposed, [d][64]
+// (zero past P) -- one coalesced copy instead of the strided gather.
 // bcnt (nullable, zeroed): per 1024-row block, the count of each output key
 // (the histogram of the counting sort, launch_region_sort_queries).
 __global__ void __launch_bounds__(256)
 region_assign_kernel(const double* __restrict__ X, const double* __restrict__ mu, int64_t n, int d,
                      int64_t stride, int jx, const float* __restrict__ cent, int P,
                      const int* __restrict__ rank, int* __restrict__ out,
-                     const float* __restrict__ cnorm, int* __restrict__ bcnt) {
+                     const float* __restrict__ cnorm, const float* __restrict__ centT,
+                     int* __restrict__ bcnt) {
   __shared__ __attribute__((aligned(16))) float cT[256 * kRegionMax];
   __shared__ float tile[64 * (kOrdDC + 1)];
   __shared__ float cn[kRegionMax];
   __shared__ float bs[4][64];
   __shared__ int bp[4][64];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int e = tid; e < d * kRegionMax; e += 256) {
-    const int c = e / kRegionMax, p = e - c * kRegionMax;
-    cT[e] = p < P ? cent[(int64_t)p * d + c] : 0.0f;
+  if (centT) {
+    for (int e = tid; e < d * kRegionMax / 4; e += 256)
+      ((float4*)cT)[e] = ((const float4*)centT)[e];
+  } else {
+    for (int e = tid; e < d * kRegionMax; e += 256) {
+      const int c = e / kRegionMax, p = e - c * kRegionMax;
+      cT[e] = p < P ? cent[(int64_t)p * d + c] : 0.0f;
+    }
   }
   __syncthreads();
   if (tid < kRegionMax) {
@@ -158,12 +166,15 @@ __global__ void region_init_kernel(const double* __restrict__ X, const double* _
 // (+inf past P), in the assignment kernel's summation order.
 __global__ void __launch_bounds__(64)
 region_chain_kernel(const float* __restrict__ cent, int P, int d, int* __restrict__ rank,
-                    float* __restrict__ cnorm) {
+                    float* __restrict__ cnorm, float* __restrict__ centT) {
   const int p = threadIdx.x;
   {
     float s = 0.0f;
-    if (p < P)
-      for (int c = 0; c < d; ++c) s = __builtin_fmaf(cent[(int64_t)p * d + c], cent[(int64_t)p * d + c], s);
+    for (int c = 0; c < d; ++c) {
+      const float v = p < P ? cent[(int64_t)p * d + c] : 0.0f;
+      s = __builtin_fmaf(v, v, s);
+      centT[c * kRegionMax + p] = v;
+    }
     cnorm[p] = p < P ? s : KNN_INF_F;
   }
   auto dist_to = [&](int cur) {
@@ -280,10 +291,11 @@ sort_scatter_kernel(const int* __restrict__ key, int64_t n, const int* __restric
     int v;
     if (inl > 0) {
       int before = 0, all = 0;
+#pragma unroll 8
       for (int b = 0; b < inl; ++b) {
         const int c = bcnt[(int64_t)b * kRegionMax + tid];
         all += c;
-        if (b < (int)blockIdx.x) before += c;
+        before += b < (int)blockIdx.x ? c : 0;
       }
       boff[tid] = before;
       v = all;
@@ -328,15 +340,15 @@ int64_t region_sort_blocks(int64_t n) { return (n + kSortB - 1) / kSortB; }
 
 void launch_region_assign(const double* X, const double* mu, int64_t n, int d, int64_t stride,
                           int jx, const float* cent, int P, const int* rank, int* out, hipStream_t s,
-                          const float* cnorm, int* bcnt) {
+                          const float* cnorm, const float* centT, int* bcnt) {
   if (n <= 0) return;
   hipLaunchKernelGGL(region_assign_kernel, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, s, X, mu,
-                     n, d, stride, jx, cent, P, rank, out, cnorm, bcnt);
+                     n, d, stride, jx, cent, P, rank, out, cnorm, centT, bcnt);
 }
 
 void launch_region_kmeans(const double* X, const double* mu, int64_t ns, int d, int64_t stride,
                           int jx, int P, int iters, float* cent, int* assign, int* rank,
-                          float* cnorm, hipStream_t s) {
+                          float* cnorm, float* centT, hipStream_t s) {
   hipLaunchKernelGGL(region_init_kernel, dim3(P), dim3(256), 0, s, X, mu, ns, d, stride, jx, P,
                      cent);
   for (int it = 0; it < iters; ++it) {
@@ -344,7 +356,7 @@ void launch_region_kmeans(const double* X, const double* mu, int64_t ns, int d, 
     hipLaunchKernelGGL(region_update_kernel, dim3(P), dim3(256), 0, s, X, mu, ns, d, stride, jx,
                        assign, cent);
   }
-  hipLaunchKernelGGL(region_chain_kernel, dim3(1), dim3(64), 0, s, cent, P, d, rank, cnorm);
+  hipLaunchKernelGGL(region_chain_kernel, dim3(1), dim3(64), 0, s, cent, P, d, rank, cnorm, centT);
 }
 
 void launch_region_sort(const int* key, int64_t n, int* bcnt, int* tot, int* perm, int* ipos,
@@ -362,13 +374,14 @@ void launch_region_sort(const int* key, int64_t n, int* bcnt, int* tot, int* per
 // then the scatter (which sums the block counts itself up to 64 blocks, i.e.
 // 64K queries; beyond, the scan kernel runs between).
 void launch_region_sort_queries(const double* Q, const double* mu, int64_t m, int d, int jx,
-                                const float* cent, const float* cnorm, int P, const int* rank,
+                                const float* cent, const float* cnorm, const float* centT, int P,
+                                const int* rank,
                                 const int* rstart, int phases, int* bcnt, int* tot, int* qkey,
                                 int* qperm, int* qpos, int* qstart, hipStream_t s) {
   if (m <= 0) return;
   const int64_t nb = region_sort_blocks(m);
   launch_fill_i32(bcnt, nb * kRegionMax, 0, s);
-  launch_region_assign(Q, mu, m, d, 1, jx, cent, P, rank, qkey, s, cnorm, bcnt);
+  launch_region_assign(Q, mu, m, d, 1, jx, cent, P, rank, qkey, s, cnorm, centT, bcnt);
   int inl = (int)nb;
   if (nb > 64) {
     hipLaunchKernelGGL(sort_scan_kernel, dim3(kRegionMax), dim3(kSortB), 0, s, bcnt, nb, tot);

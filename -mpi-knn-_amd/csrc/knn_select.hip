@@ -363,7 +363,7 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
       const unsigned long long mk = __ballot(sel);
       if (sel) {
         const int pos = cn + lanes_below(mk);
-        if (pos < Cmax) di[pos] = train_row(t, id[e]);
+        if (pos < Cmax) di[pos] = id[e];
       }
       cn += __popcll(mk);
     }
@@ -391,13 +391,23 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
           const unsigned long long mk = __ballot(sel);
           if (sel) {
             const int pos = cn + lanes_below(mk);
-            if (pos < Cmax) di[pos] = train_row(t, id[e]);
+            if (pos < Cmax) di[pos] = id[e];
           }
           cn += __popcll(mk);
         }
       }
       cn = min(cn, Cmax);
       lbx = key2f(pre);
+    }
+    if (t.perm) {
+      // image positions -> train rows (region order), one batch of
+      // independent loads (the wave's own LDS writes above complete first)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      const int nsel = min(cn, Cmax);
+      for (int i = lane; i < nsel; i += 64) di[i] = t.perm[di[i]];
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
     }
     // the candidate kernel also filtered with the query's global threshold
     // (cand_kernel): rows it dropped have proxy >= its final value

@@ -4,7 +4,8 @@ the same labels, neighbour indices and fp64 distances, bit for bit, with
 the region order off, automatic and at 64 regions, on the int8 kernels
 (16x16x64 at d = 128, 32x32x32 at d = 96) and the fp16 kernel; a slice of
 the queries also against the CPU oracle.  Sizes put the automatic choice
-above its threshold (n >= 131072: 12 regions at n = 200000)."""
+above its threshold on the int8 paths (12 regions at n = 200000; the fp16 case
+forces 64)."""
 import numpy as np
 import pytest
 
