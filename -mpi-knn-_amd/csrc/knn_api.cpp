@@ -207,7 +207,7 @@ static int build_order(knn_ctx* ctx, const double* dX, const double* mu, int64_t
   int rc;
   if ((rc = ctx->ord_cent.ensure((size_t)kRegionMax * d * sizeof(float)))) return rc;
   if ((rc = ctx->ord_cnorm.ensure(kRegionMax * sizeof(float)))) return rc;
-  if ((rc = ctx->ord_centT.ensure((size_t)kRegionMax * d * sizeof(float)))) return rc;
+  if ((rc = ctx->ord_img.ensure(kRegionImgBytes))) return rc;
   if ((rc = ctx->ord_rank.ensure(kRegionMax * sizeof(int)))) return rc;
   if ((rc = ctx->ord_rstart.ensure(kRegionMax * sizeof(int)))) return rc;
   if ((rc = ctx->ord_tot.ensure(kRegionMax * sizeof(int)))) return rc;
@@ -218,10 +218,10 @@ static int build_order(knn_ctx* ctx, const double* dX, const double* mu, int64_t
   float* cent = (float*)ctx->ord_cent.p;
   int* rank = (int*)ctx->ord_rank.p;
   int* key = (int*)ctx->ord_key.p;
-  launch_region_kmeans(dX, mu, ns, d, stride, jx, P, 8, cent, key, rank, (float*)ctx->ord_cnorm.p,
-                       (float*)ctx->ord_centT.p, ctx->stream);
-  launch_region_assign(dX, mu, n, d, 1, jx, cent, P, rank, key, ctx->stream,
-                       (const float*)ctx->ord_cnorm.p, (const float*)ctx->ord_centT.p);
+  launch_region_kmeans(dX, mu, ns, d, stride, jx, P, 8, cent, (unsigned short*)ctx->ord_img.p,
+                       (float*)ctx->ord_cnorm.p, key, rank, ctx->stream);
+  launch_region_assign(dX, mu, n, d, 1, jx, (const unsigned short*)ctx->ord_img.p,
+                       (const float*)ctx->ord_cnorm.p, rank, key, nullptr, ctx->stream);
   launch_region_sort(key, n, (int*)ctx->ord_bcnt.p, (int*)ctx->ord_tot.p, (int*)ctx->ord_perm.p,
                      (int*)ctx->ord_ipos.p, nullptr, nullptr, (int*)ctx->ord_rstart.p, ctx->stream);
   HIP_TRY(hipGetLastError());
@@ -907,9 +907,8 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
     if ((rc = ctx->ord_qperm.ensure((size_t)m * sizeof(int)))) return rc;
     if ((rc = ctx->ord_qpos.ensure((size_t)m * sizeof(int)))) return rc;
     if ((rc = ctx->ord_qstart.ensure((size_t)m * sizeof(int)))) return rc;
-    launch_region_sort_queries(dQ, t.mu, m, t.d, t.jx, (const float*)ctx->ord_cent.p,
-                               (const float*)ctx->ord_cnorm.p, (const float*)ctx->ord_centT.p,
-                               ctx->ord_P,
+    launch_region_sort_queries(dQ, t.mu, m, t.d, t.jx, (const unsigned short*)ctx->ord_img.p,
+                               (const float*)ctx->ord_cnorm.p, ctx->ord_P,
                                (const int*)ctx->ord_rank.p, (const int*)ctx->ord_rstart.p,
                                std::min(ctx->tune_ophase, ctx->ord_P), (int*)ctx->ord_bcnt.p,
                                (int*)ctx->ord_tot.p, (int*)ctx->ord_qkey.p, (int*)ctx->ord_qperm.p,

@@ -96,7 +96,7 @@ struct knn_ctx {
   DevBuf smp_x64, smp_xl2, smp_img, smp_scr, smp_v, smp_i;
   // region order: centroids [P][d], chain ranks, region starts, image
   // position <-> train row maps; k-means / sort scratch; per-call query order
-  DevBuf ord_cent, ord_cnorm, ord_centT, ord_rank, ord_rstart, ord_perm, ord_ipos, ord_key, ord_bcnt, ord_tot, ord_qkey,
+  DevBuf ord_cent, ord_cnorm, ord_img, ord_rank, ord_rstart, ord_perm, ord_ipos, ord_key, ord_bcnt, ord_tot, ord_qkey,
       ord_qperm, ord_qpos, ord_qstart;
   // per-classify workspace
   DevBuf Q64, Q32, qvalid, cand_v, cand_i, gthr, rescan_q, rescan_tau, rescan_cnt, fr_cnt, fr_buf,
@@ -115,7 +115,7 @@ struct knn_ctx {
             &gthr,    &rescan_q, &rescan_tau, &rescan_cnt, &fr_cnt, &fr_buf, &fr_q, &fr_thr,
             &slow_q,  &totals,  &lk, &mrg, &tie_q, &tie_ws, &o_lab, &o_idx, &o_dist, &o_flags, &nrm_part, &nrm_mm, &nrm_X,
             &rescan_mask, &rescan_nkeep, &smp_x64, &smp_xl2, &smp_img, &smp_scr, &smp_v, &smp_i,
-            &ord_cent, &ord_cnorm, &ord_centT, &ord_rank, &ord_rstart, &ord_perm, &ord_ipos, &ord_key, &ord_bcnt, &ord_tot,
+            &ord_cent, &ord_cnorm, &ord_img, &ord_rank, &ord_rstart, &ord_perm, &ord_ipos, &ord_key, &ord_bcnt, &ord_tot,
             &ord_qkey, &ord_qperm, &ord_qpos, &ord_qstart};
   }
 };

@@ -324,19 +324,20 @@ void launch_prep_split(const double* X64, const double* mu, int64_t n, int d, in
 // Region order (knn_order.hip).  Features are the fp32 operands 2^jx (x - mu).
 constexpr int kRegionMax = 64;  // regions (k-means centroids) at most
 // out[r] = rank[nearest centroid of row r * stride] (rank null: the centroid)
-// cnorm (nullable): the centroids' squared norms; bcnt (nullable, zeroed):
-// per-1024-row-block key counts
+// Assignment on bf16 MFMA against a centroid image (launch_region_kmeans):
+// out[r] = rank[nearest centroid of row r * stride] (rank null: the centroid);
+// bcnt (nullable, zeroed): per-1024-row-block key counts
+constexpr int kRegionImgBytes = 2 * 16 * 32 * 16 * 2;  // centroid image at d <= 256
 void launch_region_assign(const double* X, const double* mu, int64_t n, int d, int64_t stride,
-                          int jx, const float* cent, int P, const int* rank, int* out, hipStream_t s,
-                          const float* cnorm = nullptr, const float* centT = nullptr,
-                          int* bcnt = nullptr);
-// k-means over ns sample rows (row i = X row i * stride): cent [P][d],
-// assign [ns] scratch, rank [P] = each centroid's place in the greedy chain,
-// cnorm [kRegionMax] the final centroids' squared norms, centT [d][kRegionMax]
-// the final centroids transposed (zero past P)
+                          int jx, const unsigned short* img, const float* cnorm, const int* rank, int* out,
+                          int* bcnt, hipStream_t s);
+// k-means over ns sample rows (row i = X row i * stride): cent [P][d], img /
+// cnorm the final centroids' bf16 image (kRegionImgBytes) and squared norms
+// [kRegionMax], assign [ns] scratch, rank [P] = each centroid's place in the
+// greedy chain
 void launch_region_kmeans(const double* X, const double* mu, int64_t ns, int d, int64_t stride,
-                          int jx, int P, int iters, float* cent, int* assign, int* rank,
-                          float* cnorm, float* centT, hipStream_t s);
+                          int jx, int P, int iters, float* cent, unsigned short* img, float* cnorm,
+                          int* assign, int* rank, hipStream_t s);
 // Stable counting sort of n keys in [0, kRegionMax): bcnt holds
 // region_sort_blocks(n) x kRegionMax ints, tot kRegionMax; outputs (nullable)
 // perm[pos] = i, ipos[i] = pos, qstart[pos] = rstart[key] (phases > 0: of
@@ -349,8 +350,7 @@ void launch_region_sort(const int* key, int64_t n, int* bcnt, int* tot, int* per
 // Per call: queries assigned to regions and counting-sorted (qperm / qpos /
 // qstart as above); bcnt region_sort_blocks(m) x kRegionMax ints
 void launch_region_sort_queries(const double* Q, const double* mu, int64_t m, int d, int jx,
-                                const float* cent, const float* cnorm, const float* centT, int P,
-                                const int* rank,
+                                const unsigned short* img, const float* cnorm, int P, const int* rank,
                                 const int* rstart, int phases, int* bcnt, int* tot, int* qkey,
                                 int* qperm, int* qpos, int* qstart, hipStream_t s);
 

@@ -24,104 +24,112 @@
 
 namespace knnk {
 
-constexpr int kOrdDC = 32;  // dims per staged chunk of the assignment kernel
+// Centroid image of the assignment kernel: the P <= 64 centroids (fp32,
+// 2^jx-scaled) as bf16 A fragments of v_mfma_f32_32x32x16_bf16, [block b of
+// 32 centroids][k-step s of 16 dims][row r][16 dims] (zero past P and d),
+// and their fp32 squared norms (+inf past P).  One wave, lane = centroid.
+__global__ void __launch_bounds__(64)
+region_image_kernel(const float* __restrict__ cent, int P, int d, __bf16* __restrict__ img,
+                    float* __restrict__ cnorm) {
+  const int p = threadIdx.x, b = p >> 5, r = p & 31;
+  const int DS = (d + 15) / 16;
+  float s = 0.0f;
+  for (int c = 0; c < DS * 16; ++c) {
+    const float v = p < P && c < d ? cent[(int64_t)p * d + c] : 0.0f;
+    s = __builtin_fmaf(v, v, s);
+    img[((b * DS + (c >> 4)) * 32 + r) * 16 + (c & 15)] = (__bf16)v;
+  }
+  cnorm[p] = p < P ? s : KNN_INF_F;
+}
 
-// Nearest centroid of rows r = 0..n-1 (source row r * stride of X, as the
-// fp32 operands 2^jx (x - mu) of every candidate path -- any assignment is
-// valid, only locality matters).  Block = 64
-// rows x 4 waves; wave w scores centroids 16w .. 16w+15 for every row of the
-// block (lane = row), score_p = ||c_p||^2 - 2 x.c_p; the lowest score wins,
-// the lowest p on ties.  Centroids transposed in LDS ([d][64]: one 16-B
-// broadcast read per 4 centroids); out[r] = rank[p] (rank null: p).
-// cnorm (nullable): the centroids' ||c||^2 (+inf past P), else computed here;
-// centT (nullable, with cnorm): the centroids already transposed, [d][64]
-// (zero past P) -- one coalesced copy instead of the strided gather.
-// bcnt (nullable, zeroed): per 1024-row block, the count of each output key
-// (the histogram of the counting sort, launch_region_sort_queries).
-__global__ void __launch_bounds__(256)
+// Nearest centroid of rows r = 0..n-1 (source row r * stride of X), as the
+// fp32 operands 2^jx (x - mu) of every candidate path rounded to bf16 -- any
+// assignment is valid, only locality matters, so the scores
+// ||c||^2 - 2 x.c run on the matrix cores.  Block = 32 rows, 2 waves: the
+// rows are staged into LDS as bf16 first (coalesced loads, 16 in flight per
+// thread), then wave b multiplies them (B operand: lane (j, h) row j, dims
+// 16s + 8h .. +7 of k-step s) with centroid block b (A: 32 centroids); lane
+// (j, h) of wave b ends with the scores of centroids 32b + (i & 3) +
+// 8 (i >> 2) + 4h (the 32x32 C layout); the lowest over both lanes of row j
+// and both waves wins, the lowest centroid on ties.  out[r] = rank[p] (rank
+// null: p); bcnt (nullable, zeroed): per 1024-row block, the count of each
+// output key (the counting sort's histogram).
+// DS = k-steps of 16 dims (compile time: the staging and the MFMA loop
+// unroll completely, every load in flight at once).
+constexpr int kAsgRows = 32;
+constexpr int kAsgStride = 256 + 8;  // bf16 per staged row (d <= 256; 16-B aligned, conflict-reducing pad)
+template <int DS>
+__global__ void __launch_bounds__(128)
 region_assign_kernel(const double* __restrict__ X, const double* __restrict__ mu, int64_t n, int d,
-                     int64_t stride, int jx, const float* __restrict__ cent, int P,
-                     const int* __restrict__ rank, int* __restrict__ out,
-                     const float* __restrict__ cnorm, const float* __restrict__ centT,
-                     int* __restrict__ bcnt) {
-  __shared__ __attribute__((aligned(16))) float cT[256 * kRegionMax];
-  __shared__ float tile[64 * (kOrdDC + 1)];
-  __shared__ float cn[kRegionMax];
-  __shared__ float bs[4][64];
-  __shared__ int bp[4][64];
+                     int64_t stride, int jx, const __bf16* __restrict__ img,
+                     const float* __restrict__ cnorm, const int* __restrict__ rank,
+                     int* __restrict__ out, int* __restrict__ bcnt) {
+  __shared__ __attribute__((aligned(16))) __bf16 xs[kAsgRows * kAsgStride];
+  __shared__ float bs[2][kAsgRows];
+  __shared__ int bpi[2][kAsgRows];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (centT) {
-    for (int e = tid; e < d * kRegionMax / 4; e += 256)
-      ((float4*)cT)[e] = ((const float4*)centT)[e];
-  } else {
-    for (int e = tid; e < d * kRegionMax; e += 256) {
-      const int c = e / kRegionMax, p = e - c * kRegionMax;
-      cT[e] = p < P ? cent[(int64_t)p * d + c] : 0.0f;
-    }
+  const int j = lane & 31, h = lane >> 5;
+  constexpr int dp = DS * 16;
+  const int64_t r0 = (int64_t)blockIdx.x * kAsgRows;
+  constexpr int total = kAsgRows * dp;  // a multiple of 128
+  // (a constant trip count: the loop unrolls and every load is in flight
+  // before the first conversion)
+#pragma unroll
+  for (int i = 0; i < total / 128; ++i) {
+    const int e = tid + 128 * i;
+    const int rr = e / dp, c = e - rr * dp;
+    // unconditional loads at clamped addresses (no branch per load: all of
+    // them issue before the first wait), the padding zeroed after
+    const bool ok = r0 + rr < n && c < d;
+    const int64_t ri = r0 + rr < n ? r0 + rr : n - 1;
+    const int ci = c < d ? c : d - 1;
+    const float v = (float)__builtin_ldexp(X[ri * stride * d + ci] - mu[ci], jx);
+    xs[rr * kAsgStride + c] = (__bf16)(ok ? v : 0.0f);
   }
+  // this lane's 16 centroid norms, loaded before the MFMAs
+  float cn[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) cn[i] = cnorm[32 * wv + (i & 3) + 8 * (i >> 2) + 4 * h];
   __syncthreads();
-  if (tid < kRegionMax) {
-    float s = 0.0f;
-    if (cnorm) s = cnorm[tid];
-    else
-      for (int c = 0; c < d; ++c) s = __builtin_fmaf(cT[c * kRegionMax + tid], cT[c * kRegionMax + tid], s);
-    cn[tid] = tid < P ? s : KNN_INF_F;
-  }
-  const int64_t r0 = (int64_t)blockIdx.x * 64;
-  float acc[16];
+  f32x16 acc;
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
-  for (int c0 = 0; c0 < d; c0 += kOrdDC) {
-    __syncthreads();  // the previous chunk's reads of tile are done
+  const bf16x8* A = (const bf16x8*)img;  // 16-B fragments: [b][s][r][2]
 #pragma unroll
-    for (int u = 0; u < 64 * kOrdDC / 256; ++u) {
-      const int e = tid + 256 * u, rr = e / kOrdDC, cc = e - rr * kOrdDC;
-      float v = 0.0f;
-      if (r0 + rr < n && c0 + cc < d)
-        v = (float)__builtin_ldexp(X[(r0 + rr) * stride * d + c0 + cc] - mu[c0 + cc], jx);
-      tile[rr * (kOrdDC + 1) + cc] = v;
-    }
-    __syncthreads();
-    const int nc = min(kOrdDC, d - c0);
-    for (int cc = 0; cc < nc; ++cc) {
-      const float x = tile[lane * (kOrdDC + 1) + cc];
-      const float4* cr = (const float4*)(cT + (c0 + cc) * kRegionMax + 16 * wv);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float4 c4 = cr[u];
-        acc[4 * u] = __builtin_fmaf(x, c4.x, acc[4 * u]);
-        acc[4 * u + 1] = __builtin_fmaf(x, c4.y, acc[4 * u + 1]);
-        acc[4 * u + 2] = __builtin_fmaf(x, c4.z, acc[4 * u + 2]);
-        acc[4 * u + 3] = __builtin_fmaf(x, c4.w, acc[4 * u + 3]);
-      }
-    }
+  for (int st = 0; st < DS; ++st) {
+    const bf16x8 bq = *(const bf16x8*)(xs + j * kAsgStride + 16 * st + 8 * h);
+    const bf16x8 a = A[((wv * DS + st) * 32 + j) * 2 + h];
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bq, acc, 0, 0, 0);
   }
   float best = KNN_INF_F;
-  int bpi = 0x7fffffff;
+  int bp = 0x7fffffff;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    const int p = 16 * wv + i;
-    const float s = cn[p] - 2.0f * acc[i];
-    if (p < P && (s < best || bpi == 0x7fffffff)) {
-      best = s;
-      bpi = p;
+    const int p = 32 * wv + (i & 3) + 8 * (i >> 2) + 4 * h;
+    const float sc = cn[i] - 2.0f * acc[i];
+    if (sc < best || (sc == best && p < bp)) {
+      best = sc;
+      bp = p;
     }
   }
-  bs[wv][lane] = best;
-  bp[wv][lane] = bpi;
+  const float ob = __shfl_xor(best, 32, 64);
+  const int op = __shfl_xor(bp, 32, 64);
+  if (ob < best || (ob == best && op < bp)) {
+    best = ob;
+    bp = op;
+  }
+  if (h == 0) {
+    bs[wv][j] = best;
+    bpi[wv][j] = bp;
+  }
   __syncthreads();
-  if (wv == 0 && r0 + lane < n) {
-    float b = bs[0][lane];
-    int p = bp[0][lane];
-    for (int w = 1; w < 4; ++w)
-      if (bp[w][lane] != 0x7fffffff && (p == 0x7fffffff || bs[w][lane] < b)) {
-        b = bs[w][lane];
-        p = bp[w][lane];
-      }
-    if (p == 0x7fffffff) p = 0;  // no finite score (a query beyond fp32 range)
-    const int key = rank ? rank[p] : p;
-    out[r0 + lane] = key;
-    if (bcnt) atomicAdd(&bcnt[((r0 + lane) >> 10) * kRegionMax + key], 1);
+  const int64_t row = r0 + j;
+  if (wv == 0 && h == 0 && row < n) {
+    if (bpi[1][j] != 0x7fffffff && (bp == 0x7fffffff || bs[1][j] < best)) bp = bpi[1][j];
+    if (bp == 0x7fffffff) bp = 0;  // no finite score (a query beyond fp32 range)
+    const int key = rank ? rank[bp] : bp;
+    out[row] = key;
+    if (bcnt) atomicAdd(&bcnt[(row >> 10) * kRegionMax + key], 1);
   }
 }
 
@@ -162,21 +170,10 @@ __global__ void region_init_kernel(const double* __restrict__ X, const double* _
 
 // Greedy chain over the P centroids (one wave, lane = centroid): start at
 // the centroid farthest from centroid 0, then repeatedly the nearest
-// unvisited one; rank[p] = its position in the chain.  cnorm[p] = ||c_p||^2
-// (+inf past P), in the assignment kernel's summation order.
+// unvisited one; rank[p] = its position in the chain.
 __global__ void __launch_bounds__(64)
-region_chain_kernel(const float* __restrict__ cent, int P, int d, int* __restrict__ rank,
-                    float* __restrict__ cnorm, float* __restrict__ centT) {
+region_chain_kernel(const float* __restrict__ cent, int P, int d, int* __restrict__ rank) {
   const int p = threadIdx.x;
-  {
-    float s = 0.0f;
-    for (int c = 0; c < d; ++c) {
-      const float v = p < P ? cent[(int64_t)p * d + c] : 0.0f;
-      s = __builtin_fmaf(v, v, s);
-      centT[c * kRegionMax + p] = v;
-    }
-    cnorm[p] = p < P ? s : KNN_INF_F;
-  }
   auto dist_to = [&](int cur) {
     float s = KNN_INF_F;
     if (p < P) {
@@ -339,24 +336,35 @@ sort_scatter_kernel(const int* __restrict__ key, int64_t n, const int* __restric
 int64_t region_sort_blocks(int64_t n) { return (n + kSortB - 1) / kSortB; }
 
 void launch_region_assign(const double* X, const double* mu, int64_t n, int d, int64_t stride,
-                          int jx, const float* cent, int P, const int* rank, int* out, hipStream_t s,
-                          const float* cnorm, const float* centT, int* bcnt) {
+                          int jx, const unsigned short* img, const float* cnorm, const int* rank, int* out,
+                          int* bcnt, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(region_assign_kernel, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, s, X, mu,
-                     n, d, stride, jx, cent, P, rank, out, cnorm, centT, bcnt);
+  const dim3 g((unsigned)((n + kAsgRows - 1) / kAsgRows)), b(128);
+  const __bf16* im = (const __bf16*)img;
+  switch ((d + 15) / 16) {
+#define KNN_ASG(D_) \
+    case D_: hipLaunchKernelGGL(region_assign_kernel<D_>, g, b, 0, s, X, mu, n, d, stride, jx, im, cnorm, rank, out, bcnt); break;
+    KNN_ASG(1) KNN_ASG(2) KNN_ASG(3) KNN_ASG(4) KNN_ASG(5) KNN_ASG(6) KNN_ASG(7) KNN_ASG(8)
+    KNN_ASG(9) KNN_ASG(10) KNN_ASG(11) KNN_ASG(12) KNN_ASG(13) KNN_ASG(14) KNN_ASG(15) KNN_ASG(16)
+#undef KNN_ASG
+    default: break;  // (d > 256: no region order, region_count)
+  }
 }
 
 void launch_region_kmeans(const double* X, const double* mu, int64_t ns, int d, int64_t stride,
-                          int jx, int P, int iters, float* cent, int* assign, int* rank,
-                          float* cnorm, float* centT, hipStream_t s) {
+                          int jx, int P, int iters, float* cent, unsigned short* img_u, float* cnorm,
+                          int* assign, int* rank, hipStream_t s) {
+  __bf16* img = (__bf16*)img_u;
   hipLaunchKernelGGL(region_init_kernel, dim3(P), dim3(256), 0, s, X, mu, ns, d, stride, jx, P,
                      cent);
   for (int it = 0; it < iters; ++it) {
-    launch_region_assign(X, mu, ns, d, stride, jx, cent, P, nullptr, assign, s);
+    hipLaunchKernelGGL(region_image_kernel, dim3(1), dim3(64), 0, s, cent, P, d, img, cnorm);
+    launch_region_assign(X, mu, ns, d, stride, jx, img_u, cnorm, nullptr, assign, nullptr, s);
     hipLaunchKernelGGL(region_update_kernel, dim3(P), dim3(256), 0, s, X, mu, ns, d, stride, jx,
                        assign, cent);
   }
-  hipLaunchKernelGGL(region_chain_kernel, dim3(1), dim3(64), 0, s, cent, P, d, rank, cnorm, centT);
+  hipLaunchKernelGGL(region_image_kernel, dim3(1), dim3(64), 0, s, cent, P, d, img, cnorm);
+  hipLaunchKernelGGL(region_chain_kernel, dim3(1), dim3(64), 0, s, cent, P, d, rank);
 }
 
 void launch_region_sort(const int* key, int64_t n, int* bcnt, int* tot, int* perm, int* ipos,
@@ -374,14 +382,13 @@ void launch_region_sort(const int* key, int64_t n, int* bcnt, int* tot, int* per
 // then the scatter (which sums the block counts itself up to 64 blocks, i.e.
 // 64K queries; beyond, the scan kernel runs between).
 void launch_region_sort_queries(const double* Q, const double* mu, int64_t m, int d, int jx,
-                                const float* cent, const float* cnorm, const float* centT, int P,
-                                const int* rank,
+                                const unsigned short* img, const float* cnorm, int P, const int* rank,
                                 const int* rstart, int phases, int* bcnt, int* tot, int* qkey,
                                 int* qperm, int* qpos, int* qstart, hipStream_t s) {
   if (m <= 0) return;
   const int64_t nb = region_sort_blocks(m);
   launch_fill_i32(bcnt, nb * kRegionMax, 0, s);
-  launch_region_assign(Q, mu, m, d, 1, jx, cent, P, rank, qkey, s, cnorm, centT, bcnt);
+  launch_region_assign(Q, mu, m, d, 1, jx, img, cnorm, rank, qkey, bcnt, s);
   int inl = (int)nb;
   if (nb > 64) {
     hipLaunchKernelGGL(sort_scan_kernel, dim3(kRegionMax), dim3(kSortB), 0, s, bcnt, nb, tot);
