@@ -310,7 +310,8 @@ def test_int8_codes(knn, d, i8w):
             c.set_tuning("i8", 1)
         run_case(c, knn, tr, lab, te, 10, 0, 7)
         assert c.last_candidate_path() == km, mode
-        assert c.last_kernel_name().startswith("cand_kernel<%d,4,%d,8>" % (dp, km))
+        # (metric 6 keeps 8-entry lists by default, knn_api.cpp)
+        assert c.last_kernel_name().startswith("cand_kernel<%d,%d,%d,8>" % (dp, 8 if km == 6 else 4, km))
         assert c.last_rescan_count() * 16 <= te.shape[0]
         c.close()
 

@@ -81,10 +81,12 @@ def test_no_kernel_spills_more_than_a_few_registers(tmp_path):
 
 
 def test_fp16_resident_kernels_fit_4_waves(tmp_path):
-    # cand_kernel<DP, 4, 4 | 5 | 6, NW> (the fp16 / int8 default paths): <= 128
-    # registers per lane (VGPR + AGPR) so two 8-wave workgroups share a CU
+    # cand_kernel<DP, 4, 4 | 5 | 6, NW> and <DP, 8, 6, NW> (the fp16 / int8
+    # default paths): <= 128 registers per lane (VGPR + AGPR) so two 8-wave
+    # workgroups share a CU
     meta = kernel_metadata(str(tmp_path))
-    fp16 = {k: v for k, v in meta.items() if re.search(r"cand_kernelILi\d+ELi4ELi[456]ELi8E", k)}
+    fp16 = {k: v for k, v in meta.items()
+            if re.search(r"cand_kernelILi\d+ELi4ELi[456]ELi8E|cand_kernelILi\d+ELi8ELi6ELi8E", k)}
     assert fp16, "no fp16 resident kernels found"
     for k, v in fp16.items():
         dp = int(re.search(r"cand_kernelILi(\d+)E", k).group(1))
