@@ -14,7 +14,7 @@ export TMPDIR=/tmp
 TAG=${TAG:-r2}
 OUT=$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
-BENCH_COMMON="--no-cpu-baseline --no-fp32-path --no-continuous --cfg3-queries 0 --no-dropin --no-train-sharded"
+BENCH_COMMON="--no-cpu-baseline --no-fp32-path --no-continuous --cfg3-queries 0 --no-dropin --no-train-sharded --no-cfg5"
 declare -A WL
 WL[cfg2]="--steps 10 --warmup 2"
 WL[cfg4]="--steps 3 --warmup 1 --mode train --n-train 100000000 --dim 96 --queries 10000"
