@@ -185,6 +185,13 @@ static int detect_i8(knn_ctx* ctx, const double* dX, int64_t n, int d) {
 // data gained nothing (2.343 / 2.342 ms; profiles/ab_log.md r4i, r4j).
 // 1: on at any size, 2..64: that many regions.
 constexpr int64_t kOrderMaxImage = 192ll << 20;
+// Query tiles start their streams at one of 8 phases of the region chain
+// (the first region of their region's eighth), not at their own region:
+// tiles of one phase share the staged tiles in L2 again -- cfg2 candidate
+// 1.212 -> 1.209 ms, L2-miss traffic 1.94 -> 1.34 GB per launch; 4 phases
+// 1.250 ms (profiles/ab_log.md r4p).  Tuning key "ophase": -1 auto, 0 the
+// tile's own region, N phases.
+constexpr int kOrderPhases = 8;
 static int region_count(const knn_ctx* ctx, int64_t n, int d) {
   if (ctx->tune_order == 0 || pad_dim_fp16(d) <= 0) return 0;
   int P = (int)std::min<int64_t>(kRegionMax, n / 16384);
@@ -910,7 +917,8 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
     launch_region_sort_queries(dQ, t.mu, m, t.d, t.jx, (const unsigned short*)ctx->ord_img.p,
                                (const float*)ctx->ord_cnorm.p, ctx->ord_P,
                                (const int*)ctx->ord_rank.p, (const int*)ctx->ord_rstart.p,
-                               std::min(ctx->tune_ophase, ctx->ord_P), (int*)ctx->ord_bcnt.p,
+                               std::min(ctx->tune_ophase < 0 ? kOrderPhases : ctx->tune_ophase, ctx->ord_P),
+                               (int*)ctx->ord_bcnt.p,
                                (int*)ctx->ord_tot.p, (int*)ctx->ord_qkey.p, (int*)ctx->ord_qperm.p,
                                (int*)ctx->ord_qpos.p, (int*)ctx->ord_qstart.p, s);
     qperm = (const int*)ctx->ord_qperm.p;
@@ -1464,7 +1472,7 @@ int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value) {
       return knn_fail(KNN_ERR_ARG, "s3gq must be 0 (auto) or 1, 2, 4, 8, 16, 32");
     ctx->tune_s3gq = (int)value;
   } else if (!strcmp(key, "ophase")) {
-    if (value < 0 || value > kRegionMax) return knn_fail(KNN_ERR_ARG, "ophase must be 0..64");
+    if (value < -1 || value > kRegionMax) return knn_fail(KNN_ERR_ARG, "ophase must be -1 (auto) .. 64");
     ctx->tune_ophase = (int)value;
   } else if (!strcmp(key, "order")) {
     if (value < -1 || value > kRegionMax)

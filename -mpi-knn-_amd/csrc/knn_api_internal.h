@@ -73,7 +73,9 @@ struct knn_ctx {
   int tune_order = -1;
   int ord_P = 0;               // regions of the current train layout (0: train order)
   int tune_s3gq = 0;           // S3 kernel: largest XCD query-tile grouping (0 = kS3GqMax)
-  int tune_ophase = 0;         // query streams start at the region (0) or at one of N phases
+  // query streams start at one of N phases of the region chain (P regions in
+  // N groups; -1 auto = 8, 0 = at the query tile's own region)
+  int tune_ophase = -1;
   // sample image of the seeding pre-pass (strided train rows in the image
   // format of kernel metric smp_kind at width smp_dp; 0 = not built)
   int smp_kind = 0, smp_dp = 0, smp_swz = -1;

@@ -271,8 +271,10 @@ const char* knn_last_kernel_name(knn_ctx* ctx);
  * the train images, read by knn_set_train*: -1 auto -- on at n >= 131072,
  * d <= 256, one region per 32K rows up to 64 -- 0 off, 1 on, 2..64 that
  * many regions; queries of the resident fp16 / int8 kernels are then sorted
- * by region and each query tile's stream starts at its region; results stay
- * exact). */
+ * by region and each query tile's stream starts at its region -- "ophase":
+ * -1 auto (at the first region of its region's eighth of the chain, so 8
+ * groups of query tiles share their streams), 0 its own region, N phases;
+ * results stay exact). */
 int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value);
 
 /* Synchronise the context's stream. */
