@@ -246,10 +246,13 @@ def test_merge_nonfinite_query(knn, k):
         c.close()
 
 
+@pytest.mark.parametrize("order", [0, 3])
 @pytest.mark.parametrize("devs,rccl", GROUPS)
-def test_group_modes_transports(knn, devs, rccl):
+def test_group_modes_transports(knn, devs, rccl, order):
     """Both group modes and the sharded normalisation on every transport a
-    one-GPU box offers, ragged shards, against the oracle."""
+    one-GPU box offers, ragged shards, against the oracle; with every shard's
+    images in train order and in region order (3 regions per shard: list
+    positions mapped back to shard rows, then to global rows)."""
     rng = np.random.default_rng(37)
     tr, lab, te = _mix(rng, 5001, 333, 48, 6, grid=None)
     va = te[::2].copy()
@@ -261,12 +264,14 @@ def test_group_modes_transports(knn, devs, rccl):
     for a, b in ((tr, t_n), (te, e_n), (va, v_n)):
         assert a.tobytes() == b.tobytes()
     want, widx, wdist = oracle.knn(tr, lab, te, 7, True, 6, n_out=7)
+    g.set_tuning("order", order)
     g.set_train(tr, lab, 6)
     got, idx, dist, flags = g.classify(te, 7, knn.L2, return_neighbors=True)
     np.testing.assert_array_equal(got, want)
     assert_neighbors_match(idx, dist, widx, wdist, flags)
     g.close()
     g = knn.Group(devs, 1, rccl=rccl)
+    g.set_tuning("order", order)
     g.set_train(tr, lab, 6)
     got, idx, dist, flags = g.classify(te, 7, knn.L2, return_neighbors=True)
     np.testing.assert_array_equal(got, want)
