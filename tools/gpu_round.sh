@@ -10,6 +10,8 @@
 #   PROF=1         rocprofv3 kernel trace + stats of a short bench -> $TAG_prof/
 # Usage: TAG=r4b TESTS=1 AB_VARIANTS="base fl" AB_ARGS="--rounds 5 auto:0:0" \
 #        bash tools/gpu_round.sh
+#        TAG=r4x AB_SETS="--order 0 auto:0:0;--order -1 auto:0:0" bash tools/gpu_round.sh
+#        TAG=r4y BENCH_SETS="--order 0;--order -1" bash tools/gpu_round.sh
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out
@@ -33,6 +35,36 @@ if [ -n "$AB_VARIANTS" ]; then
     done
   done
   unset KNN_AMD_VARIANT
+fi
+# AB_SETS: tune.py argument sets separated by ';' (e.g. train layouts, which
+# are fixed per process: "--order 0 auto:0:0;--order -1 auto:0:0"), REPS
+# rounds of all sets in turn -> $TAG_set<i>_<rep>.log
+if [ -n "$AB_SETS" ]; then
+  for rep in $(seq 1 ${REPS:-2}); do
+    i=0
+    IFS=';' read -ra sets <<< "$AB_SETS"
+    for a in "${sets[@]}"; do
+      i=$((i + 1))
+      timeout -k 10 300 python3 -u tools/tune.py $a > $O/${TAG}_set${i}_$rep.log 2>&1
+      rc=$?; echo "set $i ($a) $rep rc=$rc"; grep " cand " $O/${TAG}_set${i}_$rep.log
+      [ $rc = 0 ] || exit $rc
+    done
+  done
+fi
+# BENCH_SETS: bench.py argument sets separated by ';' (20 timed steps each,
+# main leg only), REPS rounds -> $TAG_bset<i>_<rep>.json
+if [ -n "$BENCH_SETS" ]; then
+  B="--steps 30 --warmup 5 --no-cpu-baseline --no-fp32-path --no-continuous --no-dropin --no-train-sharded --no-cfg5 --cfg3-queries 0"
+  for rep in $(seq 1 ${REPS:-2}); do
+    i=0
+    IFS=';' read -ra sets <<< "$BENCH_SETS"
+    for a in "${sets[@]}"; do
+      i=$((i + 1))
+      timeout -k 10 240 python3 -u bench.py $B $a > $O/${TAG}_bset${i}_$rep.json 2> $O/${TAG}_bset${i}_$rep.log
+      rc=$?; echo "bench set $i ($a) $rep rc=$rc"; tail -c 300 $O/${TAG}_bset${i}_$rep.json
+      [ $rc = 0 ] || exit $rc
+    done
+  done
 fi
 if [ -n "$BENCH" ]; then
   timeout -k 10 ${BENCH_LIMIT:-400} python3 -u bench.py --steps 20 --warmup 5 ${BENCH_ARGS} \
