@@ -135,25 +135,45 @@ region_assign_kernel(const double* __restrict__ X, const double* __restrict__ mu
 
 // Lloyd update: centroid p = mean of the sample rows assigned to it (fp64
 // sums in row order: deterministic); an empty centroid keeps its value.
-// Grid = P blocks, thread = dimension (d <= 256).
+// Grid = P blocks, thread = dimension (d <= 256).  Per chunk of 256 sample
+// rows the members' offsets are compacted (in row order) into LDS first, so
+// their loads go out 8 at a time instead of one dependent load per member.
 __global__ void __launch_bounds__(256)
 region_update_kernel(const double* __restrict__ X, const double* __restrict__ mu, int64_t ns,
                      int d, int64_t stride, int jx, const int* __restrict__ assign,
                      float* __restrict__ cent) {
-  __shared__ int a[256];
-  const int p = blockIdx.x, c = threadIdx.x;
+  __shared__ int mem[256];
+  __shared__ int wcnt[4];
+  const int p = blockIdx.x, c = threadIdx.x, lane = c & 63, wv = c >> 6;
+  const double mc = c < d ? mu[c] : 0.0;
+  const int cc = c < d ? c : 0;
   double s = 0.0;
   int64_t cnt = 0;
   for (int64_t i0 = 0; i0 < ns; i0 += 256) {
+    const bool is = i0 + c < ns && assign[i0 + c] == p;
+    const unsigned long long bal = __ballot(is);
+    __syncthreads();  // the previous chunk's reads of mem are done
+    if (lane == 0) wcnt[wv] = __popcll(bal);
     __syncthreads();
-    a[threadIdx.x] = i0 + threadIdx.x < ns ? assign[i0 + threadIdx.x] : -1;
+    int before = 0, nm = 0;
+    for (int w = 0; w < 4; ++w) {
+      before += w < wv ? wcnt[w] : 0;
+      nm += wcnt[w];
+    }
+    if (is)
+      mem[before + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                             __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0))] = c;
     __syncthreads();
-    const int nb = (int)min((int64_t)256, ns - i0);
-    for (int i = 0; i < nb; ++i)
-      if (a[i] == p) {
-        ++cnt;
-        if (c < d) s += __builtin_ldexp(X[(i0 + i) * stride * d + c] - mu[c], jx);
-      }
+    cnt += nm;
+    int k = 0;
+    for (; k + 8 <= nm; k += 8) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = X[(i0 + mem[k + u]) * stride * d + cc];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += __builtin_ldexp(v[u] - mc, jx);
+    }
+    for (; k < nm; ++k) s += __builtin_ldexp(X[(i0 + mem[k]) * stride * d + cc] - mc, jx);
   }
   if (c < d && cnt > 0) cent[(int64_t)p * d + c] = (float)(s / (double)cnt);
 }
@@ -170,16 +190,23 @@ __global__ void region_init_kernel(const double* __restrict__ X, const double* _
 
 // Greedy chain over the P centroids (one wave, lane = centroid): start at
 // the centroid farthest from centroid 0, then repeatedly the nearest
-// unvisited one; rank[p] = its position in the chain.
+// unvisited one; rank[p] = its position in the chain.  The centroids are
+// staged in LDS first ([p][d + 1]: conflict-free per-lane rows).
 __global__ void __launch_bounds__(64)
 region_chain_kernel(const float* __restrict__ cent, int P, int d, int* __restrict__ rank) {
+  __shared__ float cs[kRegionMax * 257];
   const int p = threadIdx.x;
+  for (int e = p; e < P * d; e += 64) {
+    const int r = e / d, c = e - r * d;
+    cs[r * (d + 1) + c] = cent[e];
+  }
+  __syncthreads();
   auto dist_to = [&](int cur) {
     float s = KNN_INF_F;
     if (p < P) {
       s = 0.0f;
       for (int c = 0; c < d; ++c) {
-        const float t = cent[(int64_t)p * d + c] - cent[(int64_t)cur * d + c];
+        const float t = cs[p * (d + 1) + c] - cs[cur * (d + 1) + c];
         s = __builtin_fmaf(t, t, s);
       }
     }
