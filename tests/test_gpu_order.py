@@ -97,3 +97,25 @@ def test_region_order_small_batches_and_retrain(knn):
     np.testing.assert_array_equal(got, want)
     np.testing.assert_array_equal(idx, widx)
     c.close()
+
+
+def test_region_order_large_query_batch(knn):
+    """More than 64 sort blocks of queries (m > 65536): the query sort's scan
+    kernel runs between the fused histogram and the scatter.  Same results
+    as train order, bit for bit."""
+    tr, lab, te, classes = _data("i8", 200000, 70000, 99)
+    outs = []
+    for order in (0, -1):
+        c = knn.Classifier(0)
+        c.set_tuning("order", order)
+        c.set_train(tr, lab, classes)
+        got, idx, dist, _ = c.classify(te, 10, 0, return_neighbors=True)
+        assert c.last_candidate_path() == 5
+        outs.append((got, idx, dist))
+        c.close()
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
+    np.testing.assert_array_equal(outs[0][2].view(np.int64), outs[1][2].view(np.int64))
+    want, _, wdist = oracle.knn(tr, lab, te[:100], 10, True, classes, n_out=10)
+    np.testing.assert_array_equal(outs[1][0][:100], want)
+    np.testing.assert_array_equal(outs[1][2][:100].view(np.int64), wdist.view(np.int64))
