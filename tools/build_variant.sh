@@ -24,7 +24,7 @@ for g in 0 1 2 3; do
   [ -f build/$name/res_$g.o ] || cp build/knn_cand_res_$g.o build/$name/res_$g.o
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o lib/libknn_amd_$name.so \
-  build/knn_prep.o build/$name/cand.o build/knn_select.o build/$name/res_*.o \
+  build/knn_prep.o build/$name/cand.o build/knn_select.o build/knn_order.o build/$name/res_*.o \
   build/knn_normalize.o build/knn_api.o build/knn_group.o \
   -L/opt/rocm/lib -lamdhip64 -lrccl -Wl,-rpath,/opt/rocm/lib
 echo "built lib/libknn_amd_$name.so"
