@@ -14,10 +14,11 @@
 //      counting-sorted by the chain rank of their region: image position
 //      p holds train row perm[p] (ipos is the inverse).
 // Per classify call the queries get the same treatment (assign, sort), and
-// each query tile's workgroups start their streams at the first tile of the
-// tile's region (cand_kernel, qstart): the first rows each split sees are
-// the query tile's own neighbourhood, and its thresholds are tight from the
-// first tiles on.  Everything here is deterministic (integer counts, fixed
+// each query tile's workgroups start their streams at the tile's
+// neighbourhood in the chain (cand_kernel, qstart: the first region of the
+// tile's region's phase, 8 phases by default, so the tiles of one phase
+// still share staged tiles in L2); its thresholds are tight from the first
+// tiles on.  Everything here is deterministic (integer counts, fixed
 // summation orders), so the same train set always gets the same layout.
 #include "knn_device.h"
 #include "knn_kernels.h"
@@ -46,8 +47,8 @@ region_image_kernel(const float* __restrict__ cent, int P, int d, __bf16* __rest
 // fp32 operands 2^jx (x - mu) of every candidate path rounded to bf16 -- any
 // assignment is valid, only locality matters, so the scores
 // ||c||^2 - 2 x.c run on the matrix cores.  Block = 32 rows, 2 waves: the
-// rows are staged into LDS as bf16 first (coalesced loads, 16 in flight per
-// thread), then wave b multiplies them (B operand: lane (j, h) row j, dims
+// rows are staged into LDS as bf16 first (coalesced loads, all of a
+// thread's in flight at once), then wave b multiplies them (B operand: lane (j, h) row j, dims
 // 16s + 8h .. +7 of k-step s) with centroid block b (A: 32 centroids); lane
 // (j, h) of wave b ends with the scores of centroids 32b + (i & 3) +
 // 8 (i >> 2) + 4h (the 32x32 C layout); the lowest over both lanes of row j
