@@ -14,6 +14,9 @@ export TMPDIR=/tmp
 TAG=${TAG:-r2}
 OUT=$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
+# the source identity of the build being profiled (tools/profiles_commit.py
+# refuses to stamp a different tree's sha onto these results)
+python3 -c "import sys; sys.path.insert(0, '$GRAFT_REPO_ROOT'); import bench; print(bench.kernel_src_sha())" > "$OUT/src_sha.txt"
 BENCH_COMMON="--no-cpu-baseline --no-fp32-path --no-continuous --cfg3-queries 0 --no-dropin --no-train-sharded --no-cfg5"
 declare -A WL
 WL[cfg2]="--steps 10 --warmup 2"

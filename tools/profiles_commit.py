@@ -66,6 +66,11 @@ def main():
     a = ap.parse_args()
     src = os.path.join(ROOT, "gpurun_out", "prof_" + a.tag)
     dst = os.path.join(ROOT, "profiles")
+    # the profiled build must be this tree's (tools/profile_all.sh records it)
+    rec = os.path.join(src, "src_sha.txt")
+    if not os.path.exists(rec) or open(rec).read().strip() != bench.kernel_src_sha():
+        sys.exit("profiles_commit: %s was not profiled from this tree's sources (%s); re-run "
+                 "tools/profile_all.sh" % (src, bench.kernel_src_sha()))
     for cfg, wl in WORKLOADS.items():
         sdir = os.path.join(src, "stats_" + cfg)
         if not os.path.isdir(sdir):
