@@ -236,6 +236,39 @@ static int build_order(knn_ctx* ctx, const double* dX, const double* mu, int64_t
   return KNN_OK;
 }
 
+// Norm blocks (knn_order.hip, launch_norm_blocks): the int8 kernels bound a
+// sub-tile by its largest seed instead of reading every row's seed from LDS
+// (knn_cand_res.hip), which needs rows of nearly equal norm side by side.
+// Auto: integer-coded train sets of more than one window at d <= 256.
+static bool norm_blocks_on(const knn_ctx* ctx, int64_t n, int d) {
+  if (ctx->tune_nblk == 0 || pad_dim_fp16(d) <= 0 || n < 2) return false;
+  if (ctx->tune_nblk > 0) return true;
+  return ctx->i8_ok && (pad_dim_i8(d) > 0 || pad_dim_i8w(d) > 0) && n > kNormWin;
+}
+
+// The windows sorted by the int8 code norm (the seeds' own; ||x - mu||^2 for
+// other sets), on top of the region order when it is on.
+static int build_norm_blocks(knn_ctx* ctx, const double* dX, int64_t n, int d) {
+  int rc;
+  if ((rc = ctx->ord_key.ensure((size_t)n * sizeof(int)))) return rc;
+  if ((rc = ctx->ord_perm.ensure((size_t)n * sizeof(int)))) return rc;
+  if ((rc = ctx->ord_ipos.ensure((size_t)n * sizeof(int)))) return rc;
+  const int* perm0 = nullptr;
+  if (ctx->ord_P) {
+    if ((rc = ctx->ord_perm0.ensure((size_t)n * sizeof(int)))) return rc;
+    HIP_TRY(hipMemcpyAsync(ctx->ord_perm0.p, ctx->ord_perm.p, (size_t)n * sizeof(int),
+                           hipMemcpyDeviceToDevice, ctx->stream));
+    perm0 = (const int*)ctx->ord_perm0.p;
+  }
+  const bool i8 = ctx->i8_ok;
+  launch_norm_blocks(dX, i8 ? (const double*)ctx->i8_cent.p : nullptr, ctx->i8_s,
+                     (const double*)ctx->mu.p, n, d, perm0, (uint32_t*)ctx->ord_key.p,
+                     (int*)ctx->ord_perm.p, (int*)ctx->ord_ipos.p, ctx->stream);
+  HIP_TRY(hipGetLastError());
+  ctx->ord_nb = true;
+  return KNN_OK;
+}
+
 // Builds the fp32 candidate copy + seeds + norm stats from fp64 rows that
 // already sit on the device.
 static int build_train(knn_ctx* ctx, const double* dX, const int32_t* dlab, int64_t n, int d,
@@ -286,9 +319,11 @@ static int build_train(knn_ctx* ctx, const double* dX, const int32_t* dlab, int6
   // the shift is <= 2^-11 of max |x - mu|, immaterial for the centring
   launch_round_mu((double*)ctx->mu.p, d, jx + 2, ctx->stream);
   ctx->ord_P = 0;
+  ctx->ord_nb = false;
   const int P = region_count(ctx, n, d);
   if (P > 0 && (rc = build_order(ctx, dX, (const double*)ctx->mu.p, n, d, jx, P))) return rc;
-  const int* perm = ctx->ord_P ? (const int*)ctx->ord_perm.p : nullptr;
+  if (norm_blocks_on(ctx, n, d) && (rc = build_norm_blocks(ctx, dX, n, d))) return rc;
+  const int* perm = ctx->ord_P || ctx->ord_nb ? (const int*)ctx->ord_perm.p : nullptr;
   launch_prep_train(dX, (const double*)ctx->mu.p, n, d, DP, n_pad, jx, (float*)ctx->X32.p,
                     (float*)ctx->xl2.p, (float*)ctx->xl1.p, st_d, ctx->stream, perm);
   HIP_TRY(hipGetLastError());
@@ -449,7 +484,7 @@ static int ensure_fp16_s3(knn_ctx* ctx, hipStream_t s) {
 
 static int64_t seed_rows(const knn_ctx* ctx) {
   // (the sample image takes train rows by stride: train order only)
-  if (ctx->tune_seed <= 0 || ctx->ord_P) return 0;
+  if (ctx->tune_seed <= 0 || ctx->ord_P || ctx->ord_nb) return 0;
   const int64_t ns = std::min<int64_t>(ctx->tune_seed, ctx->train.n / 8) / 256 * 256;
   return ns < 4096 ? 0 : ns;
 }
@@ -1478,6 +1513,9 @@ int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value) {
     if (value < -1 || value > kRegionMax)
       return knn_fail(KNN_ERR_ARG, "order must be -1 (auto), 0, 1 or 2..64 regions");
     ctx->tune_order = (int)value;
+  } else if (!strcmp(key, "nblk")) {
+    if (value < -1 || value > 1) return knn_fail(KNN_ERR_ARG, "nblk must be -1 (auto), 0 or 1");
+    ctx->tune_nblk = (int)value;
   } else if (!strcmp(key, "ties")) {
     if (value < 0 || value > 2) return knn_fail(KNN_ERR_ARG, "ties must be 0, 1 or 2");
     ctx->tune_ties = (int)value;

@@ -72,6 +72,10 @@ struct knn_ctx {
   // starting at each split's first tile).
   int tune_order = -1;
   int ord_P = 0;               // regions of the current train layout (0: train order)
+  // norm blocks (knn_order.hip): -1 auto (integer-coded train sets, d <= 256),
+  // 0 off, 1 on; ord_nb: the current layout has them (ord_perm / ord_ipos valid)
+  int tune_nblk = -1;
+  bool ord_nb = false;
   int tune_s3gq = 0;           // S3 kernel: largest XCD query-tile grouping (0 = kS3GqMax)
   // query streams start at one of N phases of the region chain (P regions in
   // N groups; -1 auto = 8, 0 = at the query tile's own region)
@@ -99,7 +103,7 @@ struct knn_ctx {
   // region order: centroids [P][d], chain ranks, region starts, image
   // position <-> train row maps; k-means / sort scratch; per-call query order
   DevBuf ord_cent, ord_cnorm, ord_img, ord_rank, ord_rstart, ord_perm, ord_ipos, ord_key, ord_bcnt, ord_tot, ord_qkey,
-      ord_qperm, ord_qpos, ord_qstart;
+      ord_qperm, ord_qpos, ord_qstart, ord_perm0;
   // per-classify workspace
   DevBuf Q64, Q32, qvalid, cand_v, cand_i, gthr, rescan_q, rescan_tau, rescan_cnt, fr_cnt, fr_buf,
       fr_q, fr_thr, slow_q, totals, lk, rescan_mask, rescan_nkeep;
@@ -118,7 +122,7 @@ struct knn_ctx {
             &slow_q,  &totals,  &lk, &mrg, &tie_q, &tie_ws, &o_lab, &o_idx, &o_dist, &o_flags, &nrm_part, &nrm_mm, &nrm_X,
             &rescan_mask, &rescan_nkeep, &smp_x64, &smp_xl2, &smp_img, &smp_scr, &smp_v, &smp_i,
             &ord_cent, &ord_cnorm, &ord_img, &ord_rank, &ord_rstart, &ord_perm, &ord_ipos, &ord_key, &ord_bcnt, &ord_tot,
-            &ord_qkey, &ord_qperm, &ord_qpos, &ord_qstart};
+            &ord_qkey, &ord_qperm, &ord_qpos, &ord_qstart, &ord_perm0};
   }
 };
 

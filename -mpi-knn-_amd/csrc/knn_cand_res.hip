@@ -70,17 +70,39 @@ static_assert(KNN_RES_TPB * knnk::kTR == knnk::kResTileRows || KNN_RES_TPB != 2,
 #ifndef KNN_I8_WPE
 #define KNN_I8_WPE 2
 #endif
+// int8 kernels: seed-free accumulation.  The accumulators start at zero (no
+// LDS read of the rows' seeds per sub-tile: 4 of the 7 ds_read_b128 per
+// metric-6 sub-tile, 2 of 6 at metric 5) and a sub-tile's no-candidate test
+// adds the largest seed of its 32 rows (kI8SmaxRow pads, 2 reads per staged
+// tile); only a wave whose bound passes reads the exact seeds and runs the
+// exact selection.  The bound is tight on norm-blocked images (knn_order.hip):
+// 7.6 % of metric-6 sub-tile tests pass it at cfg2 against 7.56 % passing
+// exactly (profiles/ab_log.md r5e).  Metric 6 (KNN_I8_SMAX): the 12.5M x 96
+// shard 12.06 -> 11.72 ms (r5d4; bare MFMA + LDS loop 9.84 -> 9.25 ms, r5c4).
+// Metric 5 (KNN_I8_SMAX5, off): that loop is not LDS-bound (bare loop 0.912 vs
+// 0.913 ms, r5b) but issue-bound -- a 16x16x64 MFMA holds the SIMD's vector
+// issue for 8 of its 16 cycles and the selection already spends ~4 VALU per
+// MFMA -- so the bound's extra VALU made cfg2 slower (1.41 vs 1.26-1.29 ms, r5d).
+#ifndef KNN_I8_SMAX
+#define KNN_I8_SMAX 1
+#endif
+#ifndef KNN_I8_SMAX5
+#define KNN_I8_SMAX5 0
+#endif
 
 
 namespace knnk {
 
 #if KNN_COUNT_SEL
-__device__ unsigned long long knn_sel_cnt[4];
+__device__ unsigned long long knn_sel_cnt[6];
 #endif
 
+// (lgkmcnt(0): every LDS read of the wave -- the int8 kernels' seed reads of
+// a staged tile's last sub-tile among them -- has completed before any wave
+// refills that tile's buffer after the barrier)
 template <int N>
 __device__ __forceinline__ void wait_barrier() {
-  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
 // The wait count plus `extra` younger exchange ops (see cand_kernel).
@@ -384,6 +406,71 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   }
   int rowp = 0;
   SelCount selc;
+  // Seed-free int8 accumulation (KNN_I8_SMAX): a holds q.k of a sub-tile,
+  // smx the largest seed of its rows.  Every value's exact accumulator q.k +
+  // seed is at most q.k + smx, so a wave none of whose lanes passes tn - smx
+  // has no candidate; otherwise the exact seeds are added (sd(c): the seed
+  // group c of the lane's rows -- from the sub-tile's LDS rows, or from
+  // registers) and the exact selection runs.
+  constexpr bool SMX = (I8W && KNN_I8_SMAX) || (I8 && KNN_I8_SMAX5);
+  constexpr int NSG = I8W ? 4 : 2;  // i32x4 seed groups per lane and sub-tile
+  // seed group c of the sub-tile whose LDS rows start at sb: metric 5 rows
+  // 16c + 4 g16 (block c), metric 6 rows 8c + 4h
+  auto seed_lds = [&](const float* sb, int c) {
+    return __builtin_bit_cast(i32x4, *(const float4*)(sb + (I8W ? 8 * c + 4 * h : 16 * c + 4 * g16) * RSF + SEED));
+  };
+  int smxp = 0;  // PIPE: smx of the pending sub-tile
+  auto sel5 = [&](const auto& a, int row0, int smx, auto&& sd) {  // a: i32x4 [2][QB]
+   if constexpr (SMX) {
+    bool pass = false;
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb) {
+      const i32x4 x = a[0][qb], y = a[1][qb];
+      const int mx = max(max(max(x[0], x[1]), max(x[2], x[3])), max(max(y[0], y[1]), max(y[2], y[3])));
+      pass = pass || mx > tn[qb] - smx;
+    }
+#if KNN_COUNT_SEL
+    selc.bcalls++;
+    selc.bpass += __builtin_amdgcn_ballot_w64(pass) != 0;
+#endif
+    if (__builtin_amdgcn_ballot_w64(pass)) {
+      const i32x4 s0 = sd(0), s1 = sd(1);
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb)
+        select_i8(a[0][qb] + s0, a[1][qb] + s1, row0, L[qb], I[qb], te[qb], tn[qb], selc);
+    }
+   }
+  };
+  auto sel6 = [&](const auto& a, int row0, int smx, auto&& sd) {  // a: i32x16
+   if constexpr (SMX && I8W) {
+    const int mx = max(max(max(max(a[0], a[1]), max(a[2], a[3])), max(max(a[4], a[5]), max(a[6], a[7]))),
+                       max(max(max(a[8], a[9]), max(a[10], a[11])), max(max(a[12], a[13]), max(a[14], a[15]))));
+#if KNN_COUNT_SEL
+    selc.bcalls++;
+    selc.bpass += __builtin_amdgcn_ballot_w64(mx > tn[0] - smx) != 0;
+#endif
+    if (__builtin_amdgcn_ballot_w64(mx > tn[0] - smx)) {
+      i32x16 b = a;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const i32x4 g = sd(c);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) b[4 * c + e] = a[4 * c + e] + g[e];
+      }
+      select_block_i8<R>(b, row0, L[0], I[0], tn[0], selc);
+    }
+   }
+  };
+  // SMX: the largest seeds of the staged tile's sub-tiles (wave-uniform);
+  // spre: the exact seeds of the staged tile's last sub-tile, read with its
+  // A fragments -- its selection runs after the next tile's first MFMAs,
+  // when the buffer may be refilled (a pending sub-tile starts empty: raw
+  // accumulators kI8Floor and smx 0 never pass)
+  int smt[SMX ? TPB : 1];
+  i32x4 spre[SMX ? NSG : 1];
+#pragma unroll
+  for (int c = 0; c < (SMX ? NSG : 1); ++c) spre[c] = i32x4{0, 0, 0, 0};
+  static_assert(!SMX || (TPB % 4 == 0 && kTR * 4 == 128), "sub-tile maxima are stored per 128-row group");
 
   // ---- staging: this wave's LDS-DMA pieces i = wv, wv+NW, ... of tile t ->
   // buffer b.  The last piece may read past the tile (and past the last row:
@@ -544,6 +631,15 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
         if constexpr (I8A) tn[b] = i8_neg_half(te[b]);
       }
     }
+    if constexpr (SMX) {
+#pragma unroll
+      for (int u = 0; u < TPB / 4; ++u) {
+        const i32x4 v = __builtin_bit_cast(
+            i32x4, *(const float4*)(lds + cur * BUFF + (128 * u + kI8SmaxRow) * RSF + SEED));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) smt[4 * u + e] = __builtin_amdgcn_readfirstlane(v[e]);
+      }
+    }
 #pragma unroll
     for (int sub = 0; sub < TPB; ++sub) {
     const float* base = lds + cur * BUFF + sub * kTR * RSF;
@@ -553,12 +649,14 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       // j against rows (i&3) + 8(i>>2) + 4h; the accumulators start at the
       // rows' seeds -ceil(||k||^2 / 2) (the pad of row 4g carries rows 4g ..
       // 4g+3: groups 2c + h, c = i >> 2) and end at q.k - ceil(||k||^2 / 2)
-      i32x16 acc;
+      i32x16 acc = {};  // (SMX: the first MFMA's C operand is the inline zero)
+      if constexpr (!SMX) {
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const i32x4 sd = __builtin_bit_cast(i32x4, *(const float4*)(base + (8 * c + 4 * h) * RSF + SEED));
+        for (int c = 0; c < 4; ++c) {
+          const i32x4 sd = __builtin_bit_cast(i32x4, *(const float4*)(base + (8 * c + 4 * h) * RSF + SEED));
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc[4 * c + e] = sd[e];
+          for (int e = 0; e < 4; ++e) acc[4 * c + e] = sd[e];
+        }
       }
       // A fragment of k-step ks: row j, dims 32ks + 16h .. +15 (the image of
       // this kernel is not chunk-swizzled: the 32x32 reads are conflict-free)
@@ -566,15 +664,37 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
 #pragma unroll
       for (int ks = 0; ks < DP / 32; ++ks)
         af[ks] = __builtin_bit_cast(i32x4, *(const float4*)(base + j * RSF + 8 * ks + 4 * h));
+      if constexpr (SMX && PIPE) {
+        if (sub == TPB - 1) {
+#pragma unroll
+          for (int c = 0; c < NSG; ++c) spre[c] = seed_lds(base, c);
+        }
+      }
 #if KNN_I8_SCHED
       __builtin_amdgcn_sched_barrier(0);
 #endif
 #pragma unroll
       for (int ks = 0; ks < DP / 32; ++ks)
-        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[ks], __builtin_bit_cast(i32x4, qf[ks]), acc,
-                                                    0, 0, 0);
+        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[ks], __builtin_bit_cast(i32x4, qf[ks]),
+                                                    SMX && ks == 0 ? i32x16{} : acc, 0, 0, 0);
       const int row0 = (t * TPB + sub) * kTR + 4 * h;
-      if constexpr (PIPE) {
+      if constexpr (SMX) {
+        // the pending sub-tile's selection after this one's MFMAs (seeds of
+        // the previous staged tile's last sub-tile from spre)
+        if (!(abl & 2)) {
+          if constexpr (PIPE) {
+            if (sub > 0) sel6(accw, rowp, smxp, [&](int c) { return seed_lds(base - kTR * RSF, c); });
+            else sel6(accw, rowp, smxp, [&](int c) { return spre[c]; });
+            accw = acc;
+            rowp = row0;
+            smxp = smt[sub];
+          } else {
+            sel6(acc, row0, smt[sub], [&](int c) { return seed_lds(base, c); });
+          }
+        } else if (acc[0] == 12345 && acc[15] == 12345) {
+          thr[0] = (float)acc[7];  // keep the accumulators live
+        }
+      } else if constexpr (PIPE) {
         if (!(abl & 2)) {
           select_block_i8<R>(accw, rowp, L[0], I[0], tn[0], selc);
           accw = acc;
@@ -595,12 +715,14 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       // MFMAs, fenced (KNN_I8_SCHED): the registers are there (the query
       // image is half the fp16 one), and the compiler's own schedule would
       // wait on each read just before its two MFMAs
-      i32x4 acc[2][QB];
+      i32x4 acc[2][QB] = {};
+      if constexpr (!SMX) {
 #pragma unroll
-      for (int rb = 0; rb < 2; ++rb) {
-        const i32x4 sd = __builtin_bit_cast(i32x4, *(const float4*)(base + (rb * 16 + 4 * g16) * RSF + SEED));
+        for (int rb = 0; rb < 2; ++rb) {
+          const i32x4 sd = __builtin_bit_cast(i32x4, *(const float4*)(base + (rb * 16 + 4 * g16) * RSF + SEED));
 #pragma unroll
-        for (int qb = 0; qb < QB; ++qb) acc[rb][qb] = sd;
+          for (int qb = 0; qb < QB; ++qb) acc[rb][qb] = sd;
+        }
       }
       const int g16s = g16 ^ (xsw ? xh_swz(c16) : 0);
       i32x4 af[DP / 64][2];
@@ -610,6 +732,12 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
         for (int rb = 0; rb < 2; ++rb)
           af[ks][rb] = __builtin_bit_cast(
               i32x4, *(const float4*)(base + (rb * 16 + c16) * RSF + 16 * ks + 4 * g16s));
+      if constexpr (SMX && PIPE) {
+        if (sub == TPB - 1) {
+#pragma unroll
+          for (int c = 0; c < NSG; ++c) spre[c] = seed_lds(base, c);
+        }
+      }
 #if KNN_I8_SCHED
       __builtin_amdgcn_sched_barrier(0);
 #endif
@@ -621,12 +749,31 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
 #pragma unroll
           for (int qb = 0; qb < QB; ++qb) {
             const i32x4 b = __builtin_bit_cast(i32x4, qf[qb * (DP / 64) + ks]);
-            acc[rb][qb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, acc[rb][qb], 0, 0, 0);
+            acc[rb][qb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(
+                a, b, SMX && ks == 0 ? i32x4{} : acc[rb][qb], 0, 0, 0);
           }
         }
       }
       const int row0 = (t * TPB + sub) * kTR + 4 * g16;
-      if constexpr (PIPE) {
+      if constexpr (SMX) {
+        // as metric 6
+        if (!(abl & 2)) {
+          if constexpr (PIPE) {
+            if (sub > 0) sel5(accp, rowp, smxp, [&](int c) { return seed_lds(base - kTR * RSF, c); });
+            else sel5(accp, rowp, smxp, [&](int c) { return spre[c]; });
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+              for (int qb = 0; qb < QB; ++qb) accp[rb][qb] = acc[rb][qb];
+            rowp = row0;
+            smxp = smt[sub];
+          } else {
+            sel5(acc, row0, smt[sub], [&](int c) { return seed_lds(base, c); });
+          }
+        } else if (acc[0][0][0] == 12345 && acc[1][1][3] == 12345) {
+          thr[0] = (float)acc[0][1][2];  // keep the accumulators live
+        }
+      } else if constexpr (PIPE) {
         if (!(abl & 2)) {
 #pragma unroll
           for (int qb = 0; qb < QB; ++qb)
@@ -799,7 +946,13 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
 
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if constexpr (PIPE && I8W) {
+  if constexpr (SMX && PIPE) {
+    // the last tile's last sub-tile, seeds from spre
+    if (!(abl & 2)) {
+      if constexpr (I8W) sel6(accw, rowp, smxp, [&](int c) { return spre[c]; });
+      else sel5(accp, rowp, smxp, [&](int c) { return spre[c]; });
+    }
+  } else if constexpr (PIPE && I8W) {
     if (!(abl & 2)) select_block_i8<R>(accw, rowp, L[0], I[0], tn[0], selc);
   } else if constexpr (PIPE) {
     if (!(abl & 2)) {
@@ -819,6 +972,8 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
     atomicAdd(&knn_sel_cnt[1], (unsigned long long)selc.lane_pass);
     if (lane == 0) atomicAdd(&knn_sel_cnt[2], (unsigned long long)selc.wave_pass);
     atomicAdd(&knn_sel_cnt[3], (unsigned long long)selc.inserts);
+    if (lane == 0) atomicAdd(&knn_sel_cnt[4], (unsigned long long)selc.bcalls);
+    if (lane == 0) atomicAdd(&knn_sel_cnt[5], (unsigned long long)selc.bpass);
   }
 #endif
   if constexpr (M16) {
@@ -954,15 +1109,15 @@ KNN_GROUP_DPS(KNN_DEF)
 // selection counts of a KNN_COUNT_SEL build (DP 96 / 128), zeros otherwise.
 int res_sel_counters(unsigned long long* out, int reset) {
 #if KNN_COUNT_SEL
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(knn_sel_cnt), 4 * sizeof(unsigned long long)) != hipSuccess)
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(knn_sel_cnt), 6 * sizeof(unsigned long long)) != hipSuccess)
     return -1;
   if (reset) {
-    const unsigned long long z[4] = {0, 0, 0, 0};
+    const unsigned long long z[6] = {0, 0, 0, 0, 0, 0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(knn_sel_cnt), z, sizeof z) != hipSuccess) return -1;
   }
 #else
   (void)reset;
-  for (int i = 0; i < 4; ++i) out[i] = 0;
+  for (int i = 0; i < 6; ++i) out[i] = 0;
 #endif
   return 0;
 }

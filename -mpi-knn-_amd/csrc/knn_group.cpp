@@ -196,19 +196,22 @@ static int coll_alltoallv(knn_group* g, const std::vector<double*>& send,
     int rc;
     if ((rc = lb_barrier(g))) return rc;
   }
-  // a rank's own block (and every block without a transport): a device copy
-  for (int a = 0; a < G; a++)
-    for (int b = 0; b < G; b++) {
-      if (cnt[a][b] <= 0 || (a != b && g->transport == XPORT_RCCL)) continue;
-      HIP_G(hipSetDevice(g->devs[b]));
-      HIP_G(hipMemcpyAsync(recv[b] + roff[b][a], send[a] + soff[a][b], cnt[a][b] * 8,
-                           hipMemcpyDeviceToDevice, stream_of(g, b)));
-    }
-  if (g->transport == XPORT_RCCL && G > 1) {
+  // without RCCL (loopback, or no transport): every block a device copy
+  if (g->transport != XPORT_RCCL)
+    for (int a = 0; a < G; a++)
+      for (int b = 0; b < G; b++) {
+        if (cnt[a][b] <= 0) continue;
+        HIP_G(hipSetDevice(g->devs[b]));
+        HIP_G(hipMemcpyAsync(recv[b] + roff[b][a], send[a] + soff[a][b], cnt[a][b] * 8,
+                             hipMemcpyDeviceToDevice, stream_of(g, b)));
+      }
+  // RCCL: every block, a rank's own included (send to self inside the group:
+  // the one-rank communicator of KNN_GROUP_RCCL then runs this exchange's
+  // ncclSend / ncclRecv on a single GPU)
+  if (g->transport == XPORT_RCCL) {
     NCCL_G(ncclGroupStart());
     for (int a = 0; a < G; a++)
       for (int b = 0; b < G; b++) {
-        if (a == b) continue;
         if (cnt[a][b] > 0)
           NCCL_G(ncclSend(send[a] + soff[a][b], (size_t)cnt[a][b], ncclFloat64, b, g->comms[a],
                           stream_of(g, a)));

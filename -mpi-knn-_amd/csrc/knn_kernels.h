@@ -354,6 +354,18 @@ void launch_region_sort_queries(const double* Q, const double* mu, int64_t m, in
                                 const int* rstart, int phases, int* bcnt, int* tot, int* qkey,
                                 int* qperm, int* qpos, int* qstart, hipStream_t s);
 
+// Norm blocks (knn_order.hip): every window of kNormWin image positions
+// sorted by the rows' squared norm (int8 code norm with cent, else ||x -
+// mu||^2): perm[p] = perm0[source] (perm0 null: train order), ipos inverse;
+// key holds n uint32 of scratch.  perm0 must not alias perm / ipos.
+constexpr int kNormWin = 16384;
+void launch_norm_blocks(const double* X, const double* cent, int s, const double* mu, int64_t n,
+                        int d, const int* perm0, uint32_t* key, int* perm, int* ipos, hipStream_t st);
+// Int8 images carry, in the pad of row 128u + 1, the largest seed of each of
+// the 32-row sub-tiles 4u .. 4u+3 (the seed-free accumulation's bound,
+// knn_cand_res.hip)
+constexpr int kI8SmaxRow = 1;
+
 // Min-max normalisation (knn_normalize.hip, cpp:229-306).  R = rows per
 // grid sweep; `partial` holds 2*d*R doubles.  launch_minmax folds the set's
 // per-dim max/min into out_max/out_min (init: start from -1 / 999999).

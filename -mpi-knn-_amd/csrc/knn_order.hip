@@ -363,6 +363,95 @@ sort_scatter_kernel(const int* __restrict__ key, int64_t n, const int* __restric
 
 int64_t region_sort_blocks(int64_t n) { return (n + kSortB - 1) / kSortB; }
 
+// ------------------------------------------------------------ norm blocks
+// The int8 candidate kernels start their accumulators at zero and test a
+// 32-row sub-tile against the largest seed of its rows (the seed -ceil(||k||^2
+// / 2) then leaves the LDS port: knn_cand_res.hip); that bound is tight only
+// when the rows of a sub-tile have nearly equal norms.  So the image order is
+// refined once more: every window of kNormWin consecutive image positions
+// (the region order's, or train order) is sorted by the rows' squared norm.
+// A window spans 64 staged tiles of 256 rows, i.e. a split sees at most a
+// few tiles of one window: its stream stays in the window order's (region /
+// train) sequence, only the rows within a window move.
+//
+// key[p] = the squared norm of image row p's train row perm0[p] (perm0 null:
+// p): with cent (int8-coded set) the integer ||k||^2 of its codes k =
+// rint(x 2^s - cent_i), the seed's own norm; otherwise the bits of the float
+// ||x - mu||^2 (non-negative floats order as their bits).  One wave per row.
+__global__ void __launch_bounds__(256)
+norm_key_kernel(const double* __restrict__ X, const double* __restrict__ cent, int s,
+                const double* __restrict__ mu, int64_t n, int d, const int* __restrict__ perm0,
+                uint32_t* __restrict__ key) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wstride = (int64_t)gridDim.x * 4;
+  for (int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); p < n; p += wstride) {
+    const int64_t r = perm0 ? perm0[p] : p;
+    if (cent) {
+      int q2 = 0;
+      for (int c = lane; c < d; c += 64) {
+        const int k = (int)__builtin_rint(__builtin_ldexp(X[r * d + c], s) - cent[c]);
+        q2 += k * k;
+      }
+      q2 = wave_sum_i(q2);
+      if (lane == 0) key[p] = (uint32_t)q2;
+    } else {
+      double q2 = 0.0;
+      for (int c = lane; c < d; c += 64) {
+        const double t = X[r * d + c] - mu[c];
+        q2 += t * t;
+      }
+      q2 = wave_sum_d(q2);
+      if (lane == 0) key[p] = __float_as_uint((float)q2);
+    }
+  }
+}
+
+// One workgroup per window: (key, position) pairs bitonic-sorted in LDS
+// (unique, so the order is deterministic), then perm[p] = perm0[source] and
+// ipos[perm[p]] = p.  perm0 and perm are distinct buffers.
+constexpr int kNormSortT = 1024;
+__global__ void __launch_bounds__(kNormSortT)
+norm_block_sort_kernel(const uint32_t* __restrict__ key, int64_t n, const int* __restrict__ perm0,
+                       int* __restrict__ perm, int* __restrict__ ipos) {
+  __shared__ unsigned long long sk[kNormWin];  // 128 KiB
+  const int tid = threadIdx.x;
+  const int64_t w0 = (int64_t)blockIdx.x * kNormWin;
+  const int cnt = (int)(n - w0 < kNormWin ? n - w0 : kNormWin);
+  for (int i = tid; i < kNormWin; i += kNormSortT)
+    sk[i] = i < cnt ? ((unsigned long long)key[w0 + i] << 32) | (unsigned)i : ~0ull;
+  for (int size = 2; size <= kNormWin; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      __syncthreads();
+      for (int t = tid; t < kNormWin / 2; t += kNormSortT) {
+        const int lo = 2 * t - (t & (stride - 1)), hi = lo + stride;
+        const unsigned long long a = sk[lo], b = sk[hi];
+        if (((lo & size) == 0) == (b < a)) {
+          sk[lo] = b;
+          sk[hi] = a;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < cnt; i += kNormSortT) {
+    const int64_t src = w0 + (int64_t)(unsigned)(sk[i] & 0xFFFFFFFFu);
+    const int r = perm0 ? perm0[src] : (int)src;
+    perm[w0 + i] = r;
+    ipos[r] = (int)(w0 + i);
+  }
+}
+
+void launch_norm_blocks(const double* X, const double* cent, int s, const double* mu, int64_t n,
+                        int d, const int* perm0, uint32_t* key, int* perm, int* ipos, hipStream_t st) {
+  if (n <= 0) return;
+  int64_t blocks = (n + 3) / 4;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(norm_key_kernel, dim3((unsigned)blocks), dim3(256), 0, st, X, cent, s, mu, n, d,
+                     perm0, key);
+  hipLaunchKernelGGL(norm_block_sort_kernel, dim3((unsigned)((n + kNormWin - 1) / kNormWin)),
+                     dim3(kNormSortT), 0, st, key, n, perm0, perm, ipos);
+}
+
 void launch_region_assign(const double* X, const double* mu, int64_t n, int d, int64_t stride,
                           int jx, const unsigned short* img, const float* cnorm, const int* rank, int* out,
                           int* bcnt, hipStream_t s) {

@@ -447,6 +447,23 @@ prep_i8_train_kernel(const double* __restrict__ X64, const double* __restrict__ 
   if (lane == 0 && mx) atomicMax(codes_max, mx);
 }
 
+// Sub-tile seed maxima: thread u4 = 32-row sub-tile, the max of its 32 seeds
+// (pads of its rows 4g) into int slot (u4 & 3) of the pad of row 128 (u4 >>
+// 2) + kI8SmaxRow.  An all-pad sub-tile gets kI8Floor.
+__global__ void __launch_bounds__(256)
+prep_i8_smax_kernel(signed char* __restrict__ out, int DP, int64_t n_sub) {
+  const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (u >= n_sub) return;
+  const int64_t row_bytes = DP + 16;
+  int mx = kI8Floor;
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    const int4 sd = *(const int4*)(out + (u * 32 + 4 * g) * row_bytes + DP);
+    mx = max(mx, max(max(sd.x, sd.y), max(sd.z, sd.w)));
+  }
+  ((int*)(out + ((u >> 2) * 128 + kI8SmaxRow) * row_bytes + DP))[u & 3] = mx;
+}
+
 void launch_prep_i8_train(const double* X64, const double* cent, int64_t n, int d, int DP,
                           int64_t n_pad, int s, signed char* out, unsigned* codes_max, int swz,
                           hipStream_t st, const int* perm) {
@@ -454,6 +471,10 @@ void launch_prep_i8_train(const double* X64, const double* cent, int64_t n, int 
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(prep_i8_train_kernel, dim3((unsigned)blocks), dim3(256), 0, st, X64, cent, n,
                      d, DP, n_pad, s, out, codes_max, swz, perm);
+  // n_pad is a multiple of kRowAlign = 256 (whole 128-row groups)
+  const int64_t n_sub = n_pad / 32;
+  hipLaunchKernelGGL(prep_i8_smax_kernel, dim3((unsigned)((n_sub + 255) / 256)), dim3(256), 0, st,
+                     out, DP, n_sub);
 }
 
 // Query rows: int8 codes clamp(rint(q 2^s - c_i), -128, 127) (DP bytes,

@@ -298,9 +298,14 @@ class Classifier:
         _check(lib().knn_set_precision(self._h, int(mode)))
 
     def set_tuning(self, key, value):
-        """Experiment overrides (knn_amd.h): "R", "S", "nw", "ablate", "fp16",
-        "mfma16", "i8", "i8w", "gk", "s3q", "xhswz", "ties", "seed", "order"
-        ("order" before set_train); 0 (or -1 where stated) = automatic."""
+        """Experiment overrides (knn_amd.h, knn_set_tuning): "R", "S", "nw",
+        "ablate", "fp16", "mfma16", "i8", "i8w", "gk", "s3q", "s3gq", "xhswz",
+        "ties", "seed", "order", "ophase", "nblk"; 0 (or -1 where stated) =
+        automatic.  "order" and "nblk" shape the train layout and are read by
+        set_train: "order" -1 = region order only for integer-coded sets whose
+        int8 image is <= 192 MB (n / 16384 regions, up to 64, at least 8),
+        1 = n / 16384 regions (off below n = 32768); "nblk" -1 = norm blocks
+        for integer-coded sets of more than 16384 rows (d <= 256)."""
         _check(lib().knn_set_tuning(self._h, key.encode(), int(value)))
 
     def last_candidate_path(self):

@@ -207,11 +207,15 @@ class HipTies:
     this rank's shard): the merge's KNN_FLAG_TIE_PENDING rows of the slice
     outputs, knn_shard_distances_device, knn_tie_resolve_device into the same
     outputs.  Every train label is all-gathered the first time any rank has
-    a flagged query (4 B per row)."""
+    a flagged query (4 B per row).  stream: the HIP stream of the library
+    calls; default torch's current stream on `device`, the stream the torch
+    tensors (D, the flags read by pending(), the all-to-all) are ordered on."""
     FLAG_TIE_PENDING = 64
 
     def __init__(self, ctx, Q, lab_shard, n_total, k, outs, mq, metric=0, stream=None,
                  device=None):
+        if stream is None:
+            stream = torch.cuda.current_stream(device).cuda_stream
         self.ctx, self.Q, self.lab_shard, self.n_total, self.k = ctx, Q, lab_shard, n_total, k
         self.o_lab, self.o_idx, self.o_dist, self.o_flags = outs
         self.mq, self.metric, self.stream, self.device = mq, metric, stream, device

@@ -268,13 +268,22 @@ const char* knn_last_kernel_name(knn_ctx* ctx);
  * "seed" (experiment: seeded global thresholds of the fp16 / int8 resident
  * kernels from a pre-pass over N strided train rows; 0 / -1 off, the
  * default -- measured slower; results stay exact); "order" (region order of
- * the train images, read by knn_set_train*: -1 auto -- on at n >= 131072,
- * d <= 256, one region per 32K rows up to 64 -- 0 off, 1 on, 2..64 that
- * many regions; queries of the resident fp16 / int8 kernels are then sorted
- * by region and each query tile's stream starts at its region -- "ophase":
- * -1 auto (at the first region of its region's eighth of the chain, so 8
- * groups of query tiles share their streams), 0 its own region, N phases;
- * results stay exact). */
+ * the train images, read by knn_set_train*: -1 auto -- on only for
+ * integer-coded train sets (the int8 pass) whose int8 image (n x (padded d +
+ * 16) bytes) is at most 192 MB, with P = min(64, n / 16384) regions and at
+ * least 8 of them -- 0 off, 1 on with P = min(64, n / 16384) regions (stays
+ * off below n = 32768, where P < 2), 2..64 that many regions (at most n /
+ * 256); queries of the resident fp16 / int8 kernels are then sorted by
+ * region and each query tile's stream starts at its region -- "ophase": -1
+ * auto (at the first region of its region's eighth of the chain, so 8
+ * groups of query tiles share their streams), 0 its own region, N phases);
+ * "nblk" (norm blocks of the train images, read by knn_set_train*: every
+ * 16384-row window of the image order sorted by the rows' squared norm, so
+ * the int8 kernels' per-sub-tile seed bound is tight; -1 auto -- on for
+ * integer-coded train sets of more than 16384 rows at d <= 256 -- 0 off, 1
+ * on); "s3gq" (the fp16 d > 256 kernel's largest XCD grouping of query
+ * tiles, 0 = 4); "xhswz" (the fp16 image's chunk swizzle: 1 on, 0 off);
+ * all of them leave results exact. */
 int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value);
 
 /* Synchronise the context's stream. */

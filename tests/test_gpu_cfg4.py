@@ -13,10 +13,16 @@ k-way merges them and votes (≙ cpp:324-337).  Checks:
     rows gathered on the GPU), ascending, distinct rows, first-to-max vote;
   * optimality on a sample: the k distances equal the k smallest over all
     100M rows of an independent fp64 brute force on the GPU (1e-10 rel);
-  * the oracle (oracle/knn_oracle.cpp) bit for bit on a sample of queries,
-    streamed over 4M-row chunks of the train set (each chunk's exact top-w,
-    merged by (dist, idx) -- the oracle restates cpp:33-50 + std::sort, whose
-    first w entries per chunk contain the chunk's part of the global top-w).
+  * the reference's tie order across shards: queries the merge flags
+    KNN_FLAG_TIE_PENDING (their label or order depends on equal distances
+    in different shards) go through the exchange of knn_dist.resolve_ties
+    (every shard's exact distances, the owner's introsort emulation); none
+    may stay pending;
+  * the oracle (oracle/knn_oracle.cpp) bit for bit on 32 queries and on
+    every resolved one (up to 32 more), streamed over 4M-row chunks of the
+    train set (each chunk's exact top-w, merged by (dist, idx) -- the
+    oracle restates cpp:33-50 + std::sort, whose first w entries per chunk
+    contain the chunk's part of the global top-w).
 Data: bench.synth (Gaussian mixture on the 8-bit grid k/256), seeded."""
 import numpy as np
 import pytest
@@ -80,6 +86,7 @@ def test_cfg4_100m_train_sharded(knn):
     gi = torch.empty((parts, m, w), dtype=torch.int64, device=DEV)
     gl = torch.empty((parts, m, w), dtype=torch.int32, device=DEV)
     paths = []
+    ctxs, shards = [], []
     for p in range(parts):
         r0, r1 = n * p // parts, n * (p + 1) // parts
         c = knn.Classifier(0)
@@ -94,7 +101,8 @@ def test_cfg4_100m_train_sharded(knn):
                                 gl[p].data_ptr())
         c.sync()
         paths.append(c.last_candidate_path())
-        c.close()
+        ctxs.append(c)
+        shards.append((r0, r1))
     # d = 96: the int8 pass on 32x32x32 (metric 6, no padded dims)
     assert paths == [6, 4] * (parts // 2), "shards should run int8 (AUTO, grid data) / fp16 (forced)"
     ol = torch.empty(m, dtype=torch.int32, device=DEV)
@@ -106,6 +114,31 @@ def test_cfg4_100m_train_sharded(knn):
                          ol.data_ptr(), oi.data_ptr(), od.data_ptr(), of.data_ptr())
     mc.sync()
     mc.close()
+    # the reference tie order across the shards: flagged queries resolved in
+    # batches of 4 (each query's 100M exact distances are 800 MB)
+    pend_all = torch.nonzero(of & knn.FLAG_TIE_PENDING).flatten().to(torch.int32)
+    resolved = pend_all.cpu().numpy()
+    rows = [r1 - r0 for r0, r1 in shards]
+    for b0 in range(0, pend_all.numel(), 4):
+        pend = pend_all[b0:b0 + 4].contiguous()
+        T = pend.numel()
+        blocks = []
+        for c, nr in zip(ctxs, rows):
+            D = torch.empty((T, nr), dtype=torch.float64, device=DEV)
+            c.shard_distances_device(Q.data_ptr(), pend.data_ptr(), T, knn.L2, D.data_ptr())
+            c.sync()
+            blocks.append(D.reshape(-1))
+        Dall = torch.cat(blocks)
+        del blocks
+        ctxs[0].tie_resolve_device(Dall.data_ptr(), rows, T, lab.data_ptr(), pend.data_ptr(), k,
+                                   ol.data_ptr(), oi.data_ptr(), od.data_ptr(), of.data_ptr())
+        ctxs[0].sync()
+        del Dall
+    for c in ctxs:
+        c.close()
+    flags = of.cpu().numpy()
+    assert not (flags & knn.FLAG_TIE_PENDING).any(), "queries left with a pending tie order"
+    print("cfg4: %d queries resolved in the reference tie order" % len(resolved))
     got, idx, dist = ol.cpu().numpy(), oi.cpu().numpy(), od.cpu().numpy()
     assert idx.min() >= 0 and idx.max() < n
     lab_all = lab.cpu().numpy()
@@ -119,15 +152,14 @@ def test_cfg4_100m_train_sharded(knn):
     qs = np.arange(0, m, m // 64)
     bf = brute_force_kdist(X, Q[qs], k)
     np.testing.assert_allclose(dist[qs], bf, rtol=1e-10, atol=0)
-    # the oracle, bit for bit, on a few queries
-    qs = np.arange(0, m, m // 4)
+    # the oracle, bit for bit, on 32 queries and the resolved ones
+    qs = np.unique(np.concatenate([np.arange(0, m, m // 32), resolved[:32]])).astype(np.int64)
     wl, wi, wdd = oracle_streamed(X, lab_all, Q, k, qs)
     np.testing.assert_array_equal(got[qs], wl)
     assert (dist[qs].view(np.int64) == wdd.view(np.int64)).all()
     for a, q in enumerate(qs):
+        if flags[q] & knn.FLAG_TIE_REF:
+            np.testing.assert_array_equal(idx[q], wi[a])  # the reference's own order
         for t in np.nonzero(idx[q] != wi[a])[0]:
             assert (dist[q] == dist[q][t]).sum() > 1, "query %d: index differs without a tie" % q
-    # exact-tie votes (equal distances, different labels in the top k): the
-    # reference cannot run this config (cpp:140 overflows), so there is no
-    # std::sort order to compare with; the count is reported
-    print("cfg4 tie-vote queries: %d of %d" % (int(((of.cpu().numpy() & knn.FLAG_TIE_VOTE) != 0).sum()), m))
+    print("cfg4 tie-vote queries: %d of %d" % (int(((flags & knn.FLAG_TIE_VOTE) != 0).sum()), m))

@@ -35,7 +35,7 @@ def knn():
 
 
 @pytest.fixture(scope="module",
-                params=["auto", "fp32", "m16", "fp16", "fp16w", "i8", "i8w", "ord", "ordh"])
+                params=["auto", "fp32", "m16", "fp16", "fp16w", "i8", "i8w", "ord", "ordh", "nb", "nbw"])
 def clf(knn, request):
     """Every parity test runs with the default candidate path (AUTO: int8 for
     integer-coded data and fp16 otherwise for batches of >= 4096 queries at
@@ -48,23 +48,29 @@ def clf(knn, request):
     every width (i8w); other data take the AUTO path.  ord / ordh: the train
     images in region order (tuning "order" = 4 regions, knn_order.hip) with
     the AUTO path and with fp16 forced: queries sorted by region, streams
-    starting at each query tile's region, lists mapped back to train rows."""
+    starting at each query tile's region, lists mapped back to train rows.
+    nb / nbw: the int8 path forced (16x16x64 / 32x32x32) on norm-blocked
+    images (tuning "nblk" = 1, knn_order.hip: every 16K-row window sorted by
+    code norm; nbw on top of the region order), where the int8 kernels'
+    sub-tile seed bound is tight."""
     c = knn.Classifier(0)
     c.set_precision({"auto": knn.PRECISION_AUTO, "fp32": knn.PRECISION_FP32,
                      "m16": knn.PRECISION_BF16X3, "fp16": knn.PRECISION_FP16,
                      "fp16w": knn.PRECISION_FP16, "i8": knn.PRECISION_AUTO,
                      "i8w": knn.PRECISION_AUTO, "ord": knn.PRECISION_AUTO,
-                     "ordh": knn.PRECISION_FP16}[request.param])
+                     "ordh": knn.PRECISION_FP16, "nb": knn.PRECISION_AUTO,
+                     "nbw": knn.PRECISION_AUTO}[request.param])
     c.set_tuning("mfma16", 1 if request.param == "m16" else -1)
-    if request.param in ("i8", "i8w"):
+    if request.param in ("i8", "i8w", "nb", "nbw"):
         c.set_tuning("i8", 1)
-    if request.param == "i8w":
+    if request.param in ("i8w", "nbw"):
         c.set_tuning("i8w", 1)
+    c.set_tuning("nblk", 1 if request.param in ("nb", "nbw") else -1)
     if request.param == "fp16w":
         c.set_tuning("s3q", 0)
         c.set_tuning("gk", 0)
     # (the train layout is decided at set_train: every case's own)
-    c.set_tuning("order", 4 if request.param in ("ord", "ordh") else 0)
+    c.set_tuning("order", 4 if request.param in ("ord", "ordh", "nbw") else 0)
     yield c
     c.close()
 

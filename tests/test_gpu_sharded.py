@@ -207,6 +207,57 @@ def test_partial_merge_reference_tie_order(knn, metric, ties):
         c.close()
 
 
+@pytest.mark.parametrize("metric", [0, 1])
+def test_hip_ties_default_stream(knn, metric):
+    """knn_dist.resolve_ties through knn_dist.HipTies as bench.py's mode b
+    drives it, here at world 1 and with HipTies' default stream (torch's
+    current one: the flags, the distance blocks and the library calls on one
+    stream): 3 shard contexts' lists merged in one context, every flagged
+    query resolved, labels = the oracle's, none left pending."""
+    import importlib.util
+    import os
+    import torch
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location(
+        "knn_dist", os.path.join(root, "-mpi-knn-_amd", "knn_dist.py"))
+    kd = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(kd)
+    dev = torch.device("cuda", 0)
+    tr, lab, te = _tie_set(metric, n=4001, m=250)
+    n, m, k = tr.shape[0], te.shape[0], 10
+    w = k + 1
+    shards = [(0, 1300), (1300, 2701), (2701, n)]
+    Q = torch.from_numpy(te).to(dev)
+    ctxs, gd, gi, gl = _sharded_blocks(knn, tr, lab, Q, shards, w, metric, dev)
+    for c in ctxs[1:]:
+        c.close()
+    # one context over every row (world 1): its shard distances cover all rows
+    c = ctxs[0]
+    Xa = torch.from_numpy(tr).to(dev)
+    La = torch.from_numpy(lab).to(dev)
+    c.set_train_device(Xa.data_ptr(), La.data_ptr(), n, tr.shape[1], 5, keep=(Xa, La))
+    outs = (torch.empty(m, dtype=torch.int32, device=dev),
+            torch.empty((m, k), dtype=torch.int64, device=dev),
+            torch.empty((m, k), dtype=torch.float64, device=dev),
+            torch.empty(m, dtype=torch.int32, device=dev))
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    c.merge_vote_device(gd.data_ptr(), gi.data_ptr(), gl.data_ptr(), 3, m, w, k,
+                        outs[0].data_ptr(), outs[1].data_ptr(), outs[2].data_ptr(),
+                        outs[3].data_ptr(), stream=stream)
+    ties = kd.HipTies(c, Q, La, n, k, outs, m, metric=metric, device=dev)
+    resolved = kd.resolve_ties(ties, m, dev)
+    torch.cuda.synchronize()
+    got, idx, dist, flags = (t.cpu().numpy() for t in outs)
+    want, widx, wdist = oracle.knn(tr, lab, te, k, metric == 0, 5, n_out=k)
+    assert resolved > 20 and ties.resolved == resolved
+    assert not (flags & knn.FLAG_TIE_PENDING).any()
+    np.testing.assert_array_equal(got, want)
+    ref = (flags & knn.FLAG_TIE_REF) != 0
+    np.testing.assert_array_equal(idx[ref], widx[ref])
+    assert_neighbors_match(idx, dist, widx, wdist, flags)
+    c.close()
+
+
 @pytest.mark.parametrize("k", [7, 1500])
 def test_merge_nonfinite_query(knn, k):
     """A query with a NaN / inf coordinate through both merge kernels (the LDS

@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--data", default="grid", choices=("grid", "continuous"))
     ap.add_argument("--order", type=int, default=-1,
                     help="region order of the train layout (tuning key 'order', set before set_train)")
+    ap.add_argument("--nblk", type=int, default=-1,
+                    help="norm blocks of the train layout (tuning key 'nblk', set before set_train)")
     ap.add_argument("variants", nargs="*", default=["auto:0:0", "auto:4:0", "auto:8:0", "fp32:0:0"])
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -39,6 +41,7 @@ def main():
     X, lab, Q, _ = bench.synth(a.n, a.m, a.d, 10, 1234, 5678, dev, data=a.data)
     clf = knn.Classifier(0)
     clf.set_tuning("order", a.order)
+    clf.set_tuning("nblk", a.nblk)
     clf.set_train_device(X.data_ptr(), lab.data_ptr(), a.n, a.d, 10, keep=(X, lab))
     clf.set_timing(True)
     out = torch.empty(a.m, dtype=torch.int32, device=dev)
@@ -53,7 +56,7 @@ def main():
     except AttributeError:
         cnt_fn = None
     selc = {}
-    cbuf = (ctypes.c_ulonglong * 4)()
+    cbuf = (ctypes.c_ulonglong * 6)()
     prec = {"auto": knn.PRECISION_AUTO, "fp32": knn.PRECISION_FP32, "bf16x3": knn.PRECISION_BF16X3,
             "m16": knn.PRECISION_BF16X3, "fp16": knn.PRECISION_FP16}
     defaults = {"gk": -1, "s3q": -1, "xhswz": 1, "i8": -1, "i8w": -1, "seed": 0, "ophase": -1, "s3gq": 0}
@@ -99,6 +102,9 @@ def main():
             print("%-14s int8 selection per launch: calls %d, lane passes %.4f, wave passes %.4f, "
                   "inserts per lane-call %.4f" % (v, c[0], c[1] / max(1, c[0]), c[2] * 64 / max(1, c[0]),
                                                  c[3] / max(1, c[0])))
+            if c[4]:
+                print("%-14s seed-free bound: sub-tile tests %d (wave), passing %.4f; exact wave passes "
+                      "per test %.4f" % (v, c[4], c[5] / c[4], c[2] / c[4]))
         ms = np.median(res[v])
         print("%-14s cand %8.3f ms (min %8.3f)  %7.1f TF/s  all phases %8.3f ms  %s rescans=%d "
               "same_labels=%s" % (v, ms, np.min(res[v]), flops / ms / 1e9, np.median(tot[v]),
