@@ -555,13 +555,18 @@ static bool use_i8(const knn_ctx* ctx, int metric, int64_t m, int W) {
 }
 
 // Which int8 kernel: metric 6 (v_mfma_i32_32x32x32_i8, K granularity 32)
-// where it issues fewer padded dims than metric 5 (16x16x64, K 64): d = 96
-// runs 96 dims instead of 128 (configs[3]).  Tuning key "i8w": -1 auto,
-// 0 always 16x16x64, 1 always 32x32x32.
+// where it issues fewer padded dims than metric 5 (16x16x64, K 64) -- d = 96
+// runs 96 dims instead of 128 (configs[3]) -- and at DP = 128 (cfg2), where
+// its two 4-entry lists per lane (KNN_I8W_Q4) made it the faster kernel:
+// 1.278-1.290 vs 1.290-1.303 ms candidate, all phases 1.466-1.478 vs
+// 1.500-1.518 ms (profiles/ab_log.md r5g; its 32x32 MFMA holds the vector
+// issue for 8 of 32 cycles, the 16x16x64 one for 8 of 16).  Tuning key
+// "i8w": -1 auto, 0 always 16x16x64, 1 always 32x32x32.
 static int i8_kernel(const knn_ctx* ctx) {
   const int d = ctx->train.d;
   if (ctx->tune_i8w >= 0) return ctx->tune_i8w > 0 && pad_dim_i8w(d) > 0 ? 6 : 5;
-  return pad_dim_i8w(d) > 0 && pad_dim_i8w(d) < pad_dim_i8(d) ? 6 : 5;
+  const int w = pad_dim_i8w(d);
+  return w > 0 && (w < pad_dim_i8(d) || w == 128) ? 6 : 5;
 }
 
 static bool use_bf16x3(const knn_ctx* ctx, int metric) {
@@ -623,8 +628,11 @@ static void choose_geometry(knn_ctx* ctx, int metric, bool streamed, int DP, int
   int S_hi = (int)std::max<int64_t>(1, std::min<int64_t>(64, n_tiles));
   int bestS = 1, bestR = 8;
   const bool quad = !streamed && metric >= 3 && metric <= 5;  // 16x16 layouts (bf16x3, fp16, int8)
-  const bool pair4 = metric == 6;  // int8 on 32x32x32: 2 lists of R = 8 (or 4) per split
-  const int lps = quad || s3q ? 4 : 2;  // lists per query per split
+  // int8 on 32x32x32: 4 lists of R = 4 per split (two per lane), or 2 of R =
+  // 8 (one per lane, tuning "R" = 8)
+  const bool pair4 = metric == 6;
+  const bool w4 = pair4 && ctx->tune_R != 8;
+  const int lps = quad || s3q || w4 ? 4 : 2;  // lists per query per split
   // S3 on 16x16x32 (s3q): R = 8 quad lists, 4 * S * 8 <= kMaxUnion entries
   if (s3q) S_hi = std::min(S_hi, kMaxUnion / (4 * 8));
   for (int R : {4, 8, 16}) {
@@ -633,7 +641,7 @@ static void choose_geometry(knn_ctx* ctx, int metric, bool streamed, int DP, int
     // only on request (resident kernel; tuning experiments)
     // (int8: R = 8 quad lists on request, tuning key "R")
     const bool q8 = quad && metric == 5 && ctx->tune_R == 8;
-    if (pair4 ? R != (ctx->tune_R == 4 ? 4 : 8) : quad ? R != (q8 ? 8 : 4)
+    if (pair4 ? R != (w4 ? 4 : 8) : quad ? R != (q8 ? 8 : 4)
               : (ctx->tune_R ? R != ctx->tune_R : R == 4))
       continue;
     if (R == 4 && (DP > 256 || metric == 1)) continue;
@@ -869,14 +877,15 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   const int s3q_S = (W * 5 + 15) / 16;
   const bool s3q = s3h && ctx->tune_s3q != 0 && s3q_S <= kMaxUnion / 32 && s3q_S <= n_tiles;
   choose_geometry(ctx, kmetric, s3, DP, nw, n_qt, n_tiles, W, C, s3q, S, R);
-  // 16x16 layouts: 4 lists per query per split
-  const bool quad_lists = (!s3 && kmetric >= 3 && kmetric <= 5) || s3q;
+  // metric 6: 4 lists of R = 4 per query per split (two per lane, one per
+  // half of its rows: knn_cand_res.hip, KNN_I8W_Q4), the quad layout of the
+  // 16x16 kernels; tuning "R" = 8 selects one list of 8 per lane (2 per
+  // query per split, round 4's form)
+  const bool w4 = kmetric == 6 && ctx->tune_R != 8;
+  if (kmetric == 6) R = w4 ? 4 : 8;
+  // 16x16 layouts (and w4): 4 lists per query per split
+  const bool quad_lists = (!s3 && kmetric >= 3 && kmetric <= 5) || s3q || w4;
   if (quad_lists && !s3q && !(kmetric == 5 && R == 8)) R = 4;
-  // metric 6: 2 lists per query per split (pair_min filter), R = 8 by default:
-  // at a 12.5M x 96 shard R = 4 runs the candidate pass 2.7 % faster but
-  // sends 5 of 10k queries to the rescan (all phases 12.59 vs 12.27 ms,
-  // profiles/ab_log.md r4g4); tuning "R" = 4 selects the short lists
-  if (kmetric == 6) R = ctx->tune_R == 4 ? 4 : 8;
   const int NL = (quad_lists ? 4 : 2) * S;
   C = std::min(C, NL * R);
   // rescan workspace: the fast path serves the first `cap` failed queries

@@ -89,6 +89,15 @@ static_assert(KNN_RES_TPB * knnk::kTR == knnk::kResTileRows || KNN_RES_TPB != 2,
 #ifndef KNN_I8_SMAX5
 #define KNN_I8_SMAX5 0
 #endif
+// int8 on 32x32x32 (metric 6) with R = 4: each lane keeps TWO lists of 4,
+// one per half of its 16 rows (i < 8: rows (i&3) + 8(i>>2), c = 0, 1; i >= 8:
+// c = 2, 3) -- 4 lists of 4 per query per split, the merge's quad layout of
+// the 16x16 kernels -- instead of one list of 8: an insertion then shifts 4
+// entries instead of 8 (the selection's slow path is most of its cost,
+// profiles/ab_log.md r5e) at the 16x16 kernels' certification odds.
+#ifndef KNN_I8W_Q4
+#define KNN_I8W_Q4 1
+#endif
 
 
 namespace knnk {
@@ -315,6 +324,21 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
     }
     thr[b] = KNN_INF_F;
   }
+  // W4 (KNN_I8W_Q4, metric 6 at R = 4): the lane's second list (rows of its
+  // values i >= 8); L[0] holds i < 8
+  constexpr bool W4 = I8W && R == 4 && KNN_I8W_Q4 && ILIST && KNN_I8_SMAX;
+  int L2[W4 ? R : 1], I2[W4 ? R : 1];
+#pragma unroll
+  for (int t = 0; t < (W4 ? R : 1); ++t) {
+    L2[t] = kI8Floor;
+    I2[t] = -1;
+  }
+  // the lane's lists' threshold (the smaller R-th proxy of the two under W4:
+  // the merge bounds dropped rows by the min over a split's lists)
+  auto lane_thr = [&]() {
+    if constexpr (W4) return __builtin_fminf(lval(L[0][R - 1]), lval(L2[R - 1]));
+    else return lval(L[0][R - 1]);
+  };
   // the int8 selection on either list form
   auto select_i8 = [&](const auto& a, const auto& b, int row0, auto& Lq, auto& Iq, float& teq,
                        int& tnq, SelCount& sc) {
@@ -457,7 +481,8 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
 #pragma unroll
         for (int e = 0; e < 4; ++e) b[4 * c + e] = a[4 * c + e] + g[e];
       }
-      select_block_i8<R>(b, row0, L[0], I[0], tn[0], selc);
+      if constexpr (W4) select_block_i8w4<R>(b, row0, L[0], I[0], L2, I2, tn[0], selc);
+      else select_block_i8<R>(b, row0, L[0], I[0], tn[0], selc);
     }
    }
   };
@@ -519,6 +544,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
     if constexpr (TEC) {
 #pragma unroll
       for (int b = 0; b < NQL; ++b) thr[b] = lval(L[b][R - 1]);  // for the exchange below
+      if constexpr (W4) thr[0] = lane_thr();
     }
     {
       // this wave's pieces of tile `it` have landed once at most the pieces
@@ -594,6 +620,12 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
               float u[4];
 #pragma unroll
               for (int e = 0; e < 4; ++e) u[e] = lval(L[0][e]);
+              if constexpr (W4) {
+                float u2[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) u2[e] = lval(L2[e]);
+                merge_top4(u, u2);  // the lane's 4 best over both lists
+              }
               m = union_kth<2>(u, gk);
             } else {
               const auto sw = __builtin_amdgcn_permlane32_swap(
@@ -987,6 +1019,16 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
                                                 lval(L[qb][t + 2]), lval(L[qb][t + 3]));
         *(int4*)(out_i + o + t) = make_int4(I[qb][t], I[qb][t + 1], I[qb][t + 2], I[qb][t + 3]);
       }
+    }
+  } else if constexpr (W4) {
+    // 4 lists per query per split, [query][4S][R]: list 2h + half
+#pragma unroll
+    for (int li = 0; li < 2; ++li) {
+      const int64_t o = (qg * (4 * S) + split * 4 + 2 * h + li) * R;
+      const int* Ls = li ? L2 : L[0];
+      const int* Is = li ? I2 : I[0];
+      *(float4*)(out_v + o) = make_float4(lval(Ls[0]), lval(Ls[1]), lval(Ls[2]), lval(Ls[3]));
+      *(int4*)(out_i + o) = make_int4(Is[0], Is[1], Is[2], Is[3]);
     }
   } else if constexpr (ILIST) {
     float Lf[R];

@@ -619,6 +619,47 @@ __device__ __forceinline__ void select_block_i8(const i32x16& a, int row0, int (
   }
 }
 
+// select_block_i8 with two lists per lane (metric 6, KNN_I8W_Q4): values i <
+// 8 go to (L, I), i >= 8 to (L2, I2); tn >= both lists' R-th entries
+template <int R>
+__device__ __forceinline__ void select_block_i8w4(const i32x16& a, int row0, int (&L)[R], int (&I)[R],
+                                                  int (&L2)[R], int (&I2)[R], int& tn, SelCount& sc) {
+  const int h0 = max(max(max(a[0], a[1]), max(a[2], a[3])), max(max(a[4], a[5]), max(a[6], a[7])));
+  const int h1 = max(max(max(a[8], a[9]), max(a[10], a[11])),
+                     max(max(a[12], a[13]), max(a[14], a[15])));
+#if KNN_COUNT_SEL
+  sc.calls++;
+  sc.lane_pass += max(h0, h1) > tn;
+  sc.wave_pass += __builtin_amdgcn_ballot_w64(max(h0, h1) > tn) != 0;
+#endif
+  if (__builtin_amdgcn_ballot_w64(h0 > tn)) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int v = a[i];
+      if (v > tn) {
+#if KNN_COUNT_SEL
+        sc.inserts++;
+#endif
+        list_insert_desc<R>(L, I, v, row_at(row0, (i & 3) + 8 * (i >> 2)));
+        tn = max(tn, L[R - 1]);
+      }
+    }
+  }
+  if (__builtin_amdgcn_ballot_w64(h1 > tn)) {
+#pragma unroll
+    for (int i = 8; i < 16; ++i) {
+      const int v = a[i];
+      if (v > tn) {
+#if KNN_COUNT_SEL
+        sc.inserts++;
+#endif
+        list_insert_desc<R>(L2, I2, v, row_at(row0, (i & 3) + 8 * (i >> 2)));
+        tn = max(tn, L2[R - 1]);
+      }
+    }
+  }
+}
+
 // KNN_I8_SLOW = 2: the slow path inserts each lane's best passing value
 // first, found with its position by a max over keys acc * 8 + position
 // (exact and order-preserving: acc >= kI8Floor = -2^23), and tests the lane's second

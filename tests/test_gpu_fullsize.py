@@ -162,7 +162,7 @@ def test_cfg2_full(knn):
     clf.set_train_device(X.data_ptr(), lab.data_ptr(), n, d, C, keep=(X, lab))
     got, idx, dist, flags = classify(knn, clf, Q, k)
     # 8-bit grid data (bench.synth's byte features): the int8 pass, exact
-    assert clf.last_candidate_path() == 5, "cfg2 should run the int8 candidate pass"
+    assert clf.last_candidate_path() == 6, "cfg2 should run the int8 candidate pass (32x32x32)"
     assert clf.last_rescan_count() * 64 <= m
     lab_all = lab.cpu().numpy()
     check_properties(X, lab_all, Q, k, got, idx, dist, np.arange(m))

@@ -55,6 +55,8 @@ def test_region_order_changes_no_result(knn, path):
         c.set_tuning("ophase", 0 if order == 64 else -1)
         if path == "fp16":
             c.set_precision(knn.PRECISION_FP16)
+        if path == "i8":  # the 16x16x64 kernel (AUTO takes 32x32x32 at d = 128)
+            c.set_tuning("i8w", 0)
         c.set_train(tr, lab, classes)
         got, idx, dist, flags = c.classify(te, k, 0, return_neighbors=True)
         assert c.last_candidate_path() == {"i8": 5, "i8w": 6, "fp16": 4}[path]
@@ -108,6 +110,7 @@ def test_region_order_large_query_batch(knn):
     for order in (0, -1):
         c = knn.Classifier(0)
         c.set_tuning("order", order)
+        c.set_tuning("i8w", 0)  # the 16x16x64 kernel (AUTO takes 32x32x32 at d = 128)
         c.set_train(tr, lab, classes)
         got, idx, dist, _ = c.classify(te, 10, 0, return_neighbors=True)
         assert c.last_candidate_path() == 5

@@ -287,11 +287,11 @@ def _grid_codes(rng, n, m, d, classes, lo=0, hi=255, scale=256.0):
 
 def _i8_kernel(d, i8w):
     """(kernel metric, padded dim) the int8 pass runs at: 32x32x32 (metric 6,
-    K granularity 32) where it pads less than 16x16x64 (metric 5, K 64), or
-    as forced by the "i8w" tuning key."""
+    K granularity 32) where it pads less than 16x16x64 (metric 5, K 64) and
+    at DP = 128, or as forced by the "i8w" tuning key."""
     w = min(p for p in (32, 64, 96, 128, 160, 192, 256) if p >= d)
     q = (d + 63) // 64 * 64
-    if i8w == 1 or (i8w < 0 and w < q):
+    if i8w == 1 or (i8w < 0 and (w < q or w == 128)):
         return 6, w
     return 5, q
 
@@ -316,8 +316,8 @@ def test_int8_codes(knn, d, i8w):
             c.set_tuning("i8", 1)
         run_case(c, knn, tr, lab, te, 10, 0, 7)
         assert c.last_candidate_path() == km, mode
-        # (metric 6 keeps 8-entry lists by default, knn_api.cpp)
-        assert c.last_kernel_name().startswith("cand_kernel<%d,%d,%d,8>" % (dp, 8 if km == 6 else 4, km))
+        # (metric 6: two 4-entry lists per lane by default, knn_api.cpp)
+        assert c.last_kernel_name().startswith("cand_kernel<%d,4,%d,8>" % (dp, km))
         assert c.last_rescan_count() * 16 <= te.shape[0]
         c.close()
 

@@ -1,12 +1,13 @@
 #!/bin/bash
 # Two SQ counter passes (<= 8 SQ counters each, their own runs) over a short
-# cfg2 bench: issue/wait breakdown of the candidate kernel.
+# cfg2 bench (or the WLARGS workload): issue/wait breakdown of the candidate kernel.
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 TAG=${TAG:-r2k}
 OUT=$GRAFT_REPO_ROOT/gpurun_out/pmc_sq_$TAG
 mkdir -p "$OUT"
-B="--steps 3 --warmup 1 --no-cpu-baseline --no-fp32-path --no-continuous --cfg3-queries 0 --no-dropin --no-train-sharded --no-cfg5"
+# WLARGS: another workload's bench arguments (default: cfg2)
+B="${WLARGS:---steps 3 --warmup 1} --no-cpu-baseline --no-fp32-path --no-continuous --cfg3-queries 0 --no-dropin --no-train-sharded --no-cfg5"
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
   SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE \
   --kernel-trace -d "$OUT/p1" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" $B \

@@ -36,6 +36,10 @@ WORKLOADS = {
     "cfg4": dict(steps=3, warmup=1, n_train=100_000_000, queries=10_000, dim=96, k=10),
     "cfg5": dict(steps=4, warmup=1, n_train=1_000_000, queries=10_000, dim=960, k=100),
     "cfg4s": dict(steps=5, warmup=1, n_train=12_500_000, queries=10_000, dim=96, k=10),
+    "cfg2c": dict(steps=10, warmup=2, n_train=1_000_000, queries=10_000, dim=128, k=10,
+                  data="continuous"),
+    "cfg2f32": dict(steps=4, warmup=1, n_train=1_000_000, queries=10_000, dim=128, k=10,
+                    precision="fp32"),
 }
 
 
@@ -104,7 +108,8 @@ def main():
         if os.path.isdir(fdir) and os.path.isdir(wdir):
             fetch = traffic_json.per_launch(fdir, "FETCH_SIZE")
             write = traffic_json.per_launch(wdir, "WRITE_SIZE")
-            tr = {"workload": {key: wl[key] for key in ("n_train", "queries", "dim", "k")},
+            tr = {"workload": {key: wl[key] for key in ("n_train", "queries", "dim", "k", "data")
+                               if key in wl},
                   "kernel_src_sha": bench.kernel_src_sha(),
                   "formula": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE half-count "
                              "correction; KiB units)", "kernels": {}}
