@@ -224,9 +224,11 @@ __device__ __forceinline__ bool bound_ok(double LB, double dw, double qa, double
   return (LB - E) * (1.0 - 1e-12) > dw * (1.0 + 1e-12);
 }
 
+// (EPT 8, the small candidate sets of cfg2: 6 waves per SIMD at 80 VGPRs,
+// -6 us per cfg2 step against 5 at 83, profiles/ab_log.md r4mg)
 template <int METRIC, int NT, int EPL, int EPT = 16>
 __global__ void __launch_bounds__(NT)
-__attribute__((amdgpu_waves_per_eu(EPT == 8 ? 5 : 1)))
+__attribute__((amdgpu_waves_per_eu(EPT == 8 ? 6 : 1)))
 merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, int U, int R,
                     TrainDev t, const double* __restrict__ Q64, int W, int Cmax, int C2,
                     double f_err, ProxyScale ps, const uint32_t* __restrict__ gthr, Sink sink,
