@@ -103,7 +103,7 @@ static_assert(KNN_RES_TPB * knnk::kTR == knnk::kResTileRows || KNN_RES_TPB != 2,
 namespace knnk {
 
 #if KNN_COUNT_SEL
-__device__ unsigned long long knn_sel_cnt[6];
+__device__ unsigned long long knn_sel_cnt[8];
 #endif
 
 // (lgkmcnt(0): every LDS read of the wave -- the int8 kernels' seed reads of
@@ -444,6 +444,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
     return __builtin_bit_cast(i32x4, *(const float4*)(sb + (I8W ? 8 * c + 4 * h : 16 * c + 4 * g16) * RSF + SEED));
   };
   int smxp = 0;  // PIPE: smx of the pending sub-tile
+  [[maybe_unused]] int cnt_it = 0;  // (KNN_COUNT_SEL: the staged tile being selected)
   auto sel5 = [&](const auto& a, int row0, int smx, auto&& sd) {  // a: i32x4 [2][QB]
    if constexpr (SMX) {
     bool pass = false;
@@ -472,6 +473,8 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
 #if KNN_COUNT_SEL
     selc.bcalls++;
     selc.bpass += __builtin_amdgcn_ballot_w64(mx > tn[0] - smx) != 0;
+    selc.bcold += cnt_it < 2;
+    selc.bpcold += cnt_it < 2 && __builtin_amdgcn_ballot_w64(mx > tn[0] - smx) != 0;
 #endif
     if (__builtin_amdgcn_ballot_w64(mx > tn[0] - smx)) {
       i32x16 b = a;
@@ -541,6 +544,9 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   int cur = 0, nxt = PD;  // buffer of tile it, buffer that tile it+PD goes to
   for (int it = 0; it < my_nt; ++it) {
     const int t = tile_at(it);
+#if KNN_COUNT_SEL
+    cnt_it = it;
+#endif
     if constexpr (TEC) {
 #pragma unroll
       for (int b = 0; b < NQL; ++b) thr[b] = lval(L[b][R - 1]);  // for the exchange below
@@ -1006,6 +1012,8 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
     atomicAdd(&knn_sel_cnt[3], (unsigned long long)selc.inserts);
     if (lane == 0) atomicAdd(&knn_sel_cnt[4], (unsigned long long)selc.bcalls);
     if (lane == 0) atomicAdd(&knn_sel_cnt[5], (unsigned long long)selc.bpass);
+    if (lane == 0) atomicAdd(&knn_sel_cnt[6], (unsigned long long)selc.bcold);
+    if (lane == 0) atomicAdd(&knn_sel_cnt[7], (unsigned long long)selc.bpcold);
   }
 #endif
   if constexpr (M16) {
@@ -1151,15 +1159,15 @@ KNN_GROUP_DPS(KNN_DEF)
 // selection counts of a KNN_COUNT_SEL build (DP 96 / 128), zeros otherwise.
 int res_sel_counters(unsigned long long* out, int reset) {
 #if KNN_COUNT_SEL
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(knn_sel_cnt), 6 * sizeof(unsigned long long)) != hipSuccess)
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(knn_sel_cnt), 8 * sizeof(unsigned long long)) != hipSuccess)
     return -1;
   if (reset) {
-    const unsigned long long z[6] = {0, 0, 0, 0, 0, 0};
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(knn_sel_cnt), z, sizeof z) != hipSuccess) return -1;
   }
 #else
   (void)reset;
-  for (int i = 0; i < 6; ++i) out[i] = 0;
+  for (int i = 0; i < 8; ++i) out[i] = 0;
 #endif
   return 0;
 }

@@ -486,6 +486,7 @@ __device__ __forceinline__ int i8_neg_half(float te) {
 struct SelCount {
   unsigned calls = 0, lane_pass = 0, wave_pass = 0, inserts = 0;
   unsigned bcalls = 0, bpass = 0;  // seed-free int8: sub-tile bound tests / waves passing them
+  unsigned bcold = 0, bpcold = 0;  // the same in a workgroup's first two staged tiles
 };
 template <int R>
 __device__ __forceinline__ void select_quad_i8(const i32x4& a, const i32x4& b, int row0,

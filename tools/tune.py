@@ -56,7 +56,7 @@ def main():
     except AttributeError:
         cnt_fn = None
     selc = {}
-    cbuf = (ctypes.c_ulonglong * 6)()
+    cbuf = (ctypes.c_ulonglong * 8)()
     prec = {"auto": knn.PRECISION_AUTO, "fp32": knn.PRECISION_FP32, "bf16x3": knn.PRECISION_BF16X3,
             "m16": knn.PRECISION_BF16X3, "fp16": knn.PRECISION_FP16}
     defaults = {"gk": -1, "s3q": -1, "xhswz": 1, "i8": -1, "i8w": -1, "seed": 0, "ophase": -1, "s3gq": 0}
@@ -105,6 +105,9 @@ def main():
             if c[4]:
                 print("%-14s seed-free bound: sub-tile tests %d (wave), passing %.4f; exact wave passes "
                       "per test %.4f" % (v, c[4], c[5] / c[4], c[2] / c[4]))
+            if c[6]:
+                print("%-14s   first two staged tiles: %d tests (%.3f of all), passing %.4f -> %.3f of "
+                      "all passing tests" % (v, c[6], c[6] / c[4], c[7] / c[6], c[7] / max(1, c[5])))
         ms = np.median(res[v])
         print("%-14s cand %8.3f ms (min %8.3f)  %7.1f TF/s  all phases %8.3f ms  %s rescans=%d "
               "same_labels=%s" % (v, ms, np.min(res[v]), flops / ms / 1e9, np.median(tot[v]),
