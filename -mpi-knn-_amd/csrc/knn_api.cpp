@@ -905,7 +905,16 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   // and 2-4 % faster than the list thresholds (in-process A/B,
   // profiles/ab_log.md: r2f_ab_gk, r2g_ab_pair); K = 1 (8 rows < W) sends 5 %
   // of the queries to the rescan.
-  int gk = (W + 5 + kGthrSlots - 1) / kGthrSlots;
+  // slot groups G (resident kernel): the first grid round of a 10k batch
+  // runs only ~6 of the 38 splits of each query tile, so with 8 groups group
+  // 7 has published nothing until the second round and tq = max over the
+  // slots stays +inf there; with 4 groups (K = (W + 5) / 4, the same G K >=
+  // W + 5 rows below tq) every group has a split in round 1: cfg2 candidate
+  // -0.5..0.9 %, the 12.5M x 96 shard -0.5 % (profiles/ab_log.md r5n).  Auto:
+  // 4 where K stays <= 4 (W <= 11), else 8; tuning "gg" 4 / 8 forces.
+  const int G = s3 ? kGthrSlots
+                   : ctx->tune_gg > 0 ? ctx->tune_gg : ((W + 5 + 3) / 4 <= 4 ? 4 : kGthrSlots);
+  int gk = (W + 5 + G - 1) / G;
   if (gk > (s3 ? 16 : 4)) gk = 0;
   if (ctx->tune_gk >= 0) gk = std::min(ctx->tune_gk, s3 ? 16 : 4);
   const bool use_gthr = (s3 ? s3q && gk > 0 : DP <= 256) && !(ctx->tune_ablate & 4);
@@ -1009,12 +1018,14 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   cl.gk = gk;
   cl.xsw = kmetric >= 5 ? ctx->i8_swz : ctx->xh_swz;
   cl.qstart = qstart;
+  cl.gmask = gk ? G - 1 : 3;
+  cl.qblk = ctx->tune_qblk > 0 ? std::min(ctx->tune_qblk, n_qt) : 0;
   // slots of groups without a split stay 0 (never the max)
   // (experiment, tuning "ablate" bit 5: keep the previous call's final
   // thresholds -- valid only for a repeat of the same queries; measures what
   // perfectly seeded thresholds would save)
   if (use_gthr && !(ctx->tune_ablate & 32)) {
-    const int active = std::min(S, gk ? 8 : 4);
+    const int active = std::min(S, gk ? G : 4);
     const int64_t ns = (kmetric == 4 || kmetric == 5) && !s3 ? seed_rows(ctx) : 0;
     bool seeded = false;
     if (ns > 0) {
@@ -1033,7 +1044,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
       cs.gthr = nullptr;
       cs.ablate = 0;
       if (launch_cand(cs, s)) {
-        launch_seed_gthr((const float*)ctx->smp_v.p, m_pad, Us, gk ? kGthrSlots * gk : 4 * R, active,
+        launch_seed_gthr((const float*)ctx->smp_v.p, m_pad, Us, gk ? G * gk : 4 * R, active,
                          cl.gthr, s);
         seeded = true;
       }
@@ -1522,6 +1533,12 @@ int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value) {
     if (value < -1 || value > kRegionMax)
       return knn_fail(KNN_ERR_ARG, "order must be -1 (auto), 0, 1 or 2..64 regions");
     ctx->tune_order = (int)value;
+  } else if (!strcmp(key, "qblk")) {
+    if (value < 0 || value > 1 << 20) return knn_fail(KNN_ERR_ARG, "qblk must be 0 (split-major) or >= 1");
+    ctx->tune_qblk = (int)value;
+  } else if (!strcmp(key, "gg")) {
+    if (value != -1 && value != 4 && value != 8) return knn_fail(KNN_ERR_ARG, "gg must be -1 (auto), 4 or 8");
+    ctx->tune_gg = (int)value;
   } else if (!strcmp(key, "nblk")) {
     if (value < -1 || value > 1) return knn_fail(KNN_ERR_ARG, "nblk must be -1 (auto), 0 or 1");
     ctx->tune_nblk = (int)value;

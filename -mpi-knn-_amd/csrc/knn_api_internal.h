@@ -75,6 +75,8 @@ struct knn_ctx {
   // norm blocks (knn_order.hip): -1 auto (integer-coded train sets, d <= 256),
   // 0 off, 1 on; ord_nb: the current layout has them (ord_perm / ord_ipos valid)
   int tune_nblk = -1;
+  int tune_gg = -1;
+  int tune_qblk = 0;           // resident kernel workgroup order: 0 split-major, B query blocks            // gthr slot groups of the resident kernel: -1 auto (8), 4 or 8
   bool ord_nb = false;
   int tune_s3gq = 0;           // S3 kernel: largest XCD query-tile grouping (0 = kS3GqMax)
   // query streams start at one of N phases of the region chain (P regions in

@@ -196,7 +196,7 @@ __global__ void __launch_bounds__(NW * 64)
 __attribute__((amdgpu_waves_per_eu(res_wpe<DP, R, METRIC>())))
 cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
             int n_qt, float* __restrict__ out_v, int* __restrict__ out_i, int abl,
-            uint32_t* gthr, int gk, int xsw, const int* __restrict__ qstart) {
+            uint32_t* gthr, int gk, int xsw, const int* __restrict__ qstart, int gmask, int qblk) {
 #if !KNN_ABLATIONS
   abl = 0;  // (folds every ablation check below)
 #endif
@@ -234,8 +234,22 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   __shared__ __attribute__((aligned(16))) float lds[NB * BUFF];
 
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int split = bid / n_qt;
-  const int qt = bid - split * n_qt;
+  // workgroup -> (split, query tile): split-major (qblk 0: the XCD's
+  // concurrent workgroups are one split's consecutive query tiles), or query
+  // blocks of qblk tiles, splits outer inside a block (the first grid round
+  // then holds most splits of the first blocks' queries)
+  int split, qt;
+  if (qblk > 0) {
+    const int blk = bid / (qblk * S);
+    const int qt0 = blk * qblk;
+    const int bb = min(qblk, n_qt - qt0);
+    const int w = bid - blk * qblk * S;
+    split = w / bb;
+    qt = qt0 + (w - split * bb);
+  } else {
+    split = bid / n_qt;
+    qt = bid - split * n_qt;
+  }
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int j = lane & 31, h = lane >> 5;
@@ -382,7 +396,9 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   const uint32_t goff =
       M16 ? (uint32_t)(((int64_t)qt * (NW * QW) + wv * QW + (lane & (QW - 1))) * (4 * kGthrSlots))
           : (uint32_t)(qg * (4 * kGthrSlots));
-  const uint32_t* gslot = gthr + (gk ? (split & 7) : (split & 3));
+  // slot group of this split: split % G, G = gmask + 1 (8 with gk > 0 by
+  // default, 4 for the lists' R-th entries; the host may use 4 with gk > 0)
+  const uint32_t* gslot = gthr + (split & gmask);
   float tq[NQL], te[NQL];
   int tn[NQL];  // int8: i8_neg_half(te), the filter on the accumulators
 #pragma unroll
@@ -1074,7 +1090,7 @@ static void launch_res(const CandLaunch& c, hipStream_t s) {
   hipLaunchKernelGGL((cand_kernel<DP, R, METRIC, NW>), dim3((unsigned)(c.n_qt * c.S)),
                      dim3(NW * 64), 0, s, c.X32, c.Q32, (int)(c.n_pad / (kTR * res_tpb<METRIC>())), c.S,
                      c.n_qt,
-                     c.out_v, c.out_i, c.ablate, c.gthr, c.gk, c.xsw, c.qstart);
+                     c.out_v, c.out_i, c.ablate, c.gthr, c.gk, c.xsw, c.qstart, c.gmask, c.qblk);
 }
 
 // Instantiated variants: R in {4, 8, 16}; METRIC 0/2 with NW in {4, 8};

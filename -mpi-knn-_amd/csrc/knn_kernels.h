@@ -129,6 +129,8 @@ struct CandLaunch {
   // split's stream at the first of its tiles at or after qstart[first
   // query of the tile] (null: at the split's first tile)
   const int* qstart = nullptr;
+  int gmask = 7;   // slot groups of gthr - 1: a split publishes into slot split & gmask
+  int qblk = 0;    // workgroup order: 0 split-major, B: query blocks of B tiles (cand_kernel)
 };
 constexpr uint32_t kGthrInit = 0xFF800000u;  // order-preserving key of +inf
 constexpr int kGthrSlots = 8;                // slots per query in gthr

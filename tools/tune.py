@@ -59,7 +59,8 @@ def main():
     cbuf = (ctypes.c_ulonglong * 8)()
     prec = {"auto": knn.PRECISION_AUTO, "fp32": knn.PRECISION_FP32, "bf16x3": knn.PRECISION_BF16X3,
             "m16": knn.PRECISION_BF16X3, "fp16": knn.PRECISION_FP16}
-    defaults = {"gk": -1, "s3q": -1, "xhswz": 1, "i8": -1, "i8w": -1, "seed": 0, "ophase": -1, "s3gq": 0}
+    defaults = {"gk": -1, "s3q": -1, "xhswz": 1, "i8": -1, "i8w": -1, "seed": 0, "ophase": -1, "s3gq": 0,
+                "gg": -1, "qblk": 0}
     for r in range(a.rounds + 1):
         for v in a.variants:
             base, *extra = v.split(",")
