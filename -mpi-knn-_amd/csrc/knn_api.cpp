@@ -229,12 +229,28 @@ static int build_order(knn_ctx* ctx, const double* dX, const double* mu, int64_t
                        (float*)ctx->ord_cnorm.p, key, rank, ctx->stream);
   launch_region_assign(dX, mu, n, d, 1, jx, (const unsigned short*)ctx->ord_img.p,
                        (const float*)ctx->ord_cnorm.p, rank, key, nullptr, ctx->stream);
+  ctx->ord_bcnt_zero = 0;  // (the train sort leaves its prefix sums there)
   launch_region_sort(key, n, (int*)ctx->ord_bcnt.p, (int*)ctx->ord_tot.p, (int*)ctx->ord_perm.p,
                      (int*)ctx->ord_ipos.p, nullptr, nullptr, (int*)ctx->ord_rstart.p, ctx->stream);
   HIP_TRY(hipGetLastError());
   ctx->ord_P = P;
   return KNN_OK;
 }
+
+// Which int8 kernel: metric 6 (v_mfma_i32_32x32x32_i8, K granularity 32)
+// where it issues fewer padded dims than metric 5 (16x16x64, K 64) -- d = 96
+// runs 96 dims instead of 128 (configs[3]) -- and at DP = 128 (cfg2), where
+// its two 4-entry lists per lane (KNN_I8W_Q4) made it the faster kernel:
+// 1.278-1.290 vs 1.290-1.303 ms candidate, all phases 1.466-1.478 vs
+// 1.500-1.518 ms (profiles/ab_log.md r5g; its 32x32 MFMA holds the vector
+// issue for 8 of 32 cycles, the 16x16x64 one for 8 of 16).  Tuning key
+// "i8w": -1 auto, 0 always 16x16x64, 1 always 32x32x32.
+static int i8_kernel_d(const knn_ctx* ctx, int d) {
+  if (ctx->tune_i8w >= 0) return ctx->tune_i8w > 0 && pad_dim_i8w(d) > 0 ? 6 : 5;
+  const int w = pad_dim_i8w(d);
+  return w > 0 && (w < pad_dim_i8(d) || w == 128) ? 6 : 5;
+}
+static int i8_kernel(const knn_ctx* ctx) { return i8_kernel_d(ctx, ctx->train.d); }
 
 // Norm blocks (knn_order.hip, launch_norm_blocks): the int8 kernels bound a
 // sub-tile by its largest seed instead of reading every row's seed from LDS
@@ -261,9 +277,14 @@ static int build_norm_blocks(knn_ctx* ctx, const double* dX, int64_t n, int d) {
     perm0 = (const int*)ctx->ord_perm0.p;
   }
   const bool i8 = ctx->i8_ok;
+  // norm ranks interleaved over the int8 kernel's lane lists and sub-tiles
+  // spread over the window's tiles (nblk 2: the plain sorted windows, round
+  // 5's layout; 3: the interleave only)
+  const int il = !i8 || ctx->tune_nblk == 2 ? 0
+                 : i8_kernel_d(ctx, d) | (ctx->tune_nblk == 3 ? 0 : 16);
   launch_norm_blocks(dX, i8 ? (const double*)ctx->i8_cent.p : nullptr, ctx->i8_s,
                      (const double*)ctx->mu.p, n, d, perm0, (uint32_t*)ctx->ord_key.p,
-                     (int*)ctx->ord_perm.p, (int*)ctx->ord_ipos.p, ctx->stream);
+                     (int*)ctx->ord_perm.p, (int*)ctx->ord_ipos.p, il, ctx->stream);
   HIP_TRY(hipGetLastError());
   ctx->ord_nb = true;
   return KNN_OK;
@@ -320,6 +341,7 @@ static int build_train(knn_ctx* ctx, const double* dX, const int32_t* dlab, int6
   launch_round_mu((double*)ctx->mu.p, d, jx + 2, ctx->stream);
   ctx->ord_P = 0;
   ctx->ord_nb = false;
+  ctx->ord_bcnt_zero = 0;
   const int P = region_count(ctx, n, d);
   if (P > 0 && (rc = build_order(ctx, dX, (const double*)ctx->mu.p, n, d, jx, P))) return rc;
   if (norm_blocks_on(ctx, n, d) && (rc = build_norm_blocks(ctx, dX, n, d))) return rc;
@@ -554,21 +576,6 @@ static bool use_i8(const knn_ctx* ctx, int metric, int64_t m, int W) {
   return m >= 4096 && W <= kQuadMaxW;
 }
 
-// Which int8 kernel: metric 6 (v_mfma_i32_32x32x32_i8, K granularity 32)
-// where it issues fewer padded dims than metric 5 (16x16x64, K 64) -- d = 96
-// runs 96 dims instead of 128 (configs[3]) -- and at DP = 128 (cfg2), where
-// its two 4-entry lists per lane (KNN_I8W_Q4) made it the faster kernel:
-// 1.278-1.290 vs 1.290-1.303 ms candidate, all phases 1.466-1.478 vs
-// 1.500-1.518 ms (profiles/ab_log.md r5g; its 32x32 MFMA holds the vector
-// issue for 8 of 32 cycles, the 16x16x64 one for 8 of 16).  Tuning key
-// "i8w": -1 auto, 0 always 16x16x64, 1 always 32x32x32.
-static int i8_kernel(const knn_ctx* ctx) {
-  const int d = ctx->train.d;
-  if (ctx->tune_i8w >= 0) return ctx->tune_i8w > 0 && pad_dim_i8w(d) > 0 ? 6 : 5;
-  const int w = pad_dim_i8w(d);
-  return w > 0 && (w < pad_dim_i8(d) || w == 128) ? 6 : 5;
-}
-
 static bool use_bf16x3(const knn_ctx* ctx, int metric) {
   if (metric != KNN_METRIC_L2) return false;
   if (ctx->precision == KNN_PRECISION_FP32) return false;
@@ -738,12 +745,15 @@ static double err_factor(int kmetric, int DP) {
 }
 
 // ---- timing ring (knn_set_timing): events of a call are read back lazily
+// (mode 2: only ev[1] and ev[2], around the candidate kernel, are recorded)
+static bool phase_timed(const TimedCall& tc, int p) { return tc.mode != 2 || p == 1; }
 static void fold_timing(knn_ctx* ctx, TimedCall& tc) {
   if (!tc.pending) return;
-  (void)hipEventSynchronize(tc.ev[4]);
+  (void)hipEventSynchronize(tc.ev[tc.mode == 2 ? 2 : 4]);
   for (int p = 0; p < 4; p++) {
     float ms = 0.f;
-    if (hipEventElapsedTime(&ms, tc.ev[p], tc.ev[p + 1]) == hipSuccess) ctx->tsum[p] += ms;
+    if (phase_timed(tc, p) && hipEventElapsedTime(&ms, tc.ev[p], tc.ev[p + 1]) == hipSuccess)
+      ctx->tsum[p] += ms;
   }
   ctx->tcalls++;
   tc.pending = false;
@@ -756,7 +766,13 @@ static TimedCall* timing_slot(knn_ctx* ctx) {
   ctx->ring_last = ctx->ring_next;
   ctx->ring_next = (ctx->ring_next + 1) % kTimingRing;
   tc.pending = true;
+  tc.mode = ctx->timing;
   return &tc;
+}
+// the call's event e, if its timing mode records it
+static hipEvent_t timing_ev(const TimedCall* tc, int e) {
+  if (!tc || (tc->mode == 2 && e != 1 && e != 2)) return nullptr;
+  return tc->ev[e];
 }
 
 // The deferred AUTO decision: once the last fp16 call has completed, its
@@ -948,7 +964,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
     snprintf(ctx->last_kernel, sizeof ctx->last_kernel, "cand_stream_kernel<%d,%d,%d>", kStreamDC,
              R, kmetric);
   TimedCall* tc = timing_slot(ctx);
-  if (tc) HIP_TRY(hipEventRecord(tc->ev[0], s));
+  if (hipEvent_t ev = timing_ev(tc, 0)) HIP_TRY(hipEventRecord(ev, s));
   // query operands: scale * 2^jx (q - mu), scale -2 for L2; a query whose
   // operands would leave the format's range (fp16: 65000, else 2^100) is
   // marked void and goes to the exact rescan
@@ -961,9 +977,13 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   const int* qperm = nullptr;
   const int* qpos = nullptr;
   const int* qstart = nullptr;
+  int64_t bcnt_clear = 0;  // block counts the int8 query builder clears after the sort
   if (ctx->ord_P > 0 && ctx->tune_order != 0 && !s3 && kmetric >= 4 && DP <= 256) {
+    const int64_t nbc = region_sort_blocks(m) * kRegionMax;
     if ((rc = ctx->ord_qkey.ensure((size_t)m * sizeof(int)))) return rc;
-    if ((rc = ctx->ord_bcnt.ensure((size_t)region_sort_blocks(m) * kRegionMax * sizeof(int)))) return rc;
+    const size_t bcnt_cap = ctx->ord_bcnt.cap;
+    if ((rc = ctx->ord_bcnt.ensure((size_t)nbc * sizeof(int)))) return rc;
+    if (ctx->ord_bcnt.cap != bcnt_cap) ctx->ord_bcnt_zero = 0;  // (a new allocation)
     if ((rc = ctx->ord_qperm.ensure((size_t)m * sizeof(int)))) return rc;
     if ((rc = ctx->ord_qpos.ensure((size_t)m * sizeof(int)))) return rc;
     if ((rc = ctx->ord_qstart.ensure((size_t)m * sizeof(int)))) return rc;
@@ -973,18 +993,30 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
                                std::min(ctx->tune_ophase < 0 ? kOrderPhases : ctx->tune_ophase, ctx->ord_P),
                                (int*)ctx->ord_bcnt.p,
                                (int*)ctx->ord_tot.p, (int*)ctx->ord_qkey.p, (int*)ctx->ord_qperm.p,
-                               (int*)ctx->ord_qpos.p, (int*)ctx->ord_qstart.p, s);
+                               (int*)ctx->ord_qpos.p, (int*)ctx->ord_qstart.p, s,
+                               ctx->ord_bcnt_zero >= nbc);
+    ctx->ord_bcnt_zero = 0;
+    if (kmetric >= 5) bcnt_clear = nbc;
     qperm = (const int*)ctx->ord_qperm.p;
     qpos = (const int*)ctx->ord_qpos.p;
     qstart = (const int*)ctx->ord_qstart.p;
   }
-  launch_query_check(dQ, t.mu, m, t.d, m_pad, qscale, t.jx,
-                     kmetric >= 5 ? DBL_MAX : kmetric == 4 ? 65000.0 : std::ldexp(1.0, 100), qvalid,
-                     s);
-  if (kmetric >= 5)  // codes of the train set's grid; a query off it: valid 0 (rescan)
-    launch_prep_i8_queries(dQ, (const double*)ctx->i8_cent.p, m, t.d, DP, m_pad, ctx->i8_s,
-                           (signed char*)ctx->Q32.p, qvalid, s, qperm);
-  else if (s3h)
+  // gthr init (slots of groups without a split stay 0, never the max); the
+  // int8 query builder writes it with the operands (ablate bit 5, an
+  // experiment: keep the previous call's final thresholds -- valid only for
+  // a repeat of the same queries; measures what perfect seeds would save)
+  const bool gthr_init = use_gthr && !(ctx->tune_ablate & 32);
+  const int active = std::min(S, gk ? G : 4);
+  if (kmetric < 5)
+    launch_query_check(dQ, t.mu, m, t.d, m_pad, qscale, t.jx,
+                       kmetric == 4 ? 65000.0 : std::ldexp(1.0, 100), qvalid, s);
+  if (kmetric >= 5) {  // codes of the train set's grid; a query off it: valid 0 (rescan)
+    launch_prep_i8_queries(dQ, t.mu, qscale, t.jx, DBL_MAX, (const double*)ctx->i8_cent.p, m, t.d,
+                           DP, m_pad, ctx->i8_s, (signed char*)ctx->Q32.p, qvalid, s, qperm,
+                           gthr_init ? (uint32_t*)ctx->gthr.p : nullptr, active,
+                           (int*)ctx->ord_bcnt.p, bcnt_clear);
+    if (bcnt_clear) ctx->ord_bcnt_zero = bcnt_clear;
+  } else if (s3h)
     launch_prep_half_tiled(dQ, t.mu, m, t.d, DP, m_pad, t.jx, -2.0, (unsigned short*)ctx->Q32.p,
                            nullptr, nullptr, qvalid, nullptr, s);
   else if (s3)
@@ -998,7 +1030,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
                       (unsigned short*)ctx->Q32.p, 2 * DP, nullptr, nullptr, s);
   else
     launch_prep_queries(dQ, t.mu, m, t.d, DP, m_pad, qscale, t.jx, (float*)ctx->Q32.p, s);
-  if (tc) HIP_TRY(hipEventRecord(tc->ev[1], s));
+  if (hipEvent_t ev = timing_ev(tc, 1)) HIP_TRY(hipEventRecord(ev, s));
   CandLaunch cl{};
   cl.metric = kmetric;
   cl.DP = DP;
@@ -1020,12 +1052,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   cl.qstart = qstart;
   cl.gmask = gk ? G - 1 : 3;
   cl.qblk = ctx->tune_qblk > 0 ? std::min(ctx->tune_qblk, n_qt) : 0;
-  // slots of groups without a split stay 0 (never the max)
-  // (experiment, tuning "ablate" bit 5: keep the previous call's final
-  // thresholds -- valid only for a repeat of the same queries; measures what
-  // perfectly seeded thresholds would save)
-  if (use_gthr && !(ctx->tune_ablate & 32)) {
-    const int active = std::min(S, gk ? G : 4);
+  if (gthr_init) {
     const int64_t ns = (kmetric == 4 || kmetric == 5) && !s3 ? seed_rows(ctx) : 0;
     bool seeded = false;
     if (ns > 0) {
@@ -1049,7 +1076,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
         seeded = true;
       }
     }
-    if (!seeded) launch_fill_gthr(cl.gthr, m_pad, active, s);
+    if (!seeded && kmetric < 5) launch_fill_gthr(cl.gthr, m_pad, active, s);
   }
   if (s3h)
     launch_cand_s3h((const unsigned short*)ctx->XT16.p, (const float*)ctx->XS16.p,
@@ -1062,7 +1089,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   else if (!launch_cand(cl, s))
     return knn_fail(KNN_ERR_ARG, "no candidate kernel for this geometry (tuning overrides?)");
   HIP_TRY(hipGetLastError());
-  if (tc) HIP_TRY(hipEventRecord(tc->ev[2], s));
+  if (hipEvent_t ev = timing_ev(tc, 2)) HIP_TRY(hipEventRecord(ev, s));
   HIP_TRY(hipMemsetAsync(ctx->rescan_cnt.p, 0, 4 * sizeof(int), s));
   // per-split certification: a query failing only through some splits'
   // lists rescans just those splits' rows (knn_select.hip)
@@ -1074,6 +1101,20 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   sm.mask = (unsigned long long*)ctx->rescan_mask.p;
   sm.nkeep = (int*)ctx->rescan_nkeep.p;
   sm.keep = (int*)ctx->fr_buf.p;
+  // the fast rescan's per-query setup, run by the merge on the queries it
+  // fails (timing-only ablations leave every query uncertified: none then)
+  const bool abl = ctx->tune_ablate & 27;
+  RescanPrep rp;
+  rp.mu = t.mu;
+  rp.x2max = t.x2max;
+  rp.x1max = t.x1max;
+  rp.jx = t.jx;
+  rp.DP = t.DP;
+  rp.f_err = err_factor(metric, t.DP);
+  rp.qf = (float*)ctx->fr_q.p;
+  rp.thr = (float*)ctx->fr_thr.p;
+  rp.fcnt = (int*)ctx->fr_cnt.p;
+  rp.cap = abl ? 0 : cap;
   if (kmetric >= 5) {
     // int8 proxies are exact up to +1 (the odd-norm half of the seed): the
     // merge sees the pass's own centre and scale (codes (x - cent/2^s) 2^s),
@@ -1089,17 +1130,17 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
                         ProxyScale{qvalid, 0.0, 1.0 / DP, false, (const double*)ctx->i8_cent.p, qpos},
                         cl.gthr, sink,
                         (int*)ctx->rescan_q.p, (double*)ctx->rescan_tau.p, (int*)ctx->rescan_cnt.p,
-                        sm, s);
+                        sm, rp, s);
   } else {
     launch_merge_rerank(metric, (const float*)ctx->cand_v.p, (const int*)ctx->cand_i.p, NL, R, t,
                         dQ, m, W, C, err_factor(kmetric, DP),
                         kmetric == 4 ? ProxyScale{qvalid, 0x1p-14, 0x1p-28, true, nullptr, qpos}
                                      : ProxyScale{qvalid, 0x1p-125, 0x1p-124, false, nullptr, qpos},
                         cl.gthr, sink, (int*)ctx->rescan_q.p, (double*)ctx->rescan_tau.p,
-                        (int*)ctx->rescan_cnt.p, sm, s);
+                        (int*)ctx->rescan_cnt.p, sm, rp, s);
   }
   HIP_TRY(hipGetLastError());
-  if (tc) HIP_TRY(hipEventRecord(tc->ev[3], s));
+  if (hipEvent_t ev = timing_ev(tc, 3)) HIP_TRY(hipEventRecord(ev, s));
   // rescan of uncertified queries, sized on the device (knn_select.hip)
   RescanBufs rb{};
   rb.q = (int*)ctx->rescan_q.p;
@@ -1117,8 +1158,6 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   rb.S = sm.S;
   rb.trows = sm.trows;
   rb.cus = ctx->cu_count;
-  // (timing-only ablations leave every query uncertified: no rescan then)
-  const bool abl = ctx->tune_ablate & 27;
   launch_rescan(metric, t, dQ, rb, abl ? 0 : cap, W, err_factor(metric, t.DP), sink,
                 abl ? 0 : (int)std::min<int64_t>(m, ctx->cu_count), s);
   // (without the full-scan launch nothing writes this call's counts)
@@ -1129,7 +1168,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
                      (unsigned char*)ctx->tie_ws.p, tie_per, tie_nwg, sink,
                      (unsigned long long*)ctx->totals.p + 2, s);
   HIP_TRY(hipGetLastError());
-  if (tc) HIP_TRY(hipEventRecord(tc->ev[4], s));
+  if (hipEvent_t ev = timing_ev(tc, 4)) HIP_TRY(hipEventRecord(ev, s));
   HIP_TRY(hipEventRecord(ctx->done_ev, s));
   // the deferred AUTO decision reads done_ev and h_counts, which belong to
   // the LAST call: it is armed by an fp16 call and dropped by any other
@@ -1540,7 +1579,7 @@ int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value) {
     if (value != -1 && value != 4 && value != 8) return knn_fail(KNN_ERR_ARG, "gg must be -1 (auto), 4 or 8");
     ctx->tune_gg = (int)value;
   } else if (!strcmp(key, "nblk")) {
-    if (value < -1 || value > 1) return knn_fail(KNN_ERR_ARG, "nblk must be -1 (auto), 0 or 1");
+    if (value < -1 || value > 3) return knn_fail(KNN_ERR_ARG, "nblk must be -1 (auto), 0, 1, 2 or 3");
     ctx->tune_nblk = (int)value;
   } else if (!strcmp(key, "ties")) {
     if (value < 0 || value > 2) return knn_fail(KNN_ERR_ARG, "ties must be 0, 1 or 2");
@@ -1560,7 +1599,8 @@ int knn_set_timing(knn_ctx* ctx, int enable) {
   if (enable && !ctx->ring[0].ev[0])
     for (auto& tc : ctx->ring)
       for (auto& e : tc.ev) HIP_TRY(hipEventCreate(&e));
-  ctx->timing = enable != 0;
+  if (enable < 0 || enable > 2) return knn_fail(KNN_ERR_ARG, "timing must be 0, 1 or 2");
+  ctx->timing = enable;
   return KNN_OK;
 }
 
@@ -1568,7 +1608,8 @@ double knn_last_phase_ms(knn_ctx* ctx, int phase) {
   if (!ctx || phase < 0 || phase > 3 || ctx->ring_last < 0) return -1.0;
   if (hipSetDevice(ctx->device) != hipSuccess) return -1.0;
   TimedCall& tc = ctx->ring[ctx->ring_last];
-  if (hipEventSynchronize(tc.ev[4]) != hipSuccess) return -1.0;
+  if (!phase_timed(tc, phase)) return -1.0;
+  if (hipEventSynchronize(tc.ev[tc.mode == 2 ? 2 : 4]) != hipSuccess) return -1.0;
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, tc.ev[phase], tc.ev[phase + 1]) != hipSuccess) return -1.0;
   return ms;

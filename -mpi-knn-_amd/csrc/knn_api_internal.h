@@ -20,6 +20,7 @@ constexpr int kTimingRing = 32;
 struct TimedCall {
   hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
   bool pending = false;
+  int mode = 1;  // knn_set_timing: 1 every phase, 2 the candidate kernel only (ev[1], ev[2])
 };
 
 struct knn_ctx {
@@ -75,9 +76,12 @@ struct knn_ctx {
   // norm blocks (knn_order.hip): -1 auto (integer-coded train sets, d <= 256),
   // 0 off, 1 on; ord_nb: the current layout has them (ord_perm / ord_ipos valid)
   int tune_nblk = -1;
-  int tune_gg = -1;
-  int tune_qblk = 0;           // resident kernel workgroup order: 0 split-major, B query blocks            // gthr slot groups of the resident kernel: -1 auto (8), 4 or 8
+  int tune_gg = -1;            // gthr slot groups of the resident kernel: -1 auto, 4 or 8
+  int tune_qblk = 0;           // resident kernel workgroup order: 0 split-major, B query blocks
   bool ord_nb = false;
+  // ints of ord_bcnt known to be zero (the int8 query builder clears the
+  // region sort's block counts after the sort read them; 0: unknown)
+  int64_t ord_bcnt_zero = 0;
   int tune_s3gq = 0;           // S3 kernel: largest XCD query-tile grouping (0 = kS3GqMax)
   // query streams start at one of N phases of the region chain (P regions in
   // N groups; -1 auto = 8, 0 = at the query tile's own region)
@@ -90,7 +94,7 @@ struct knn_ctx {
   int last_kmetric = -1; // candidate kernel metric of the last search (knn_kernels.h)
   char last_kernel[96] = {0};  // name of the last candidate kernel launched
   knnk::TrainDev train{};
-  bool timing = false;
+  int timing = 0;  // knn_set_timing mode
   TimedCall ring[kTimingRing];
   int ring_next = 0, ring_last = -1;
   double tsum[4] = {0, 0, 0, 0};

@@ -192,11 +192,24 @@ struct SplitMap {
   int* nkeep = nullptr;       // [cap] re-ranked rows of the other splits handed to the rescan
   int* keep = nullptr;        // [cap][kRescanCap] (the fast rescan's row buffer)
 };
+// The fast rescan's per-query setup, done by the merge for each query it
+// fails (the first `cap`): the fp32 query operand of the rescan's X32 image
+// (its centre mu, scale 2^jx, padded dim DP and norms x2max / x1max), the
+// proxy threshold every row within tau passes (f_err: the fp32 error factor
+// of DP) and the count of rows the merge already handed over (fcnt = nkeep).
+struct RescanPrep {
+  const double* mu = nullptr;
+  double x2max = 0.0, x1max = 0.0, f_err = 0.0;
+  float* qf = nullptr;   // [cap][DP]
+  float* thr = nullptr;  // [cap]
+  int* fcnt = nullptr;   // [cap]
+  int jx = 0, DP = 0, cap = 0;
+};
 void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int R,
                          const TrainDev& t, const double* Q64, int64_t m, int W, int C,
                          double f_err, ProxyScale ps, const uint32_t* gthr, const Sink& sink,
                          int* rescan_q, double* rescan_tau, int* rescan_cnt, const SplitMap& sm,
-                         hipStream_t s);
+                         const RescanPrep& rp, hipStream_t s);
 constexpr int kRescanCap = 1024;        // rows a fast rescan may append per query
 constexpr int kRescanStageMaxDP = 256;  // fast rescan stages rows in LDS up to this DP
 constexpr int kRescanFastQueries = 65536;  // failed queries per call the fast path serves
@@ -219,8 +232,9 @@ struct RescanBufs {
   int64_t trows;
   int cus;                   // compute units (the staged filter's grid)
 };
-// Enqueues the whole rescan path (prep, filter, exact finish, full scan);
-// every kernel reads the counts on the device.  f_err: the fp32 candidate
+// Enqueues the rescan path (filter, exact finish, full scan; the merge did
+// each fast-path query's setup, RescanPrep); every kernel reads the counts on
+// the device.  f_err: the fp32 candidate
 // error factor of t.DP; full_blocks: workgroups of the full-scan kernel.
 void launch_rescan(int metric, const TrainDev& t, const double* Q64, const RescanBufs& rb, int cap,
                    int W, double f_err, const Sink& sink, int full_blocks, hipStream_t s);
@@ -284,10 +298,15 @@ void launch_grid_stats(const double* X64, int64_t n, int d, double* partial, dou
 void launch_prep_i8_train(const double* X64, const double* cent, int64_t n, int d, int DP,
                           int64_t n_pad, int s, signed char* out, unsigned* codes_max, int swz,
                           hipStream_t st, const int* perm = nullptr);
-// qperm (query operand builders): operand row p <- query qperm[p] (null: p)
-void launch_prep_i8_queries(const double* Q64, const double* cent, int64_t m, int d, int DP,
+// qperm (query operand builders): operand row p <- query qperm[p] (null: p).
+// The int8 builder also runs launch_query_check's test (mu, scale, jx, limit)
+// into valid, with gthr set launch_fill_gthr's init of each row's slots, and
+// clears zero[0, nzero).
+void launch_prep_i8_queries(const double* Q64, const double* mu, double scale, int jx,
+                            double limit, const double* cent, int64_t m, int d, int DP,
                             int64_t m_pad, int s, signed char* out, float* valid, hipStream_t st,
-                            const int* qperm = nullptr);
+                            const int* qperm, uint32_t* gthr, int active, int* zero = nullptr,
+                            int64_t nzero = 0);
 int pad_dim_i8(int d);  // padded dim of the int8 kernel (a multiple of 64, <= 256), -1 if none
 int pad_dim_i8w(int d); // padded dim of the int8 32x32x32 kernel (metric 6), -1 if none
 // The reference's exact neighbour order on exact distance ties (knn_select.hip,
@@ -350,19 +369,24 @@ void launch_region_sort(const int* key, int64_t n, int* bcnt, int* tot, int* per
                         const int* rstart, int* qstart, int* bases, hipStream_t s, int P = 1,
                         int phases = 0);
 // Per call: queries assigned to regions and counting-sorted (qperm / qpos /
-// qstart as above); bcnt region_sort_blocks(m) x kRegionMax ints
+// qstart as above); bcnt region_sort_blocks(m) x kRegionMax ints, cleared
+// first unless bcnt_zero (already zero)
 void launch_region_sort_queries(const double* Q, const double* mu, int64_t m, int d, int jx,
                                 const unsigned short* img, const float* cnorm, int P, const int* rank,
                                 const int* rstart, int phases, int* bcnt, int* tot, int* qkey,
-                                int* qperm, int* qpos, int* qstart, hipStream_t s);
+                                int* qperm, int* qpos, int* qstart, hipStream_t s,
+                                bool bcnt_zero = false);
 
 // Norm blocks (knn_order.hip): every window of kNormWin image positions
 // sorted by the rows' squared norm (int8 code norm with cent, else ||x -
 // mu||^2): perm[p] = perm0[source] (perm0 null: train order), ipos inverse;
-// key holds n uint32 of scratch.  perm0 must not alias perm / ipos.
+// key holds n uint32 of scratch.  perm0 must not alias perm / ipos.  il: the
+// int8 kernel metric (5 / 6) whose lane lists the norm ranks of each 32-row
+// sub-tile are interleaved over (0: sorted order).
 constexpr int kNormWin = 16384;
 void launch_norm_blocks(const double* X, const double* cent, int s, const double* mu, int64_t n,
-                        int d, const int* perm0, uint32_t* key, int* perm, int* ipos, hipStream_t st);
+                        int d, const int* perm0, uint32_t* key, int* perm, int* ipos, int il,
+                        hipStream_t st);
 // Int8 images carry, in the pad of row 128u + 1, the largest seed of each of
 // the 32-row sub-tiles 4u .. 4u+3 (the seed-free accumulation's bound,
 // knn_cand_res.hip)

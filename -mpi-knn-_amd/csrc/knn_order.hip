@@ -406,13 +406,48 @@ norm_key_kernel(const double* __restrict__ X, const double* __restrict__ cent, i
   }
 }
 
+// Interleave of the norm ranks inside each 32-row sub-tile (il = the int8
+// kernel's metric, 0: none): norm ranks 4a + b go to rows of the lane lists
+// b = 0..3 of the query in the kernel's accumulator layout, so 4 rows of
+// consecutive norm -- where a query's nearest neighbours cluster -- land in 4
+// different lists.  Uninterleaved, a run of 4 adjacent rows shares a list, and
+// one list holding 4 of a query's top W is what fails certification (an exact
+// rescan): cfg2 sent 2 queries per 10k batch to it (~40 us per call).  The
+// sub-tile's set of rows, hence its largest seed, does not change.
+//   metric 6 (32x32: lane (j, h) list 0 = rows (i&3) + 8(i>>2) + 4h, i < 8,
+//            list 1 the same + 16): list b = 2h + half at rows
+//            16 half + 8x + 4h + y
+//   metric 5 (16x16: lane group g16 = rows 4 g16 + i of each 16-row block)
+__device__ __forceinline__ int norm_il(int r, int il) {
+  const int a = r >> 2, b = r & 3;
+  if (il == 6) return (b & 1) * 16 + (a >> 2) * 8 + (b >> 1) * 4 + (a & 3);
+  if (il == 5) return (a >> 2) * 16 + b * 4 + (a & 3);
+  return r;
+}
+
+// Spread of the sub-tiles over the window's staged tiles (il & 16, whole
+// windows): the 512 sub-tiles of 32 rows, in norm order u = 64 a + b, go to
+// tile b, slot a -- sub-tiles of adjacent norm lie in adjacent tiles, i.e.
+// in different splits (tile t streams in split t mod S).  A query's nearest
+// neighbours are near one another, hence of nearly equal norm: sorted
+// windows put them into one tile of one split, where the interleave alone
+// still let 4 of a cfg2 query's top 7 share a list (profiles/ab_log.md r5w).
+// Each sub-tile keeps its rows, so its seed bound is unchanged.
+constexpr int kNormSub = kNormWin / 32;            // sub-tiles per window
+constexpr int kNormTiles = kNormWin / 256;          // staged tiles per window (256 rows)
+__device__ __forceinline__ int norm_spread(int u) {
+  return (u % kNormTiles) * (kNormSub / kNormTiles) + u / kNormTiles;
+}
+
 // One workgroup per window: (key, position) pairs bitonic-sorted in LDS
 // (unique, so the order is deterministic), then perm[p] = perm0[source] and
-// ipos[perm[p]] = p.  perm0 and perm are distinct buffers.
+// ipos[perm[p]] = p, p the sorted rank, interleaved within whole 32-row
+// sub-tiles (norm_il, il & 15) and, il & 16, the sub-tiles spread over the
+// window's tiles (norm_spread).  perm0 and perm are distinct buffers.
 constexpr int kNormSortT = 1024;
 __global__ void __launch_bounds__(kNormSortT)
 norm_block_sort_kernel(const uint32_t* __restrict__ key, int64_t n, const int* __restrict__ perm0,
-                       int* __restrict__ perm, int* __restrict__ ipos) {
+                       int* __restrict__ perm, int* __restrict__ ipos, int il) {
   __shared__ unsigned long long sk[kNormWin];  // 128 KiB
   const int tid = threadIdx.x;
   const int64_t w0 = (int64_t)blockIdx.x * kNormWin;
@@ -436,20 +471,23 @@ norm_block_sort_kernel(const uint32_t* __restrict__ key, int64_t n, const int* _
   for (int i = tid; i < cnt; i += kNormSortT) {
     const int64_t src = w0 + (int64_t)(unsigned)(sk[i] & 0xFFFFFFFFu);
     const int r = perm0 ? perm0[src] : (int)src;
-    perm[w0 + i] = r;
-    ipos[r] = (int)(w0 + i);
+    int p = (i | 31) < cnt ? (i & ~31) | norm_il(i & 31, il & 15) : i;
+    if ((il & 16) && cnt == kNormWin) p = norm_spread(p >> 5) * 32 + (p & 31);
+    perm[w0 + p] = r;
+    ipos[r] = (int)(w0 + p);
   }
 }
 
 void launch_norm_blocks(const double* X, const double* cent, int s, const double* mu, int64_t n,
-                        int d, const int* perm0, uint32_t* key, int* perm, int* ipos, hipStream_t st) {
+                        int d, const int* perm0, uint32_t* key, int* perm, int* ipos, int il,
+                        hipStream_t st) {
   if (n <= 0) return;
   int64_t blocks = (n + 3) / 4;
   if (blocks > 16384) blocks = 16384;
   hipLaunchKernelGGL(norm_key_kernel, dim3((unsigned)blocks), dim3(256), 0, st, X, cent, s, mu, n, d,
                      perm0, key);
   hipLaunchKernelGGL(norm_block_sort_kernel, dim3((unsigned)((n + kNormWin - 1) / kNormWin)),
-                     dim3(kNormSortT), 0, st, key, n, perm0, perm, ipos);
+                     dim3(kNormSortT), 0, st, key, n, perm0, perm, ipos, il);
 }
 
 void launch_region_assign(const double* X, const double* mu, int64_t n, int d, int64_t stride,
@@ -501,10 +539,11 @@ void launch_region_sort(const int* key, int64_t n, int* bcnt, int* tot, int* per
 void launch_region_sort_queries(const double* Q, const double* mu, int64_t m, int d, int jx,
                                 const unsigned short* img, const float* cnorm, int P, const int* rank,
                                 const int* rstart, int phases, int* bcnt, int* tot, int* qkey,
-                                int* qperm, int* qpos, int* qstart, hipStream_t s) {
+                                int* qperm, int* qpos, int* qstart, hipStream_t s,
+                                bool bcnt_zero) {
   if (m <= 0) return;
   const int64_t nb = region_sort_blocks(m);
-  launch_fill_i32(bcnt, nb * kRegionMax, 0, s);
+  if (!bcnt_zero) launch_fill_i32(bcnt, nb * kRegionMax, 0, s);
   launch_region_assign(Q, mu, m, d, 1, jx, img, cnorm, rank, qkey, bcnt, s);
   int inl = (int)nb;
   if (nb > 64) {

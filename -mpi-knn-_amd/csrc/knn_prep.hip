@@ -481,16 +481,39 @@ void launch_prep_i8_train(const double* X64, const double* cent, int64_t n, int 
 // plain row-major).  A value off the train set's grid or beyond the code
 // range is rounded / saturated; the merge rebuilds the same code, measures
 // the query's coding error and widens its bound by it (merge_rerank_kernel).
-// Rows launch_query_check marked invalid get zero operands.
+// One wave per operand row p (query q = qperm[p]), and in the same launch
+// the two per-query steps that precede the candidate pass: the operand-range
+// check of query_check_kernel (valid[q]: 1, 0 = void proxies / exact rescan,
+// -1 = a non-finite coordinate; a void query gets zero codes) and, with gthr
+// set, row p's threshold slots as launch_fill_gthr writes them -- one kernel
+// instead of three (~4-6 us each at cfg2, profiles/r5_kernels_cfg2.json).
+// zero[0, nzero): the region sort's block counts, read by this call's sort
+// (which ran before) and cleared here for the next call's histogram.
 __global__ void __launch_bounds__(256)
-prep_i8_queries_kernel(const double* __restrict__ Q64, const double* __restrict__ cent, int64_t m,
-                       int d, int DP, int64_t m_pad, int s, signed char* __restrict__ out,
-                       float* __restrict__ valid, const int* __restrict__ qperm) {
+prep_i8_queries_kernel(const double* __restrict__ Q64, const double* __restrict__ mu, double scale,
+                       int jx, double limit, const double* __restrict__ cent, int64_t m, int d,
+                       int DP, int64_t m_pad, int s, signed char* __restrict__ out,
+                       float* __restrict__ valid, const int* __restrict__ qperm,
+                       uint32_t* __restrict__ gthr, int active, int* __restrict__ zero,
+                       int64_t nzero) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < nzero; e += (int64_t)gridDim.x * 256)
+    zero[e] = 0;
   const int lane = threadIdx.x & 63;
   const int64_t wstride = (int64_t)gridDim.x * 4;
   for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < m_pad; row += wstride) {
     const int64_t q = src_row(qperm, row, m);
-    const bool use = row < m && valid[q] > 0.0f;
+    bool ok = true, fin = true;
+    if (row < m)
+      for (int c = lane; c < d; c += 64) {
+        const double x = Q64[q * d + c];
+        fin = fin && !nonfinite_bits(x);
+        ok = ok && __builtin_fabs(__builtin_ldexp(scale * (x - mu[c]), jx)) < limit;
+      }
+    ok = __ballot(!ok) == 0;
+    fin = __ballot(!fin) == 0;
+    const float vq = !fin ? -1.0f : (ok ? 1.0f : 0.0f);
+    if (lane == 0) valid[q] = vq;  // (pad rows: q = row, valid 1)
+    const bool use = row < m && vq > 0.0f;
     for (int c = lane; c < DP; c += 64) {
       int k = 0;
       if (use && c < d) {
@@ -499,16 +522,20 @@ prep_i8_queries_kernel(const double* __restrict__ Q64, const double* __restrict_
       }
       out[row * DP + c] = (signed char)k;
     }
+    if (gthr && lane < kGthrSlots) gthr[row * kGthrSlots + lane] = lane < active ? kGthrInit : 0u;
   }
 }
 
-void launch_prep_i8_queries(const double* Q64, const double* cent, int64_t m, int d, int DP,
+void launch_prep_i8_queries(const double* Q64, const double* mu, double scale, int jx,
+                            double limit, const double* cent, int64_t m, int d, int DP,
                             int64_t m_pad, int s, signed char* out, float* valid, hipStream_t st,
-                            const int* qperm) {
+                            const int* qperm, uint32_t* gthr, int active, int* zero,
+                            int64_t nzero) {
   int64_t blocks = (m_pad + 3) / 4;
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(prep_i8_queries_kernel, dim3((unsigned)blocks), dim3(256), 0, st, Q64, cent, m,
-                     d, DP, m_pad, s, out, valid, qperm);
+  hipLaunchKernelGGL(prep_i8_queries_kernel, dim3((unsigned)blocks), dim3(256), 0, st, Q64, mu,
+                     scale, jx, limit, cent, m, d, DP, m_pad, s, out, valid, qperm, gthr, active,
+                     zero, nzero);
 }
 
 __global__ void fill_i32_kernel(int32_t* p, int64_t n, int32_t v) {

@@ -113,6 +113,49 @@ __device__ void finish_partial(int64_t q, const double* dk, const int* di, const
   }
 }
 
+// The fast rescan's setup of one failed query (one wave; the merge runs it
+// for the queries it fails): the centred fp32 query row qf (x -2 for L2, the
+// candidate pass's operand) and the proxy threshold *thr every row with
+// exact distance <= tau passes (fp32 fmaf-chain error bound f_err of t.DP).
+template <int METRIC>
+__device__ void rescan_prep_query(const RescanPrep& t, int d, const double* __restrict__ qr,
+                                  double tq, float* __restrict__ qf, float* __restrict__ thr) {
+  const int lane = threadIdx.x & 63, DP = t.DP;
+  const double f_err = t.f_err;
+  double qa = 0.0, q1 = 0.0;
+  for (int i = lane; i < DP; i += 64) {
+    float v = 0.0f;
+    if (i < d) {
+      const double x = qr[i] - t.mu[i];
+      qa += METRIC == 0 ? x * x : __builtin_fabs(x);
+      q1 += __builtin_fabs(x);
+      v = (float)__builtin_ldexp(x * (METRIC == 0 ? -2.0 : 1.0), t.jx);  // X32's scale
+    }
+    qf[i] = v;
+  }
+  qa = wave_sum_d(qa) * (1.0 + 1e-12);
+  q1 = wave_sum_d(q1) * (1.0 + 1e-12);
+  if (lane == 0) {
+    const double sinv = __builtin_ldexp(1.0, -t.jx);
+    double T;
+    // unscaled threshold (+ the fp32 absolute terms of the merge), then
+    // scaled to the proxies' units
+    if (METRIC == 0) {
+      const double E = f_err * (t.x2max + 2.1 * __builtin_sqrt(qa) * __builtin_sqrt(t.x2max)) +
+                       0x1p-125 * 1.001 * (2.0 * q1 + t.x1max) * sinv +
+                       DP * 0x1p-124 * sinv * sinv + 1e-300;
+      T = __builtin_ldexp(tq * tq * (1.0 + 1e-12) - qa * (1.0 - 2e-12) + E, 2 * t.jx);
+    } else {
+      const double E = f_err * (qa + t.x1max) + 2.0 * 0x1p-125 * 1.001 * DP * sinv + 1e-300;
+      T = __builtin_ldexp(tq * (1.0 + 1e-12) + E, t.jx);
+    }
+    // round T up to a float (the order-preserving key's successor is the next float up)
+    float tf = (float)T;
+    if ((double)tf < T && tf < KNN_INF_F) tf = key2f(f2key(tf) + 1u);
+    *thr = tq < KNN_INF_D ? tf : -KNN_INF_F;  // unknown tau: nothing passes, full scan
+  }
+}
+
 // --------------------------------------------- merge + exact re-rank
 // One block per query (NT = 64 or 256 threads).
 //  1. wave 0 holds the union of the 2S lists in registers (EPL per lane),
@@ -138,56 +181,65 @@ __device__ __forceinline__ int lanes_below(unsigned long long mask) {
 }
 
 // Exact fp64 distances of rows di[0..cn) to the query row qv, in the
-// reference's operation order: rows are read coalesced (16 lanes per 128-B
-// row piece) into an LDS tile of squared (L1: absolute) differences, then
-// thread c adds its candidate's terms in dimension order -- bit-exact with
-// cpp:33-50 / cpp:51-67 (sequential, no FMA; sqrt correctly rounded).
+// reference's operation order: rows are read coalesced into an LDS tile of
+// squared (L1: absolute) differences, then thread c adds its candidate's
+// terms in dimension order -- bit-exact with cpp:33-50 / cpp:51-67
+// (sequential, no FMA; sqrt correctly rounded).
 // (The squared difference is formed from the same fp64 operands in the
 // same operation as before the prefetch: the result bits are unchanged.)
 // Pads [cn, C2) with (+inf, INT_MAX) and sorts (dist, idx) ascending.
-// All NT threads; rows go in batches of RB = NT * EPT / 16 (tb holds RB x 17
-// doubles): EPT = 8 halves the prefetch registers where the candidate set
-// is at most NT / 2 rows.
+// All NT threads; rows go in batches of RB = NT * EPT / 16, each batch in
+// chunks of DC dims: as many as the EPT values per thread and the tile tb
+// (tbcap doubles, >= RB * 17) hold -- a small candidate set is read in one
+// or two rounds of loads instead of d / 16 dependent ones (the rescan's
+// exact finish: ~15 rows, all 128 dims at once; the merge at cfg2: 11-16
+// rows, 32 dims per round).  EPT = 8 halves the prefetch registers where
+// the candidate set is at most NT / 2 rows.
 template <int METRIC, int NT, int EPT = 16>
 __device__ void exact_sorted(const TrainDev& t, const double* qv, int* di, double* dk, double* tb,
-                             int cn, int C2, int tid) {
+                             int cn, int C2, int tid, int tbcap) {
   const int d = t.d;
-  // the raw fp64 values of a 16-dim chunk, EPT per thread (nb * 16 <= NT * EPT);
-  // two register sets in flight: chunk c+1's and c+2's loads overlap chunk c's
-  // sums and barriers (rows of 7.7 KB at d = 960 make this an HBM stream)
   constexpr int RB = NT * EPT / 16;
   for (int b0 = 0; b0 < cn; b0 += RB) {
     const int nb = min(RB, cn - b0);
-    const int ne = nb * 16;
+    // chunk width DC = 2^lg: the largest power of two the registers and the
+    // tile hold, >= 16 (nb <= RB and tbcap >= 17 RB), <= d rounded up
+    const int cap = min(NT * EPT, tbcap - nb) / nb;
+    int lg = 4;
+    while (lg < 12 && (2 << lg) <= cap && (1 << lg) < d) ++lg;
+    const int DC = 1 << lg;
+    const int ne = nb * DC, ts = DC + 1;  // elements per chunk, tb row stride
+    // element e of a chunk: row c = e >> lg (-1 past the chunk), dim e & (DC - 1)
+    auto row_of = [&](int e) { return e < ne ? e >> lg : -1; };
+    // the raw fp64 values of a chunk, EPT per thread; two register sets in
+    // flight: chunk c+2's loads overlap chunk c's sums and barriers
     auto fetch = [&](int c0, double (&o)[EPT]) {
 #pragma unroll
       for (int k = 0; k < EPT; ++k) {
-        const int e = tid + k * NT;
-        const int c = e >> 4, j = e & 15;
-        o[k] = (e < ne && c0 + j < d) ? t.X64[(int64_t)di[b0 + c] * d + c0 + j] : 0.0;
+        const int e = tid + k * NT, c = row_of(e), j = e & (DC - 1);
+        o[k] = (c >= 0 && c0 + j < d) ? t.X64[(int64_t)di[b0 + c] * d + c0 + j] : 0.0;
       }
     };
     double r = 0.0;
-    // stage chunk c0 (values in x) into tb, refill x with chunk c0 + 32, add
+    // stage chunk c0 (values in x) into tb, refill x with chunk c0 + 2 DC, add
     auto step = [&](int c0, double (&x)[EPT]) {
-      const int nd = min(16, d - c0);
+      const int nd = min(DC, d - c0);
 #pragma unroll
       for (int k = 0; k < EPT; ++k) {
-        const int e = tid + k * NT;
-        const int c = e >> 4, j = e & 15;
-        if (e < ne) {
+        const int e = tid + k * NT, c = row_of(e), j = e & (DC - 1);
+        if (c >= 0) {
           double val = 0.0;
           if (j < nd) {
             const double tq = qv[c0 + j] - x[k];
             val = METRIC == 0 ? tq * tq : __builtin_fabs(tq);
           }
-          tb[c * 17 + j] = val;
+          tb[c * ts + j] = val;
         }
       }
       __syncthreads();
-      if (c0 + 32 < d) fetch(c0 + 32, x);
+      if (c0 + 2 * DC < d) fetch(c0 + 2 * DC, x);
       if (tid < nb) {
-        const double* row = tb + tid * 17;
+        const double* row = tb + tid * ts;
         if (nd == 16) {
 #pragma unroll
           for (int j = 0; j < 16; ++j) r = r + row[j];
@@ -199,10 +251,10 @@ __device__ void exact_sorted(const TrainDev& t, const double* qv, int* di, doubl
     };
     double xa[EPT], xb[EPT];
     fetch(0, xa);
-    if (16 < d) fetch(16, xb);
-    for (int c0 = 0; c0 < d; c0 += 32) {
+    if (DC < d) fetch(DC, xb);
+    for (int c0 = 0; c0 < d; c0 += 2 * DC) {
       step(c0, xa);
-      if (c0 + 16 < d) step(c0 + 16, xb);
+      if (c0 + DC < d) step(c0 + DC, xb);
     }
     if (tid < nb) dk[b0 + tid] = METRIC == 0 ? __builtin_sqrt(r) : r;  // correctly rounded
   }
@@ -233,9 +285,9 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
                     TrainDev t, const double* __restrict__ Q64, int W, int Cmax, int C2,
                     double f_err, ProxyScale ps, const uint32_t* __restrict__ gthr, Sink sink,
                     int* __restrict__ rescan_q, double* __restrict__ rescan_tau,
-                    int* __restrict__ rescan_cnt, SplitMap sm) {
+                    int* __restrict__ rescan_cnt, SplitMap sm, RescanPrep rp) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ int s_cn, s_cert;
+  __shared__ int s_cn, s_cert, s_f;
   __shared__ double s_lb, s_lbr, s_qa, s_e, s_pinv;
   __shared__ uint32_t s_bs[64];  // per split: min over its full lists' R-th entries (keys)
   const int d = t.d;
@@ -344,13 +396,38 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
     mlr = wave_min(mlr);
     double tsel = KNN_INF_D;  // select proxies <= tsel
     if (nv > W) {
-      uint32_t pre = 0;  // radix select: key of the W-th smallest proxy
-      for (int b = 31; b >= 0; --b) {
+      // radix select of the key of the W-th smallest proxy (finite: nv > W),
+      // from the highest bit in which the finite keys differ (the common
+      // prefix of their min and max is its prefix), and done as soon as
+      // exactly W keys lie at or below the probe: it is then their largest
+      // (cfg2: ~10 probes instead of 32)
+      uint32_t ky[EPL];
+      uint32_t kmn = kKeyInf, kmx = 0;
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) {
+        ky[e] = f2key(v[e]);
+        kmn = min(kmn, ky[e]);
+        if (v[e] < KNN_INF_F) kmx = max(kmx, ky[e]);
+      }
+      kmn = wave_min_u(kmn);
+      kmx = wave_max_u(kmx);
+      const uint32_t dif = kmn ^ kmx;
+      const int hb = dif ? 31 - __builtin_clz(dif) : -1;
+      uint32_t pre = hb < 0 ? kmn : hb == 31 ? 0u : kmn & ~((2u << hb) - 1u);
+      for (int b = hb; b >= 0; --b) {
         const uint32_t T = pre | ((1u << b) - 1u);
         int cnt = 0;
 #pragma unroll
-        for (int e = 0; e < EPL; ++e) cnt += __popcll(__ballot(f2key(v[e]) <= T));
-        if (cnt < W) pre |= 1u << b;
+        for (int e = 0; e < EPL; ++e) cnt += __popcll(__ballot(ky[e] <= T));
+        if (cnt < W) {
+          pre |= 1u << b;
+        } else if (cnt == W) {
+          uint32_t mx = 0;
+#pragma unroll
+          for (int e = 0; e < EPL; ++e) mx = ky[e] <= T ? max(mx, ky[e]) : mx;
+          pre = wave_max_u(mx);
+          break;
+        }
       }
       const double vw = (double)key2f(pre) * pinv;
       tsel = vw + 2.0 * E + 1e-9 * (__builtin_fabs(vw) + qa + E) + 1e-300;
@@ -446,11 +523,19 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
         sm.mask[f] = ~0ull;
         if (f < sm.cap) sm.nkeep[f] = 0;
       }
+      s_f = f;
+    }
+    __syncthreads();
+    // the fast rescan's setup: tau unknown, nothing passes its filter (the
+    // full scan takes the query)
+    if (tid < 64 && s_f < rp.cap) {
+      rescan_prep_query<METRIC>(rp, d, qv, KNN_INF_D, rp.qf + (int64_t)s_f * rp.DP, rp.thr + s_f);
+      if (tid == 0) rp.fcnt[s_f] = 0;
     }
     return;
   }
 
-  exact_sorted<METRIC, NT, EPT>(t, qv, di, dk, tb, cn, C2, tid);
+  exact_sorted<METRIC, NT, EPT>(t, qv, di, dk, tb, cn, C2, tid, min(NT, C2) * 17);
 
   // certification: every row not re-ranked has proxy >= LB, hence exact
   // distance >= the bound below (rigorous error bound E)
@@ -471,8 +556,15 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
       // the W-th exact distance among the re-ranked rows bounds the true
       // W-th from above: the fast rescan keeps every row that can reach it
       const int f = atomicAdd(rescan_cnt, 1);
+      s_f = f;
       rescan_q[f] = (int)q;
       rescan_tau[f] = cn >= W ? dk[W - 1] : KNN_INF_D;
+#if KNN_DEBUG_CERT
+      // (diagnostic build only: which bound failed)
+      printf("cert fail q %d cn %d W %d LB %.6f LBr %.6f qa %.6f E %.3g dW2 %.6f dW1 %.6f dlast %.6f\n",
+             (int)q, cn, W, LB, s_lbr, s_qa, s_e, cn >= W ? dk[W - 1] * dk[W - 1] : -1.0,
+             cn >= W + 1 ? dk[W] * dk[W] : -1.0, dk[cn - 1] * dk[cn - 1]);
+#endif
       if (sm.mask) {
         // Per split: rows a split dropped have proxy >= min(its lists' final
         // R-th entries, the final global threshold) -- its quad filter and
@@ -502,12 +594,21 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
             }
           }
           sm.nkeep[f] = nk;
+          if (f < rp.cap) rp.fcnt[f] = nk;  // (cap = sm.cap)
         }
+      } else if (f < rp.cap) {
+        rp.fcnt[f] = 0;
       }
     }
   }
   __syncthreads();
-  if (!s_cert) return;
+  if (!s_cert) {
+    // the fast rescan's setup of this query (tau: its W-th exact distance)
+    if (tid < 64 && s_f < rp.cap)
+      rescan_prep_query<METRIC>(rp, d, qv, cn >= W ? dk[W - 1] : KNN_INF_D,
+                                rp.qf + (int64_t)s_f * rp.DP, rp.thr + s_f);
+    return;
+  }
 
   const int need = sink.mode == MODE_SINGLE ? sink.k : sink.w;
   for (int c = tid; c < need && c < cn; c += NT) ls[c] = t.lab[di[c]];
@@ -524,21 +625,22 @@ template <int METRIC, int NT, int EPL, int EPT = 16>
 static void launch_mr(const float* cv, const int* ci, int U, int R, const TrainDev& t,
                       const double* Q64, int64_t m, int W, int Cmax, int C2, double f_err,
                       ProxyScale ps, const uint32_t* gthr, const Sink& sink, int* rescan_q,
-                      double* rescan_tau, int* rescan_cnt, const SplitMap& sm, hipStream_t s) {
+                      double* rescan_tau, int* rescan_cnt, const SplitMap& sm,
+                      const RescanPrep& rp, hipStream_t s) {
   // (the staging tile only as large as the candidate set: a smaller
   // footprint keeps more of these latency-bound workgroups per CU)
   const size_t lds = (size_t)(t.d <= kMergeLdsDim ? t.d : 0) * 8 + (size_t)C2 * 8 +
                      (size_t)std::min(NT, C2) * 17 * 8 + (size_t)C2 * 8;
   hipLaunchKernelGGL((merge_rerank_kernel<METRIC, NT, EPL, EPT>), dim3((unsigned)m), dim3(NT), lds, s,
                      cv, ci, U, R, t, Q64, W, Cmax, C2, f_err, ps, gthr, sink, rescan_q, rescan_tau,
-                     rescan_cnt, sm);
+                     rescan_cnt, sm, rp);
 }
 
 void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int R,
                          const TrainDev& t, const double* Q64, int64_t m, int W, int C,
                          double f_err, ProxyScale ps, const uint32_t* gthr, const Sink& sink,
                          int* rescan_q, double* rescan_tau, int* rescan_cnt, const SplitMap& sm_in,
-                         hipStream_t s) {
+                         const RescanPrep& rp, hipStream_t s) {
   if (m <= 0) return;
   SplitMap sm = sm_in;
   if (sm.S > 64 || sm.trows <= 0) sm.S = 0;  // per-split bounds need S <= 64 mask bits
@@ -549,7 +651,7 @@ void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int
 #define KNN_MR(M_, NT_, EPL_) KNN_MRE(M_, NT_, EPL_, 16)
 #define KNN_MRE(M_, NT_, EPL_, EPT_) \
   launch_mr<M_, NT_, EPL_, EPT_>(cv, ci, U, R, t, Q64, m, W, C, C2, f_err, ps, gthr, sink,  \
-                                 rescan_q, rescan_tau, rescan_cnt, sm, s)
+                                 rescan_q, rescan_tau, rescan_cnt, sm, rp, s)
   // fewer entries per lane when the union is small (cfg2: 152 lists x 4 =
   // 608 entries -> 10 per lane): every radix-select step and the selection
   // loops run over EPL unrolled entries
@@ -590,56 +692,6 @@ void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int
 //     distance and keeps the top W by (dist, idx) with a threshold-filtered
 //     LDS buffer.
 
-// One wave per failed query: the centred fp32 query row (x -2 for L2, the
-// candidate pass's operand) and the proxy threshold every row with exact
-// distance <= tau passes (fp32 fmaf-chain error bound f_err of t.DP).
-template <int METRIC>
-__global__ void __launch_bounds__(64)
-rescan_prep_kernel(TrainDev t, const double* __restrict__ Q64, const int* __restrict__ rescan_q,
-                   const double* __restrict__ tau, const int* __restrict__ cnt, int cap,
-                   double f_err, float* __restrict__ qf, float* __restrict__ thr,
-                   int* __restrict__ fcnt, const int* __restrict__ nkeep) {
-  const int nf = min(cnt[0], cap);
-  const int lane = threadIdx.x, d = t.d, DP = t.DP;
-  for (int s = blockIdx.x; s < nf; s += gridDim.x) {
-    const double* qr = Q64 + (int64_t)rescan_q[s] * d;
-    double qa = 0.0, q1 = 0.0;
-    for (int i = lane; i < DP; i += 64) {
-      float v = 0.0f;
-      if (i < d) {
-        const double x = qr[i] - t.mu[i];
-        qa += METRIC == 0 ? x * x : __builtin_fabs(x);
-        q1 += __builtin_fabs(x);
-        v = (float)__builtin_ldexp(x * (METRIC == 0 ? -2.0 : 1.0), t.jx);  // X32's scale
-      }
-      qf[(int64_t)s * DP + i] = v;
-    }
-    qa = wave_sum_d(qa) * (1.0 + 1e-12);
-    q1 = wave_sum_d(q1) * (1.0 + 1e-12);
-    if (lane == 0) {
-      const double tq = tau[s];
-      const double sinv = __builtin_ldexp(1.0, -t.jx);
-      double T;
-      // unscaled threshold (+ the fp32 absolute terms of the merge), then
-      // scaled to the proxies' units
-      if (METRIC == 0) {
-        const double E = f_err * (t.x2max + 2.1 * __builtin_sqrt(qa) * __builtin_sqrt(t.x2max)) +
-                         0x1p-125 * 1.001 * (2.0 * q1 + t.x1max) * sinv +
-                         DP * 0x1p-124 * sinv * sinv + 1e-300;
-        T = __builtin_ldexp(tq * tq * (1.0 + 1e-12) - qa * (1.0 - 2e-12) + E, 2 * t.jx);
-      } else {
-        const double E = f_err * (qa + t.x1max) + 2.0 * 0x1p-125 * 1.001 * DP * sinv + 1e-300;
-        T = __builtin_ldexp(tq * (1.0 + 1e-12) + E, t.jx);
-      }
-      // round T up to a float (the order-preserving key's successor is the next float up)
-      float tf = (float)T;
-      if ((double)tf < T && tf < KNN_INF_F) tf = key2f(f2key(tf) + 1u);
-      thr[s] = tq < KNN_INF_D ? tf : -KNN_INF_F;  // unknown tau: nothing passes, full scan
-      fcnt[s] = nkeep ? nkeep[s] : 0;  // the merge's re-ranked rows of the certified splits
-    }
-  }
-}
-
 // Appends image row `row` (as its train row) to query s's list if its proxy
 // passes (pad rows never do: +inf seeds).
 __device__ __forceinline__ void rescan_append(float acc, float th, int s, int64_t row,
@@ -671,6 +723,7 @@ rescan_filter_kernel(TrainDev t, const float* __restrict__ qf, const float* __re
   float* rows = thr_s + FQ;                 // [NWB][64][RSF]
   __shared__ unsigned long long mask_s[FQ];  // splits each query of the group scans
   __shared__ unsigned long long s_u;         // union of the failed queries' splits
+  __shared__ int s_sp[64], s_ns;             // its splits, in order, and their count
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (tid == 0) {
@@ -680,24 +733,45 @@ rescan_filter_kernel(TrainDev t, const float* __restrict__ qf, const float* __re
       for (int f = 0; f < nf; ++f) u |= mask[f];
     }
     s_u = u;
+    int ns = 0;
+    if (u != ~0ull)
+      for (int b = 0; b < 64; ++b)
+        if ((u >> b) & 1) s_sp[ns++] = b;
+    s_ns = ns;
   }
   __syncthreads();
   const unsigned long long need = s_u;
-  // grid-stride over blocks of NWB x 64 rows; a row block none of whose rows
-  // lies in a split some failed query scans is skipped before its rows load
-  // (a targeted rescan reads only the flagged splits' rows)
-  const int64_t nrb = (t.n_pad + NWB * 64 - 1) / (NWB * 64);
-  for (int64_t rbk = blockIdx.x; rbk < nrb; rbk += gridDim.x) {
-  const int64_t row0 = (rbk * NWB + wv) * 64;
-  const bool active = row0 < t.n_pad;
-  // split of this wave's 64 rows (64 | trows)
-  const int wsp = mask ? (int)((row0 / trows) % S) : 0;
-  if (mask && need != ~0ull) {
-    unsigned long long bits = 0;  // (block-uniform)
-    for (int w = 0; w < NWB; ++w) bits |= 1ull << (int)((((rbk * NWB + w) * 64) / trows) % S);
-    if (!(bits & need)) continue;
+  // Units of 64 rows, one per wave; a workgroup's NWB waves take NWB
+  // consecutive units per step (grid-stride).  A targeted rescan (every
+  // failed query flags some splits) walks only those splits' tiles -- tile
+  // sp + k S holds trows / 64 units (64 | trows) -- so a workgroup loads
+  // only rows it scans and no step is spent skipping (cfg2: one failed
+  // query, one split's 103 tiles, at most one tile per workgroup); else
+  // every row, unit u = rows 64 u ...
+  const bool tgt = mask && need != ~0ull;
+  const int gpt = tgt ? (int)(trows / 64) : 1;
+  const int64_t ntile = tgt ? (t.n_pad + trows - 1) / trows : 0;
+  const int64_t units = tgt ? (int64_t)s_ns * ((ntile + S - 1) / S) * gpt : (t.n_pad + 63) / 64;
+  for (int64_t u0 = (int64_t)blockIdx.x * NWB; u0 < units; u0 += (int64_t)gridDim.x * NWB) {
+  const int64_t u = u0 + wv;
+  int64_t row0 = -1;
+  int wsp = 0;  // split of this wave's 64 rows
+  if (u < units) {
+    if (tgt) {
+      const int64_t r = u / gpt, k = r / s_ns;
+      const int sp = s_sp[r - k * s_ns];
+      const int64_t tile = sp + k * S;
+      if (tile < ntile) {
+        row0 = tile * trows + (u - r * gpt) * 64;
+        wsp = sp;
+      }
+    } else {
+      row0 = u * 64;
+      wsp = mask ? (int)((row0 / trows) % S) : 0;
+    }
   }
-  __syncthreads();  // every wave is done with the previous row block's group loop
+  const bool active = row0 >= 0 && row0 < t.n_pad;
+  __syncthreads();  // every wave is done with the previous step's group loop
 
   float* my_rows = rows + (size_t)wv * 64 * RSF;
   if (active) {  // X32 carries 1 KiB of slack past the last row
@@ -752,7 +826,7 @@ rescan_filter_kernel(TrainDev t, const float* __restrict__ qf, const float* __re
           rescan_append(acc[qi], thr_s[qi], g0 + qi, row0 + lane, t, fcnt, buf);
     }
   }
-  }  // row blocks
+  }  // units
 }
 
 // DP > 256 (rows too long to stage 64 per wave): 4 lanes per train row, 16
@@ -885,7 +959,7 @@ rescan_finish_fast_kernel(TrainDev t, const double* __restrict__ Q64,
     __syncthreads();
     int C2 = 1;
     while (C2 < c) C2 <<= 1;
-    exact_sorted<METRIC, NT>(t, qv, di, dk, tb, c, C2, tid);
+    exact_sorted<METRIC, NT>(t, qv, di, dk, tb, c, C2, tid, NT * 17);
     const int need = sink.mode == MODE_SINGLE ? sink.k : sink.w;
     for (int i = tid; i < need && i < c; i += NT) ls[i] = t.lab[di[i]];
     __syncthreads();
@@ -1023,13 +1097,6 @@ void launch_rescan(int metric, const TrainDev& t, const double* Q64, const Resca
     const unsigned long long* mk = rb.S > 0 && rb.S <= 64 && rb.trows > 0 ? rb.mask : nullptr;
     const int mS = mk ? rb.S : 1;
     const int64_t mT = mk ? rb.trows : 64;
-    const int gp = std::min(cap, 256);
-    if (metric == 0)
-      hipLaunchKernelGGL(rescan_prep_kernel<0>, dim3(gp), dim3(64), 0, s, t, Q64, rb.q, rb.tau,
-                         rb.cnt, cap, f_err, rb.qf, rb.thr, rb.fcnt, rb.nkeep);
-    else
-      hipLaunchKernelGGL(rescan_prep_kernel<1>, dim3(gp), dim3(64), 0, s, t, Q64, rb.q, rb.tau,
-                         rb.cnt, cap, f_err, rb.qf, rb.thr, rb.fcnt, rb.nkeep);
     constexpr int FQ = 16;
     const size_t qbytes = (size_t)FQ * (t.DP + 1) * 4;
     if (t.DP <= kRescanStageMaxDP) {
@@ -1037,8 +1104,9 @@ void launch_rescan(int metric, const TrainDev& t, const double* Q64, const Resca
       const size_t tile = (size_t)64 * (t.DP + 4) * 4;
       const int nwb = (int)std::max<size_t>(1, std::min<size_t>(4, (150 * 1024 - qbytes) / tile));
       const int64_t rpb = 64 * nwb;
-      // (grid-stride over row blocks: a targeted rescan skips most of them;
-      // one block per CU -- its ~150 KiB of LDS admits no second one)
+      // (grid-stride over 64-row units, a targeted rescan's only over the
+      // flagged splits' tiles; one block per CU -- its ~150 KiB of LDS admits
+      // no second one)
       const dim3 fg((unsigned)std::min<int64_t>((t.n_pad + rpb - 1) / rpb, std::max(1, rb.cus)));
       const size_t flds = qbytes + nwb * tile;
       if (metric == 0)

@@ -305,14 +305,19 @@ class Classifier:
         set_train: "order" -1 = region order only for integer-coded sets whose
         int8 image is <= 192 MB (n / 16384 regions, up to 64, at least 8),
         1 = n / 16384 regions (off below n = 32768); "nblk" -1 = norm blocks
-        for integer-coded sets of more than 16384 rows (d <= 256)."""
+        for integer-coded sets of more than 16384 rows (d <= 256), 1 on, 2 on
+        as plain sorted windows, 3 without spreading the sub-tiles over the
+        window's tiles."""
         _check(lib().knn_set_tuning(self._h, key.encode(), int(value)))
 
     def last_candidate_path(self):
         return int(lib().knn_last_candidate_path(self._h))
 
-    def set_timing(self, enable=True):
-        _check(lib().knn_set_timing(self._h, int(bool(enable))))
+    def set_timing(self, enable=True, kernel_only=False):
+        """HIP-event phase timing (knn_set_timing): every phase, or with
+        kernel_only the candidate kernel alone (2 events per call instead of
+        5; each event record holds the stream a few microseconds)."""
+        _check(lib().knn_set_timing(self._h, 0 if not enable else (2 if kernel_only else 1)))
 
     def last_phase_ms(self, phase):
         return float(lib().knn_last_phase_ms(self._h, int(phase)))

@@ -205,7 +205,10 @@ int knn_normalize(knn_ctx* ctx, double* const* sets, const int64_t* rows, int32_
  * rescan.  knn_last_phase_ms: the last classify/search call (waits for it;
  * -1 if none).  knn_timing_totals: per-phase sums over every timed call
  * since the last reset, and their number (waits for them); reset != 0
- * starts a new sum.  Recording never makes a call wait. */
+ * starts a new sum.  Recording never makes a call wait.  enable: 0 off, 1
+ * every phase (5 events per call), 2 the candidate kernel only (2 events:
+ * each event record holds the stream ~6 us, profiles/ab_log.md r5u; the
+ * other phases then read -1 / 0). */
 #define KNN_PHASE_PREP 0
 #define KNN_PHASE_CANDIDATE 1
 #define KNN_PHASE_RERANK 2
@@ -281,7 +284,10 @@ const char* knn_last_kernel_name(knn_ctx* ctx);
  * 16384-row window of the image order sorted by the rows' squared norm, so
  * the int8 kernels' per-sub-tile seed bound is tight; -1 auto -- on for
  * integer-coded train sets of more than 16384 rows at d <= 256 -- 0 off, 1
- * on); "s3gq" (the fp16 d > 256 kernel's largest XCD grouping of query
+ * on, 2 on as plain sorted windows, 3 on with the interleave only: by
+ * default the norm ranks of each 32-row sub-tile are spread over the int8
+ * kernel's per-lane lists and the sub-tiles over the window's tiles, so rows
+ * of adjacent norm share neither a list nor a split); "s3gq" (the fp16 d > 256 kernel's largest XCD grouping of query
  * tiles, 0 = 4); "xhswz" (the fp16 image's chunk swizzle: 1 on, 0 off);
  * all of them leave results exact. */
 int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value);
