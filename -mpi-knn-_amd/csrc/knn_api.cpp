@@ -1127,7 +1127,8 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
     t8.DP = DP;
     launch_merge_rerank(metric, (const float*)ctx->cand_v.p, (const int*)ctx->cand_i.p, NL, R, t8,
                         dQ, m, W, C, 0.0,
-                        ProxyScale{qvalid, 0.0, 1.0 / DP, false, (const double*)ctx->i8_cent.p, qpos},
+                        ProxyScale{qvalid, 0.0, 1.0 / DP, false, (const double*)ctx->i8_cent.p, qpos,
+                                   (const signed char*)ctx->XI.p, DP + 16, DP, ctx->i8_swz},
                         cl.gthr, sink,
                         (int*)ctx->rescan_q.p, (double*)ctx->rescan_tau.p, (int*)ctx->rescan_cnt.p,
                         sm, rp, s);

@@ -179,6 +179,11 @@ struct ProxyScale {
   // queries in region order: query q's lists and thresholds sit at position
   // qpos[q] (null: at q)
   const int* qpos = nullptr;
+  // int8 pass: the train image (rows of i8rb bytes, i8dp codes, chunks
+  // swizzled when i8swz) -- the exact re-rank of a query on the train grid
+  // reads it instead of the fp64 rows (merge_rerank_kernel, exact_sorted_i8)
+  const signed char* i8x = nullptr;
+  int i8rb = 0, i8dp = 0, i8swz = 0;
 };
 // Per-split certification (merge) and the targeted rescan: a query whose
 // bound fails only through some splits' lists (a list holding R of its top

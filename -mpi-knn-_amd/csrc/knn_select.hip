@@ -4,6 +4,17 @@
 
 #include <algorithm>
 
+// Timing-only experiment builds (tools: a variant library): the merge kernel
+// returns after stage N (1 loads + error bound, 2 + selection, 3 + exact
+// re-rank); 0 in production.  KNN_DEBUG_CERT: print each certification
+// failure's bounds (diagnostic build).
+#ifndef KNN_MERGE_STOP
+#define KNN_MERGE_STOP 0
+#endif
+#ifndef KNN_DEBUG_CERT
+#define KNN_DEBUG_CERT 0
+#endif
+
 namespace knnk {
 
 // ------------------------------------------------ finish: vote / outputs
@@ -267,6 +278,63 @@ __device__ void exact_sorted(const TrainDev& t, const double* qv, int* di, doubl
   bitonic_sort_lds(dk, di, C2, tid, NT);
 }
 
+// The exact re-rank of a query on the int8 pass's train grid (every
+// coordinate q_i = (cent_i + kq_i) / 2^s, as every train value is): each
+// term (q_i - x_i)^2 = (kq_i - kx_i)^2 / 4^s of the reference's sequential
+// fp64 sum (cpp:33-50) is exact, and so is every partial sum (multiples of
+// 4^-s below d 255^2 / 4^s < 2^53 4^-s), i.e. the reference's r is exactly
+// (||kq||^2 + ||kx||^2 - 2 kq.kx) / 4^s -- integer arithmetic on the codes,
+// v_dot4_i32_i8 over 16-B chunks of the int8 image rows (a row's 144 B
+// instead of its 1 KiB of fp64 values: the merge at cfg2 reads ~13 rows per
+// query) -- and sqrt(r) is the reference's distance bit for bit.  di holds
+// image positions on entry and train rows on exit; then as exact_sorted
+// (pads, (dist, idx) sort).  8 lanes per row, NT / 8 rows per pass.
+template <int NT>
+__device__ void exact_sorted_i8(const TrainDev& t, const ProxyScale& ps, const signed char* qc,
+                                int qq, int* di, double* dk, int cn, int C2, int tid) {
+  constexpr int G = 8, RP = NT / G;
+  const int g = tid & (G - 1);
+  const int nch = ps.i8dp / 16;
+  const double sc = __builtin_ldexp(1.0, -2 * t.jx);  // (t.jx = s: the pass's scale)
+  for (int r0 = 0; r0 < cn; r0 += RP) {
+    const int c = r0 + tid / G;
+    int dot = 0, xx = 0;
+    if (c < cn) {
+      const int p = di[c];
+      const signed char* row = ps.i8x + (int64_t)p * ps.i8rb;
+      const int sw = ps.i8swz ? xh_swz(p & 15) : 0;
+      for (int ch = g; ch < nch; ch += G) {
+        const int4 xv = *(const int4*)(row + ((ch ^ sw) << 4));
+        const int4 qv = *(const int4*)(qc + (ch << 4));
+        dot = __builtin_amdgcn_sdot4(xv.x, qv.x, dot, false);
+        dot = __builtin_amdgcn_sdot4(xv.y, qv.y, dot, false);
+        dot = __builtin_amdgcn_sdot4(xv.z, qv.z, dot, false);
+        dot = __builtin_amdgcn_sdot4(xv.w, qv.w, dot, false);
+        xx = __builtin_amdgcn_sdot4(xv.x, xv.x, xx, false);
+        xx = __builtin_amdgcn_sdot4(xv.y, xv.y, xx, false);
+        xx = __builtin_amdgcn_sdot4(xv.z, xv.z, xx, false);
+        xx = __builtin_amdgcn_sdot4(xv.w, xv.w, xx, false);
+      }
+    }
+#pragma unroll
+    for (int o = 1; o < G; o <<= 1) {
+      dot += __shfl_xor(dot, o, 64);
+      xx += __shfl_xor(xx, o, 64);
+    }
+    if (c < cn && g == 0) dk[c] = __builtin_sqrt((double)(qq + xx - 2 * dot) * sc);
+  }
+  __syncthreads();
+  if (t.perm)  // image positions -> train rows (region order)
+    for (int c = tid; c < cn; c += NT) di[c] = t.perm[di[c]];
+  for (int c = tid; c < C2; c += NT) {
+    if (c >= cn) {
+      dk[c] = KNN_INF_D;
+      di[c] = INT_MAX;
+    }
+  }
+  bitonic_sort_lds(dk, di, C2, tid, NT);
+}
+
 // The certification test: every row whose proxy is >= LB (unscaled) has an
 // exact distance beyond dw, the W-th exact distance re-ranked (rigorous error
 // bound E; +inf LB: no such row can be closer)
@@ -289,6 +357,10 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int s_cn, s_cert, s_f;
   __shared__ double s_lb, s_lbr, s_qa, s_e, s_pinv;
+  // the int8 pass: the query's codes and their squared norm, and whether it
+  // is on the train grid (exact_sorted_i8)
+  __shared__ __attribute__((aligned(16))) signed char s_qc[256];
+  __shared__ int s_qq, s_i8x;
   __shared__ uint32_t s_bs[64];  // per split: min over its full lists' R-th entries (keys)
   const int d = t.d;
   // the query row is staged in LDS up to kMergeLdsDim dims, else read in place
@@ -308,6 +380,7 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
   if (tid < 64) s_bs[tid] = kKeyInf;
   __syncthreads();
 
+  bool i8x = false;  // (wave 0) exact re-rank on the int8 codes
   if (tid < 64) {
     // error bound of this query's proxies (the candidate operands are centred)
     double qa = 0.0, q1 = 0.0;
@@ -348,13 +421,25 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
       // does); with delta = Q - k_q, |qa + proxy - d^2| gains
       // 2 |delta . k_x| 4^-s <= 2 ||delta|| 2^-s sqrt(x2max) (value units)
       double dq2 = 0.0;
+      int qq = 0;
       for (int c = lane; c < d; c += 64) {
         const double y = __builtin_ldexp(qv[c], t.jx) - ps.i8c[c];
         const double r = __builtin_fmin(__builtin_fmax(__builtin_rint(y), -128.0), 127.0);
         dq2 += (y - r) * (y - r);
+        if (ps.i8x && c < 256) {
+          s_qc[c] = (signed char)(int)r;
+          qq += (int)r * (int)r;
+        }
       }
-      const double dq = __builtin_sqrt(wave_sum_d(dq2) * (1.0 + 1e-12)) * (1.0 + 1e-12);
+      if (ps.i8x)
+        for (int c = d + lane; c < ps.i8dp && c < 256; c += 64) s_qc[c] = 0;
+      dq2 = wave_sum_d(dq2);
+      qq = wave_sum_i(qq);
+      const double dq = __builtin_sqrt(dq2 * (1.0 + 1e-12)) * (1.0 + 1e-12);
       E += 2.0 * __builtin_ldexp(dq, -t.jx) * __builtin_sqrt(t.x2max) * 1.001;
+      // on the grid (no coding error): the exact re-rank runs on the codes
+      i8x = ps.i8x && dq2 == 0.0 && ps.i8dp <= 256;
+      if (lane == 0) s_qq = qq;
     }
     // proxies are in scaled units (operands 2^jx (x - mu), knn_prep.hip):
     // unscale exactly; operand values outside the format's normal range add
@@ -394,6 +479,9 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
       nv += __popcll(__ballot(v[e] < KNN_INF_F));
     }
     mlr = wave_min(mlr);
+#if KNN_MERGE_STOP == 1
+    if (nv >= 0) return;  // (timing-only experiment build: the loads and the error bound)
+#endif
     double tsel = KNN_INF_D;  // select proxies <= tsel
     if (nv > W) {
       // radix select of the key of the W-th smallest proxy (finite: nv > W),
@@ -478,9 +566,10 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
       cn = min(cn, Cmax);
       lbx = key2f(pre);
     }
-    if (t.perm) {
+    if (t.perm && !i8x) {
       // image positions -> train rows (region order), one batch of
-      // independent loads (the wave's own LDS writes above complete first)
+      // independent loads (the wave's own LDS writes above complete first;
+      // exact_sorted_i8 reads the image rows first and maps after)
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       const int nsel = min(cn, Cmax);
@@ -506,6 +595,7 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
       s_pinv = pinv;
       s_qa = qa;
       s_e = E;
+      s_i8x = i8x;
     }
   }
   __syncthreads();
@@ -535,7 +625,16 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
     return;
   }
 
-  exact_sorted<METRIC, NT, EPT>(t, qv, di, dk, tb, cn, C2, tid, min(NT, C2) * 17);
+#if KNN_MERGE_STOP == 2
+  if (cn >= 0) return;  // (timing-only experiment build: + selection)
+#endif
+  if (METRIC == 0 && s_i8x)
+    exact_sorted_i8<NT>(t, ps, s_qc, s_qq, di, dk, cn, C2, tid);
+  else
+    exact_sorted<METRIC, NT, EPT>(t, qv, di, dk, tb, cn, C2, tid, min(NT, C2) * 17);
+#if KNN_MERGE_STOP == 3
+  if (cn >= 0) return;  // (timing-only experiment build: + exact re-rank and sort)
+#endif
 
   // certification: every row not re-ranked has proxy >= LB, hence exact
   // distance >= the bound below (rigorous error bound E)
