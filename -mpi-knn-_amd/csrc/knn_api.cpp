@@ -1014,7 +1014,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
     launch_prep_i8_queries(dQ, t.mu, qscale, t.jx, DBL_MAX, (const double*)ctx->i8_cent.p, m, t.d,
                            DP, m_pad, ctx->i8_s, (signed char*)ctx->Q32.p, qvalid, s, qperm,
                            gthr_init ? (uint32_t*)ctx->gthr.p : nullptr, active,
-                           (int*)ctx->ord_bcnt.p, bcnt_clear);
+                           (int*)ctx->ord_bcnt.p, bcnt_clear, (int*)ctx->rescan_cnt.p);
     if (bcnt_clear) ctx->ord_bcnt_zero = bcnt_clear;
   } else if (s3h)
     launch_prep_half_tiled(dQ, t.mu, m, t.d, DP, m_pad, t.jx, -2.0, (unsigned short*)ctx->Q32.p,
@@ -1090,7 +1090,8 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
     return knn_fail(KNN_ERR_ARG, "no candidate kernel for this geometry (tuning overrides?)");
   HIP_TRY(hipGetLastError());
   if (hipEvent_t ev = timing_ev(tc, 2)) HIP_TRY(hipEventRecord(ev, s));
-  HIP_TRY(hipMemsetAsync(ctx->rescan_cnt.p, 0, 4 * sizeof(int), s));
+  // the rescan / tie counters (the int8 query builder cleared them already)
+  if (kmetric < 5) HIP_TRY(hipMemsetAsync(ctx->rescan_cnt.p, 0, 4 * sizeof(int), s));
   // per-split certification: a query failing only through some splits'
   // lists rescans just those splits' rows (knn_select.hip)
   SplitMap sm;

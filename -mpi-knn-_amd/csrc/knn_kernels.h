@@ -306,12 +306,12 @@ void launch_prep_i8_train(const double* X64, const double* cent, int64_t n, int 
 // qperm (query operand builders): operand row p <- query qperm[p] (null: p).
 // The int8 builder also runs launch_query_check's test (mu, scale, jx, limit)
 // into valid, with gthr set launch_fill_gthr's init of each row's slots, and
-// clears zero[0, nzero).
+// clears zero[0, nzero) and zero4[0, 4) (when set).
 void launch_prep_i8_queries(const double* Q64, const double* mu, double scale, int jx,
                             double limit, const double* cent, int64_t m, int d, int DP,
                             int64_t m_pad, int s, signed char* out, float* valid, hipStream_t st,
                             const int* qperm, uint32_t* gthr, int active, int* zero = nullptr,
-                            int64_t nzero = 0);
+                            int64_t nzero = 0, int* zero4 = nullptr);
 int pad_dim_i8(int d);  // padded dim of the int8 kernel (a multiple of 64, <= 256), -1 if none
 int pad_dim_i8w(int d); // padded dim of the int8 32x32x32 kernel (metric 6), -1 if none
 // The reference's exact neighbour order on exact distance ties (knn_select.hip,

@@ -488,16 +488,19 @@ void launch_prep_i8_train(const double* X64, const double* cent, int64_t n, int 
 // set, row p's threshold slots as launch_fill_gthr writes them -- one kernel
 // instead of three (~4-6 us each at cfg2, profiles/r5_kernels_cfg2.json).
 // zero[0, nzero): the region sort's block counts, read by this call's sort
-// (which ran before) and cleared here for the next call's histogram.
+// (which ran before) and cleared here for the next call's histogram; zero4:
+// the call's rescan / tie counters (4 ints, read by the merge), cleared here
+// instead of by a memset launch after the candidate kernel.
 __global__ void __launch_bounds__(256)
 prep_i8_queries_kernel(const double* __restrict__ Q64, const double* __restrict__ mu, double scale,
                        int jx, double limit, const double* __restrict__ cent, int64_t m, int d,
                        int DP, int64_t m_pad, int s, signed char* __restrict__ out,
                        float* __restrict__ valid, const int* __restrict__ qperm,
                        uint32_t* __restrict__ gthr, int active, int* __restrict__ zero,
-                       int64_t nzero) {
+                       int64_t nzero, int* __restrict__ zero4) {
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < nzero; e += (int64_t)gridDim.x * 256)
     zero[e] = 0;
+  if (zero4 && blockIdx.x == 0 && threadIdx.x < 4) zero4[threadIdx.x] = 0;
   const int lane = threadIdx.x & 63;
   const int64_t wstride = (int64_t)gridDim.x * 4;
   for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < m_pad; row += wstride) {
@@ -530,12 +533,12 @@ void launch_prep_i8_queries(const double* Q64, const double* mu, double scale, i
                             double limit, const double* cent, int64_t m, int d, int DP,
                             int64_t m_pad, int s, signed char* out, float* valid, hipStream_t st,
                             const int* qperm, uint32_t* gthr, int active, int* zero,
-                            int64_t nzero) {
+                            int64_t nzero, int* zero4) {
   int64_t blocks = (m_pad + 3) / 4;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(prep_i8_queries_kernel, dim3((unsigned)blocks), dim3(256), 0, st, Q64, mu,
                      scale, jx, limit, cent, m, d, DP, m_pad, s, out, valid, qperm, gthr, active,
-                     zero, nzero);
+                     zero, nzero, zero4);
 }
 
 __global__ void fill_i32_kernel(int32_t* p, int64_t n, int32_t v) {

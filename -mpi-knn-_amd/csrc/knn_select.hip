@@ -459,6 +459,10 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
     const int64_t qp = ps.qpos ? ps.qpos[q] : q;
     const float* lv = cv + qp * U;
     const int* li = ci + qp * U;
+    // the query's final global-threshold slots (cand_kernel), loaded with the
+    // lists: the kernel also filtered with them, so rows it dropped have
+    // proxy >= max over the slots (lane s < kGthrSlots holds slot s)
+    const uint32_t gsl = gthr && lane < kGthrSlots ? gthr[qp * kGthrSlots + lane] : 0u;
     float v[EPL];
     int id[EPL];
     float mlr = KNN_INF_F;
@@ -577,16 +581,7 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       __builtin_amdgcn_wave_barrier();
     }
-    // the candidate kernel also filtered with the query's global threshold
-    // (cand_kernel): rows it dropped have proxy >= its final value
-    float tq = KNN_INF_F;
-    if (gthr) {
-      const uint32_t* g = gthr + qp * kGthrSlots;
-      uint32_t mk = g[0];
-#pragma unroll
-      for (int e = 1; e < kGthrSlots; ++e) mk = max(mk, g[e]);
-      tq = key2f(mk);
-    }
+    const float tq = gthr ? key2f(wave_max_u(gsl)) : KNN_INF_F;
     if (lane == 0) {
       // void proxies: exact rescan below; non-finite query: no neighbours
       s_cn = nonfinite ? -1 : (void_q ? Cmax + 1 : cn);
