@@ -98,6 +98,12 @@ static_assert(KNN_RES_TPB * knnk::kTR == knnk::kResTileRows || KNN_RES_TPB != 2,
 #ifndef KNN_I8W_Q4
 #define KNN_I8W_Q4 1
 #endif
+// metric 6: issue priority of a wave inside its selection slow path (0:
+// none).  At 2: cfg2 candidate -1.1 %, the 12.5M x 96 shard -0.6 % in every
+// interleaved pair (profiles/ab_log.md r5ag)
+#ifndef KNN_SLOWPRIO
+#define KNN_SLOWPRIO 2
+#endif
 
 
 namespace knnk {
@@ -493,6 +499,11 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
     selc.bpcold += cnt_it < 2 && __builtin_amdgcn_ballot_w64(mx > tn[0] - smx) != 0;
 #endif
     if (__builtin_amdgcn_ballot_w64(mx > tn[0] - smx)) {
+#if KNN_SLOWPRIO
+      // the slow path at a raised issue priority: the other 7 waves of the
+      // workgroup wait for it at the next barrier
+      __builtin_amdgcn_s_setprio(KNN_SLOWPRIO);
+#endif
       i32x16 b = a;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -502,6 +513,9 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       }
       if constexpr (W4) select_block_i8w4<R>(b, row0, L[0], I[0], L2, I2, tn[0], selc);
       else select_block_i8<R>(b, row0, L[0], I[0], tn[0], selc);
+#if KNN_SLOWPRIO
+      __builtin_amdgcn_s_setprio(0);
+#endif
     }
    }
   };

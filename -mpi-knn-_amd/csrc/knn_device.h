@@ -545,13 +545,28 @@ __device__ __forceinline__ float i8_proxy(int acc) {
 // a list entry as the proxy the merge reads (float lists: itself)
 __device__ __forceinline__ float lval(float v) { return v; }
 __device__ __forceinline__ float lval(int acc) { return i8_proxy(acc); }
+// L[t] = min(L[t-1], max(v, L[t])) in one v_med3_i32 (L[t-1] >= L[t]: the
+// median of the three is that clamp); the compiler only forms med3 from
+// constant bounds and otherwise emits a v_max + v_min pair per position
+#ifndef KNN_MED3
+#define KNN_MED3 1
+#endif
+__device__ __forceinline__ int clamp_desc(int v, int lo, int hi) {
+#if KNN_MED3
+  int r;
+  asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(v), "v"(lo), "v"(hi));
+  return r;
+#else
+  return min(hi, max(v, lo));
+#endif
+}
 template <int R>
 __device__ __forceinline__ void list_insert_desc(int (&L)[R], int (&I)[R], int v, int id) {
   bool cc = true;  // v > L[R-1] by precondition
 #pragma unroll
   for (int t = R - 1; t > 0; --t) {
     const bool cp = v > L[t - 1];
-    L[t] = min(L[t - 1], max(v, L[t]));
+    L[t] = clamp_desc(v, L[t], L[t - 1]);
     I[t] = cp ? I[t - 1] : (cc ? id : I[t]);
     cc = cp;
   }
