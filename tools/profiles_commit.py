@@ -64,6 +64,13 @@ def kernels(trace):
     return per
 
 
+def timed_slice(launches, steps):
+    """The candidate launches of bench.timed_run's K timed calls: they are
+    followed by min(K, 5) untimed calls that record every phase's events."""
+    tail = min(steps, 5)
+    return launches[-(steps + tail):-tail]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tag", default="r2")
@@ -94,7 +101,7 @@ def main():
             d = [e - s for s, e, _ in v]
             rec = {"dispatches": len(d), "mean_ns_all": sum(d) / len(d), "min_ns": min(d)}
             if k == cand:
-                timed = d[-wl["steps"]:]
+                timed = timed_slice(d, wl["steps"])
                 rec["mean_ns_timed"] = sum(timed) / len(timed)
                 flops = line["roofline"]["algorithmic_flops_per_launch"]
                 ach = flops / (rec["mean_ns_timed"] * 1e-9) / 1e12
@@ -126,7 +133,7 @@ def main():
         line = bench_line(os.path.join(src, "api_cfg2.log"))
         cand = line["roofline"]["kernel"]
         launches = sorted(per[cand], key=lambda x: x[0])
-        timed = launches[-WORKLOADS["cfg2"]["steps"]:]
+        timed = timed_slice(launches, WORKLOADS["cfg2"]["steps"])
         corr = {c for _, _, c in timed}
         api = list(csv.DictReader(open(os.path.join(adir, "run_hip_api_trace.csv"))))
         by_corr = {int(r["Correlation_Id"]): r for r in api}
