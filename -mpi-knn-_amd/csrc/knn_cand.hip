@@ -221,20 +221,8 @@ cand_stream_kernel(const float* __restrict__ X32, const float* __restrict__ xini
 // and two v_mfma_f32_32x32x16_f16 per block and chunk (one per 16 dims,
 // products exact in fp32) instead of three bf16 ones per 16 dims: 3x fewer
 // MFMAs per algorithmic flop and half the staged bytes per MFMA.
-// Two LDS rings with their own prefetch distances: row chunks (+ seeds) in
-// KNN_S3_NR buffers, staged by waves 0-3 NR - 1 steps ahead; query chunks in
-// KNN_S3_NQ buffers, staged by waves 4-7 NQ - 1 steps ahead.  Each wave's
-// vmcnt counts only its own ring's pieces, so the two streams get their own
-// leads.  The staging waits on the query chunks (re-read every train tile and
-// thrashed out of the XCD's L2 by the row stream, so served by the MALL), not
-// on the rows: cfg5 (d = 960, k = 100) 19.8-19.9 ms with one shared ring of
-// 4, 19.3-19.6 with the rows 1 step and the queries 6 steps ahead, 21.3-22.7
-// with longer row leads (profiles/ab_log.md r5ah, r5ai)
-#ifndef KNN_S3_NR
-#define KNN_S3_NR 2
-#endif
-#ifndef KNN_S3_NQ
-#define KNN_S3_NQ 7
+#ifndef KNN_S3_NB
+#define KNN_S3_NB 4
 #endif
 // Q16: A-fragment ring depth (LDS reads in flight behind the MFMAs) and
 // whether the MFMA / read interleave is pinned with sched_group_barrier
@@ -244,7 +232,7 @@ cand_stream_kernel(const float* __restrict__ X32, const float* __restrict__ xini
 #ifndef KNN_S3_SCHED
 #define KNN_S3_SCHED 1
 #endif
-// one 8-wave workgroup per CU (the two LDS rings take 146 KiB): 2 waves
+// one 8-wave workgroup per CU (the 4-deep LDS ring takes 132 KiB): 2 waves
 // per SIMD, so up to 256 registers each for fragments in flight
 #ifndef KNN_S3_WPE
 #define KNN_S3_WPE 2
@@ -254,9 +242,7 @@ __device__ __forceinline__ void s3_wait_barrier(int n) {
   switch (n) {
 #define KNN_W(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")\n\ts_barrier" ::: "memory"); break;
     KNN_W(1) KNN_W(2) KNN_W(3) KNN_W(4) KNN_W(5) KNN_W(6) KNN_W(7) KNN_W(8) KNN_W(9) KNN_W(10)
-    KNN_W(11) KNN_W(12) KNN_W(13) KNN_W(14) KNN_W(15) KNN_W(16) KNN_W(17) KNN_W(18) KNN_W(19)
-    KNN_W(20) KNN_W(21) KNN_W(22) KNN_W(23) KNN_W(24) KNN_W(25) KNN_W(26) KNN_W(27) KNN_W(28)
-    KNN_W(29) KNN_W(30) KNN_W(31)
+    KNN_W(11) KNN_W(12) KNN_W(13) KNN_W(14) KNN_W(15)
 #undef KNN_W
     default: asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   }
@@ -318,11 +304,11 @@ cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* 
   // abl: timing-only ablations as in cand_kernel (bit0 no staging after the
   // first steps, bit1 no selection epilogue); 0 in production.
   constexpr int BLK = kS3R * 64;        // bytes of one operand image
-  constexpr int BUFR = BLK + 1024;      // row ring buffer: A (rows) | seeds
-  constexpr int NR = KNN_S3_NR, NQ = KNN_S3_NQ;
-  static_assert(4 * (NR - 2) + NR - 1 + 2 <= 31 && 4 * (NQ - 2) + 2 <= 31 && NR >= 2 && NQ >= 2,
-                "vmcnt wait range");
-  __shared__ __attribute__((aligned(16))) unsigned char lds[NR * BUFR + NQ * BLK];
+  constexpr int BUFB = 2 * BLK + 1024;  // A (rows) | B (queries) | seeds
+  constexpr int NB = KNN_S3_NB;  // LDS buffers: prefetch distance NB - 1 steps
+  constexpr int PD = NB - 1;
+  static_assert(4 * (PD - 1) + PD <= 15, "vmcnt wait range");
+  __shared__ __attribute__((aligned(16))) unsigned char lds[NB * BUFB];
   __shared__ __attribute__((aligned(16))) u32x4 gls[Q16 ? 8 * 64 : 1];
 
   int qt, split;
@@ -345,31 +331,21 @@ cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* 
   const int total = my_nt * nch;
   const uint32_t lds_base =
       (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)lds;
-  const unsigned char* ldsq = lds + NR * BUFR;  // the query ring
 
-  // this wave's ring (rows: waves 0-3, queries: 4-7), its prefetch distance
-  // PD (wave-uniform) and issue cursor (chunk, tile, buffer) of the next step
-  const bool rw = wv < 4;
-  const int PD = rw ? NR - 1 : NQ - 1;
-  const int wq = wv & 3;
+  // issue cursor (chunk, tile, buffer) of the next step to stage
   int ic = 0, itile = split, ib = 0;
   auto issue = [&]() {
-    if (rw) {
-      const char* gA = (const char*)XT + ((int64_t)itile * nch + ic) * BLK + lane * 16;
-      const uint32_t l = lds_base + (uint32_t)(ib * BUFR);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) glds16(gA + (wq + 4 * i) * 1024, l + (wq + 4 * i) * 1024);
-      if (ic == 0 && wv == 0)
-        glds16((const char*)(XS + (int64_t)itile * kS3R) + lane * 16, l + BLK);
-      if (++ib == NR) ib = 0;
-    } else {
-      const char* gB = (const char*)QT + ((int64_t)qt * nch + ic) * BLK + lane * 16;
-      const uint32_t l = lds_base + (uint32_t)(NR * BUFR + ib * BLK);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) glds16(gB + (wq + 4 * i) * 1024, l + (wq + 4 * i) * 1024);
-      if (++ib == NQ) ib = 0;
-    }
+    const char* gA = (const char*)XT + ((int64_t)itile * nch + ic) * BLK + lane * 16;
+    const char* gB = (const char*)QT + ((int64_t)qt * nch + ic) * BLK + lane * 16;
+    const uint32_t l = lds_base + (uint32_t)(ib * BUFB);
+    glds16(gA + wv * 1024, l + wv * 1024);
+    glds16(gA + (wv + 8) * 1024, l + (wv + 8) * 1024);
+    glds16(gB + wv * 1024, l + BLK + wv * 1024);
+    glds16(gB + (wv + 8) * 1024, l + BLK + (wv + 8) * 1024);
+    if (ic == 0 && wv == 0)
+      glds16((const char*)(XS + (int64_t)itile * kS3R) + lane * 16, l + 2 * BLK);
     if (++ic == nch) { ic = 0; itile += (abl & 8) ? 0 : S; }  // abl bit 3: see cand_kernel
+    if (++ib == NB) ib = 0;
   };
 
   constexpr int NQL = Q16 ? 2 : 1;  // lists per lane (Q16: one per query block)
@@ -401,12 +377,12 @@ cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* 
     x_age = PD;
   }
 #pragma unroll
-  for (int p = 0; p < NR - 1; ++p)
-    if (p < PD && total > p) issue();
+  for (int p = 0; p < PD; ++p)
+    if (total > p) issue();
 
   f32x16 acc[8];
   f32x4 aq[16][2];  // Q16: [row block][query block]
-  int c = 0, t = split, cbr = 0, cbq = 0, ti = 0;
+  int c = 0, t = split, cb = 0, ti = 0;
   for (int st = 0; st < total; ++st) {
     // own pieces of step st landed (those of st+1 may still be in flight),
     // then the barrier publishes every wave's pieces and retires all reads
@@ -418,7 +394,6 @@ cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* 
       int n = 4 * y;
       if (wv == 0)
         for (int jj = 1; jj <= y; ++jj) n += (c + jj) % nch == 0;
-      // (the wait immediates dispatched below cover 0 .. 31)
       if (abl & 1) n = 0;
       if (x_age >= 0) ++x_age;
       if (x_age >= 1 && x_age <= PD) n += x_ops;
@@ -459,19 +434,18 @@ cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* 
       }
     }
 
-    const unsigned char* buf = lds + cbr * BUFR;         // rows | seeds
-    const unsigned char* qbuf = ldsq + cbq * BLK - BLK;  // queries (at qbuf + BLK)
+    const unsigned char* buf = lds + cb * BUFB;
     if constexpr (Q16) {
       if (c == 0) {
-        const float* seed = (const float*)(buf + BLK);
+        const float* seed = (const float*)(buf + 2 * BLK);
 #pragma unroll
         for (int rb = 0; rb < 16; ++rb) {
           const float4 s4 = *(const float4*)(seed + 16 * rb + 4 * g16);
           aq[rb][0] = aq[rb][1] = f32x4{s4.x, s4.y, s4.z, s4.w};
         }
       }
-      const f16x8 b0 = *(const f16x8*)(qbuf + BLK + off_q + off_16);
-      const f16x8 b1 = *(const f16x8*)(qbuf + BLK + off_q + 16 * 64 + off_16);
+      const f16x8 b0 = *(const f16x8*)(buf + BLK + off_q + off_16);
+      const f16x8 b1 = *(const f16x8*)(buf + BLK + off_q + 16 * 64 + off_16);
       // A fragments through a ring of KNN_S3_RING registers: the read of row
       // block rb + RING is issued as block rb's two MFMAs go out, so RING - 1
       // reads are in flight behind the MFMAs instead of the one or two the
@@ -514,12 +488,11 @@ cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* 
         }
       }
       if (++c == nch) { c = 0; t += S; ++ti; }
-      if (++cbr == NR) cbr = 0;
-      if (++cbq == NQ) cbq = 0;
+      if (++cb == NB) cb = 0;
       continue;
     }
     if (c == 0) {
-      const float* seed = (const float*)(buf + BLK);
+      const float* seed = (const float*)(buf + 2 * BLK);
 #pragma unroll
       for (int bb = 0; bb < 8; ++bb) {
 #pragma unroll
@@ -534,8 +507,8 @@ cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* 
     }
     if constexpr (F16) {
       // k-step 0 = dims 0-15 of the chunk (slots 0, 1), k-step 1 = 16-31 (2, 3)
-      const f16x8 b0 = *(const f16x8*)(qbuf + BLK + off_q + off_hi);
-      const f16x8 b1 = *(const f16x8*)(qbuf + BLK + off_q + off_lo);
+      const f16x8 b0 = *(const f16x8*)(buf + BLK + off_q + off_hi);
+      const f16x8 b1 = *(const f16x8*)(buf + BLK + off_q + off_lo);
 #pragma unroll
       for (int bb = 0; bb < 8; ++bb) {
         const f16x8 a0 = *(const f16x8*)(buf + bb * 32 * 64 + off_hi);
@@ -544,8 +517,8 @@ cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* 
         acc[bb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b1, acc[bb], 0, 0, 0);
       }
     } else {
-      const bf16x8 bh = *(const bf16x8*)(qbuf + BLK + off_q + off_hi);
-      const bf16x8 bl = *(const bf16x8*)(qbuf + BLK + off_q + off_lo);
+      const bf16x8 bh = *(const bf16x8*)(buf + BLK + off_q + off_hi);
+      const bf16x8 bl = *(const bf16x8*)(buf + BLK + off_q + off_lo);
 #pragma unroll
       for (int bb = 0; bb < 8; ++bb) {
         const bf16x8 ah = *(const bf16x8*)(buf + bb * 32 * 64 + off_hi);
@@ -565,8 +538,7 @@ cand_s3_kernel(const unsigned short* XT, const float* XS, const unsigned short* 
       }
     }
     if (++c == nch) { c = 0; t += S; }
-    if (++cbr == NR) cbr = 0;
-    if (++cbq == NQ) cbq = 0;
+    if (++cb == NB) cb = 0;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if constexpr (Q16) {
