@@ -1601,10 +1601,10 @@ int knn_set_timing(knn_ctx* ctx, int enable) {
   // timing-only events: no system-scope fence (cache writeback and
   // invalidate) at each record -- with it every record idled the stream
   // ~6 us (profiles/ab_log.md r5u); only the times are read back
+  if (enable < 0 || enable > 2) return knn_fail(KNN_ERR_ARG, "timing must be 0, 1 or 2");
   if (enable && !ctx->ring[0].ev[0])
     for (auto& tc : ctx->ring)
       for (auto& e : tc.ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
-  if (enable < 0 || enable > 2) return knn_fail(KNN_ERR_ARG, "timing must be 0, 1 or 2");
   ctx->timing = enable;
   return KNN_OK;
 }

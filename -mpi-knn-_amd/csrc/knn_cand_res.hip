@@ -1112,9 +1112,17 @@ static void launch_res(const CandLaunch& c, hipStream_t s) {
 // (int8) with R = 4 (8 on request), NW = 8 or 4 at DP % 64 == 0;
 // METRIC 1 (L1, not perf-graded) with NW = 4 and R in {8, 16}; METRIC 2
 // needs DP % 16 == 0.
+// Metric 6 at R = 4 writes 4 lists per query per split (W4 above) only with
+// KNN_I8W_Q4, KNN_I8_ILIST and KNN_I8_SMAX all on; the host's merge then
+// reads that quad layout (knn_api.cpp: w4).  A build with any of them off
+// has no R = 4 metric-6 kernel, so the host's launch is refused ("no
+// candidate kernel for this geometry") instead of the merge reading 2 lists
+// per split as 4 (stale entries).
+constexpr bool kI8WQuad = KNN_I8W_Q4 && KNN_I8_ILIST && KNN_I8_SMAX;
+
 template <int DP, int R, int M, int NW>
 constexpr bool res_variant() {
-  return (M != 2 || DP % 16 == 0) && (M != 1 || (NW == 4 && R != 4)) &&
+  return (M != 6 || R != 4 || kI8WQuad) && (M != 2 || DP % 16 == 0) && (M != 1 || (NW == 4 && R != 4)) &&
          (M < 3 || (DP % 32 == 0 && (R == 4 || (M >= 5 && R == 8)) && (NW == 8 || M >= 4))) && (NW != 16 || M == 4) &&
          (M != 5 || (DP % 64 == 0 && (NW == 8 || NW == 4))) && (M != 6 || (NW == 8 && (R == 4 || R == 8)));
 }

@@ -471,8 +471,10 @@ void launch_prep_i8_train(const double* X64, const double* cent, int64_t n, int 
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(prep_i8_train_kernel, dim3((unsigned)blocks), dim3(256), 0, st, X64, cent, n,
                      d, DP, n_pad, s, out, codes_max, swz, perm);
-  // n_pad is a multiple of kRowAlign = 256 (whole 128-row groups)
-  const int64_t n_sub = n_pad / 32;
+  // the sub-tile maxima of 128-row group g sit in the pad of its row 1: only
+  // whole groups (callers pass n_pad a multiple of kRowAlign = 256; a ragged
+  // tail group would place them past the image, so it gets none)
+  const int64_t n_sub = n_pad / 128 * 4;
   hipLaunchKernelGGL(prep_i8_smax_kernel, dim3((unsigned)((n_sub + 255) / 256)), dim3(256), 0, st,
                      out, DP, n_sub);
 }

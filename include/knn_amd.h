@@ -208,7 +208,9 @@ int knn_normalize(knn_ctx* ctx, double* const* sets, const int64_t* rows, int32_
  * starts a new sum.  Recording never makes a call wait.  enable: 0 off, 1
  * every phase (5 events per call), 2 the candidate kernel only (2 events:
  * each event record holds the stream ~6 us, profiles/ab_log.md r5u; the
- * other phases then read -1 / 0). */
+ * other phases then read -1 / 0).  Behaviour change (round 5): any other
+ * value of enable (earlier builds took every non-zero value as "on") is
+ * refused with KNN_ERR_ARG and leaves the timing state unchanged. */
 #define KNN_PHASE_PREP 0
 #define KNN_PHASE_CANDIDATE 1
 #define KNN_PHASE_RERANK 2
@@ -261,7 +263,10 @@ const char* knn_last_kernel_name(knn_ctx* ctx);
  * per-query global threshold exchange, results stay exact); -1 = auto for "fp16" (fp16
  * candidate pass: 0 off, 1 on), "i8" (the int8 candidate pass where the
  * train set is integer-coded: 0 off, 1 on at every batch size), "i8w" (int8
- * kernel: -1 auto, 0 the 16x16x64 one, 1 the 32x32x32 one), "mfma16" (bf16x3 on the 16x16x32 layout: 0
+ * kernel: -1 auto, 0 the 16x16x64 one, 1 the 32x32x32 one; also read by
+ * knn_set_train*, whose norm blocks interleave the rows over that kernel's
+ * lane lists -- set it before the train set: a later change keeps results
+ * exact but loses the interleave's certification odds), "mfma16" (bf16x3 on the 16x16x32 layout: 0
  * off, 1 on), "s3q" (the fp16 d > 256 kernel on 16x16x32: 0 off, 1 on) and
  * "gk" (what the global threshold exchange publishes: 0 the lists' R-th
  * entries (resident kernel) / no exchange (S3), K = 1..16 the K-th smallest

@@ -18,9 +18,13 @@ the checks are:
   * exact-tie votes: every query flagged KNN_FLAG_TIE_VOTE is re-run through
     the oracle (std::sort's own tie order) and must get the same label;
   * optimality against an independent fp64 brute force on the GPU
-    (fp64 GEMM form) on a query sample: the reported k distances equal the
-    k smallest distances over ALL train rows to within 1e-10 relative (that
-    brute force's own rounding error is ~1e-14 relative here).
+    (fp64 GEMM form) on EVERY query of the batch (cfg3: its 20k sample),
+    before the oracle: the reported k distances equal the k smallest
+    distances over ALL train rows to within 1e-10 relative (that brute
+    force's own rounding error is ~1e-14 relative here).  Certification
+    assumes the candidate kernel's proxies are right; a kernel that drops
+    rows is seen only by this check (round 5's r5ai variant passed
+    check_properties on 2,500 cfg5 queries).
 Data: bench.synth (Gaussian mixture on the 8-bit grid k/256), seeded."""
 import numpy as np
 import pytest
@@ -88,19 +92,29 @@ def vote(nlab, k):
     return out
 
 
-def brute_force_kdist(X, Q, k, chunk=1 << 18):
+def brute_force_kdist(X, Q, k, chunk=1 << 18, qchunk=2048):
     """Independent fp64 top-k distances over all rows: ||q||^2 + ||x||^2 - 2 q.x
     on the fp64 GEMM (hipBLAS), |error| ~ 1e-16 (||q||^2 + ||x||^2), i.e.
-    ~1e-14 relative at these distances.  (torch.cdist's non-GEMM mode is not
-    used: it returned zeros for some elements on this stack.)"""
+    ~1e-14 relative at these distances.  Rows stream in chunks of `chunk`
+    (their norms formed once per chunk), queries in blocks of `qchunk`, so a
+    whole 10k-query batch against 1M rows (or 1024 queries against 100M)
+    needs at most a [qchunk x chunk] fp64 block at a time.  (torch.cdist's
+    non-GEMM mode is not used: it returned zeros for some elements on this
+    stack.)"""
+    m = Q.shape[0]
+    kk = min(k, X.shape[0])
     qn = (Q * Q).sum(1, keepdim=True)
-    best = None
+    best = torch.full((m, kk), float("inf"), dtype=torch.float64, device=Q.device)
     for c0 in range(0, X.shape[0], chunk):
         Xc = X[c0:c0 + chunk]
-        D2 = qn + (Xc * Xc).sum(1)[None, :] - 2.0 * (Q @ Xc.T)
-        d = torch.topk(D2.clamp_(min=0.0), min(k, D2.shape[1]), dim=1, largest=False).values
-        best = d if best is None else torch.topk(torch.cat([best, d], 1), k, dim=1,
-                                                 largest=False).values
+        xn = (Xc * Xc).sum(1)[None, :]
+        for q0 in range(0, m, qchunk):
+            Qb = Q[q0:q0 + qchunk]
+            D2 = qn[q0:q0 + qchunk] + xn - 2.0 * (Qb @ Xc.T)
+            d = torch.topk(D2.clamp_(min=0.0), min(kk, D2.shape[1]), dim=1, largest=False).values
+            best[q0:q0 + qchunk] = torch.topk(torch.cat([best[q0:q0 + qchunk], d], 1), kk, dim=1,
+                                              largest=False).values
+            del D2, d
     return best.sqrt().cpu().numpy()
 
 
@@ -150,8 +164,15 @@ def check_tie_votes(knn, X, lab_all, Q, k, got, flags, limit=64):
 
 
 def check_optimal(X, Q, k, dist, qs):
+    """The reported k distances are the k smallest over ALL rows (an
+    independent fp64 brute force).  This is the check that sees a dropped
+    neighbour: the certification assumes the candidate
+    kernel's proxies are right, and check_properties only recomputes the rows
+    that were reported.  Run before the oracle on every query of a batch."""
     bf = brute_force_kdist(X, Q[qs], k)
-    np.testing.assert_allclose(dist[qs], bf, rtol=1e-10, atol=0)
+    bad = np.nonzero(~np.isclose(dist[qs], bf, rtol=1e-10, atol=0).all(1))[0]
+    assert bad.size == 0, "%d of %d queries miss a true neighbour, e.g. query %s: got %s want %s" % (
+        bad.size, len(qs), qs[bad[0]], dist[qs[bad[0]]], bf[bad[0]])
 
 
 def test_cfg2_full(knn):
@@ -166,8 +187,8 @@ def test_cfg2_full(knn):
     assert clf.last_rescan_count() * 64 <= m
     lab_all = lab.cpu().numpy()
     check_properties(X, lab_all, Q, k, got, idx, dist, np.arange(m))
+    check_optimal(X, Q, k, dist, np.arange(m))
     check_oracle(X, lab_all, Q, k, got, idx, dist, np.arange(0, m, m // 32))
-    check_optimal(X, Q, k, dist, np.arange(0, m, m // 512))
     check_tie_votes(knn, X, lab_all, Q, k, got, flags)
     # the other candidate paths give the same exact answer: fp16, bf16x3, fp32
     clf.set_tuning("i8", 0)
@@ -203,8 +224,8 @@ def test_cfg3_shard_1m_queries(knn):
     rng = np.random.default_rng(3)
     sample = np.sort(rng.choice(m, 20_000, replace=False))
     check_properties(X, lab_all, Q, k, got, idx, dist, sample)
+    check_optimal(X, Q, k, dist, sample)
     check_oracle(X, lab_all, Q, k, got, idx, dist, sample[::1250])
-    check_optimal(X, Q, k, dist, sample[::40])
     check_tie_votes(knn, X, lab_all, Q, k, got, flags)
     clf.close()
 
@@ -226,8 +247,8 @@ def test_cfg5_d960_k100(knn):
     lab_all = lab.cpu().numpy()
     sample = np.arange(0, m, 4)                  # 2,500 queries
     check_properties(X, lab_all, Q, k, got, idx, dist, sample)
+    check_optimal(X, Q, k, dist, np.arange(m))
     check_oracle(X, lab_all, Q, k, got, idx, dist, np.arange(0, m, m // 8))
-    check_optimal(X, Q, k, dist, np.arange(0, m, m // 80))
     check_tie_votes(knn, X, lab_all, Q, k, got, flags)
     # the fp16 S3 kernel on 32x32x16 and the bf16x3 S3 kernel give the same
     # exact answer
@@ -274,8 +295,8 @@ def test_cfg4_train_sharded_merge(knn):
     got, idx, dist = ol.cpu().numpy(), oi.cpu().numpy(), od.cpu().numpy()
     lab_all = lab.cpu().numpy()
     check_properties(X, lab_all, Q, k, got, idx, dist, np.arange(m))
+    check_optimal(X, Q, k, dist, np.arange(m))
     check_oracle(X, lab_all, Q, k, got, idx, dist, np.arange(0, m, m // 8))
-    check_optimal(X, Q, k, dist, np.arange(0, m, m // 128))
     check_tie_votes(knn, X, lab_all, Q, k, got, of.cpu().numpy())
     for c in ctxs:
         c.close()
@@ -297,8 +318,8 @@ def test_cfg2_full_continuous(knn):
     assert resc * 16 <= m, "fp16 pass certified too few queries (%d rescans)" % resc
     lab_all = lab.cpu().numpy()
     check_properties(X, lab_all, Q, k, got, idx, dist, np.arange(m))
+    check_optimal(X, Q, k, dist, np.arange(m))
     check_oracle(X, lab_all, Q, k, got, idx, dist, np.arange(0, m, m // 32))
-    check_optimal(X, Q, k, dist, np.arange(0, m, m // 512))
     check_tie_votes(knn, X, lab_all, Q, k, got, flags)
     # the fp32 path gives the same exact answer
     clf.set_precision(knn.PRECISION_FP32)

@@ -7,6 +7,15 @@ export TMPDIR=/tmp
 O=gpurun_out
 mkdir -p $O
 B="--steps 30 --warmup 5 --no-cpu-baseline --no-fp32-path --no-continuous --no-dropin --no-train-sharded --no-cfg5 --cfg3-queries 0 $BENCH_ARGS"
+# parity gate per library before any timing (tests/test_gpu_gate.py: the
+# oracle on 8 queries + brute-force optimality on 256 at cfg2)
+for v in $AB_VARIANTS; do
+  if [ $v = base ]; then unset KNN_AMD_VARIANT; else export KNN_AMD_VARIANT=$v; fi
+  timeout -k 10 300 python -u -m pytest -x -q -m gpu --timeout 240 --timeout-method thread \
+      tests/test_gpu_gate.py -s > $O/${TAG}_gate_$v.log 2>&1
+  rc=$?; echo "gate $v rc=$rc"; grep "^gate " $O/${TAG}_gate_$v.log
+  [ $rc = 0 ] || exit 1
+done
 for rep in $(seq 1 ${REPS:-2}); do
   for v in $AB_VARIANTS; do
     if [ $v = base ]; then unset KNN_AMD_VARIANT; else export KNN_AMD_VARIANT=$v; fi

@@ -1,13 +1,22 @@
 #!/bin/bash
-# One GPU call of the build/measure loop (replaces round 3's per-tag
-# r3*_gpu.sh scripts).  Steps, each with its own time limit, stopping at the
+# One GPU call of the build/measure loop (every round's one-shot scripts are
+# folded into it).  Steps, each with its own time limit, stopping at the
 # first failure:
+#   SMOKE=1        __graft_entry__.smoke()         -> gpurun_out/$TAG_smoke.log
 #   TESTS=1        the whole -m gpu suite          -> gpurun_out/$TAG_tests.log
 #   TESTS="<args>" those pytest arguments instead
 #   AB_VARIANTS    cross-process A/B of lib/libknn_amd_<v>.so ("base" = default)
-#                  with tools/tune.py $AB_ARGS, REPS rounds -> $TAG_ab_<v>_<rep>.log
+#                  with tools/tune.py $AB_ARGS, REPS rounds -> $TAG_ab_<v>_<rep>.log;
+#                  every library first passes the parity gate (tests/test_gpu_gate.py:
+#                  the oracle on 8 queries + brute-force optimality on 256, for each
+#                  tuning variant named in $AB_ARGS; GATE=0 skips) -> $TAG_gate_<v>.log,
+#                  and tune.py itself gates each variant before timing it
 #   BENCH=1        bench.py --steps 20 --warmup 5 -> $TAG_bench.log / .json
 #   PROF=1         rocprofv3 kernel trace + stats of a short bench -> $TAG_prof/
+#   PROF_PARTS     "A R B S": tools/prof_round.sh parts (kernel traces of every
+#                  workload, RCCL API trace, FETCH/WRITE passes, SQ passes)
+#                  -> gpurun_out/prof_$TAG, pmc_sq_$TAG*; tools/profiles_commit.py
+#                  --tag $TAG turns them into profiles/
 # Usage: TAG=r4b TESTS=1 AB_VARIANTS="base fl" AB_ARGS="--rounds 5 auto:0:0" \
 #        bash tools/gpu_round.sh
 #        TAG=r4x AB_SETS="--order 0 auto:0:0;--order -1 auto:0:0" bash tools/gpu_round.sh
@@ -17,6 +26,11 @@ export TMPDIR=/tmp
 O=gpurun_out
 mkdir -p $O
 TAG=${TAG:-run}
+if [ -n "$SMOKE" ]; then
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/${TAG}_smoke.log 2>&1
+  rc=$?; echo "smoke rc=$rc"; tail -1 $O/${TAG}_smoke.log
+  [ $rc = 0 ] || exit $rc
+fi
 if [ -n "$TESTS" ]; then
   args="tests"
   [ "$TESTS" = 1 ] || args="$TESTS"
@@ -25,7 +39,32 @@ if [ -n "$TESTS" ]; then
   rc=$?; echo "tests rc=$rc"; tail -5 $O/${TAG}_tests.log
   [ $rc = 0 ] || exit $rc
 fi
+# gate_env: KNN_GATE* variables from a tune.py argument string (its variants
+# and workload); timing-only ablation variants (bits 1/2/8/16) are skipped
+gate_env() {
+  local g="" prev="" t
+  GN=1000000; GM=10000; GD=128; GK=10
+  for t in $1; do
+    case "$prev" in --n) GN=$t;; --m) GM=$t;; --d) GD=$t;; --k) GK=$t;; esac
+    case "$t" in
+      *:*:*) a=$(echo "$t" | cut -d, -f1 | cut -d: -f4); a=${a:-0}
+             [ $((a & 27)) = 0 ] && g="$g;$t";;
+    esac
+    prev=$t
+  done
+  echo "KNN_GATE='${g#;}' KNN_GATE_N=$GN KNN_GATE_M=$GM KNN_GATE_D=$GD KNN_GATE_K=$GK"
+}
+run_gate() {  # $1 variant library ("base" = default), $2 tune.py arguments
+  [ "${GATE:-1}" = 0 ] && return 0
+  if [ $1 = base ]; then unset KNN_AMD_VARIANT; else export KNN_AMD_VARIANT=$1; fi
+  eval "$(gate_env "$2")" timeout -k 10 300 python -u -m pytest -x -q -m gpu --timeout 240 \
+      --timeout-method thread tests/test_gpu_gate.py -s > $O/${TAG}_gate_$1.log 2>&1
+  local rc=$?; echo "gate $1 rc=$rc"; grep "^gate " $O/${TAG}_gate_$1.log
+  unset KNN_AMD_VARIANT
+  return $rc
+}
 if [ -n "$AB_VARIANTS" ]; then
+  for v in $AB_VARIANTS; do run_gate $v "$AB_ARGS" || exit 1; done
   for rep in $(seq 1 ${REPS:-2}); do
     for v in $AB_VARIANTS; do
       if [ $v = base ]; then unset KNN_AMD_VARIANT; else export KNN_AMD_VARIANT=$v; fi
@@ -45,6 +84,7 @@ if [ -n "$AB_SETS" ]; then
     IFS=';' read -ra sets <<< "$AB_SETS"
     for a in "${sets[@]}"; do
       i=$((i + 1))
+      [ $rep = 1 ] && { run_gate base "$a" || exit 1; }
       timeout -k 10 300 python3 -u tools/tune.py $a > $O/${TAG}_set${i}_$rep.log 2>&1
       rc=$?; echo "set $i ($a) $rep rc=$rc"; grep " cand " $O/${TAG}_set${i}_$rep.log
       [ $rc = 0 ] || exit $rc
@@ -77,5 +117,8 @@ if [ -n "$PROF" ]; then
       python3 -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-fp32-path --no-continuous --no-dropin --no-train-sharded --cfg3-queries 0 > $O/${TAG}_prof.log 2>&1
   rc=$?; echo "prof rc=$rc"
   [ $rc = 0 ] || exit $rc
+fi
+if [ -n "$PROF_PARTS" ]; then
+  TAG=$TAG PART="$PROF_PARTS" bash tools/prof_round.sh || exit $?
 fi
 exit 0

@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round-5 evidence, each step its own time limit (a failing step ends the call):
+# Profiling evidence of one build (any round; TAG names it), each step its own
+# time limit (a failing step ends the call):
 #   PART=A  kernel trace + stats of cfg2 / cfg4s (12.5M x 96 shard) / cfg5 and
 #           of the general-data kernels (cfg2c: fp16 on continuous data,
 #           cfg2f32: the fp32 path); HIP API trace of cfg2
@@ -11,11 +12,12 @@
 # tools/profiles_commit.py --tag $TAG turns them into profiles/.
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-TAG=${TAG:-r5}
+TAG=${TAG:-prof}
 export TAG
 OUT=$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
-case "$PART" in
+for part in ${PART:-A}; do
+case "$part" in
   A) bash tools/profile_all.sh stats api cfg4s cfg5 cfg2c cfg2f32 || exit $? ;;
   R) timeout -k 10 300 rocprofv3 --rccl-trace --kernel-trace --stats -d "$OUT/rccl" -o run --output-format csv -- \
        python3 -m pytest -x -q -m gpu --timeout 200 tests/test_gpu_sharded.py -k True \
@@ -24,5 +26,9 @@ case "$PART" in
   B) bash tools/profile_all.sh pmc cfg4s cfg5 cfg2c cfg2f32 || exit $? ;;
   S) bash tools/pmc_sq2.sh || exit $?
      TAG=${TAG}_cfg4s WLARGS="--steps 3 --warmup 1 --mode train --n-train 12500000 --dim 96 --queries 10000" \
-       bash tools/pmc_sq2.sh || exit $? ;;
+       bash tools/pmc_sq2.sh || exit $?
+     TAG=${TAG}_cfg2c WLARGS="--steps 3 --warmup 1 --data continuous" bash tools/pmc_sq2.sh || exit $?
+     TAG=${TAG}_cfg5 WLARGS="--steps 2 --warmup 1 --dim 960 --k 100" bash tools/pmc_sq2.sh || exit $? ;;
+  *) echo "unknown PART $part"; exit 2 ;;
 esac
+done

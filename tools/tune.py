@@ -8,7 +8,17 @@ Variants: "prec:R:S[:ablate[:nw]]" e.g. auto:0:0 fp32:8:0 auto:8:0:1:8
 (ablate bits: 1 = no staging loads, 2 = no selection epilogue; timing only;
 nw = waves per candidate workgroup, 0 auto / 4 / 8)
 Extra tuning keys after a comma, e.g. "fp16:0:0,mfma16=1" (keys listed in
-`defaults` and not named by a variant are reset to automatic)."""
+`defaults` and not named by a variant are reset to automatic).
+
+Parity gate (before any time is logged): the first call of every variant
+returns its neighbour distances, and --gate queries (default 256, spread over
+the batch) must hold the k smallest distances over ALL train rows (the
+independent fp64 brute force of tests/test_gpu_fullsize.py) and every label
+must equal the first variant's; a variant that fails exits non-zero with no
+timing line.  (The oracle half of the gate -- 8 queries bit for bit -- is
+tests/test_gpu_gate.py, which tools/gpu_round.sh runs on every library
+variant before its A/B.)  Round 5's r5ai variant, which skipped query loads,
+would have stopped here instead of being logged as a gain."""
 import argparse
 import ctypes
 import os
@@ -19,7 +29,37 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
 import bench  # noqa: E402
+from test_gpu_fullsize import brute_force_kdist  # noqa: E402  (torch fp64 GEMM, not the oracle)
+
+DEFAULTS = {"gk": -1, "s3q": -1, "xhswz": 1, "i8": -1, "i8w": -1, "seed": 0, "ophase": -1, "s3gq": 0,
+            "gg": -1, "qblk": 0}
+
+
+def apply_variant(knn, clf, v):
+    """Set a variant string's precision and tuning keys on clf; returns its
+    ablation bits."""
+    prec = {"auto": knn.PRECISION_AUTO, "fp32": knn.PRECISION_FP32, "bf16x3": knn.PRECISION_BF16X3,
+            "m16": knn.PRECISION_BF16X3, "fp16": knn.PRECISION_FP16}
+    base, *extra = v.split(",")
+    kv = dict(DEFAULTS)
+    for e in extra:
+        key, val = e.split("=")
+        kv[key] = int(val)
+    for key, val in kv.items():
+        clf.set_tuning(key, val)
+    parts = base.split(":")
+    p, R, S = parts[:3]
+    abl = int(parts[3]) if len(parts) > 3 else 0
+    nw = int(parts[4]) if len(parts) > 4 else 0
+    clf.set_tuning("nw", nw)
+    clf.set_precision(prec[p])
+    clf.set_tuning("mfma16", 1 if p == "m16" else (0 if p == "bf16x3" else -1))
+    clf.set_tuning("R", int(R))
+    clf.set_tuning("S", int(S))
+    clf.set_tuning("ablate", abl)
+    return abl
 
 
 def main():
@@ -34,6 +74,8 @@ def main():
                     help="region order of the train layout (tuning key 'order', set before set_train)")
     ap.add_argument("--nblk", type=int, default=-1,
                     help="norm blocks of the train layout (tuning key 'nblk', set before set_train)")
+    ap.add_argument("--gate", type=int, default=256,
+                    help="queries checked for optimality per variant before timing (0: off)")
     ap.add_argument("variants", nargs="*", default=["auto:0:0", "auto:4:0", "auto:8:0", "fp32:0:0"])
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -57,41 +99,43 @@ def main():
         cnt_fn = None
     selc = {}
     cbuf = (ctypes.c_ulonglong * 8)()
-    prec = {"auto": knn.PRECISION_AUTO, "fp32": knn.PRECISION_FP32, "bf16x3": knn.PRECISION_BF16X3,
-            "m16": knn.PRECISION_BF16X3, "fp16": knn.PRECISION_FP16}
-    defaults = {"gk": -1, "s3q": -1, "xhswz": 1, "i8": -1, "i8w": -1, "seed": 0, "ophase": -1, "s3gq": 0,
-                "gg": -1, "qblk": 0}
+    gq = np.unique(np.linspace(0, a.m - 1, min(a.gate, a.m)).astype(np.int64)) if a.gate > 0 else None
+    idx = torch.empty((a.m, a.k), dtype=torch.int64, device=dev)
+    dist = torch.empty((a.m, a.k), dtype=torch.float64, device=dev)
+    bf = None
     for r in range(a.rounds + 1):
         for v in a.variants:
-            base, *extra = v.split(",")
-            kv = dict(defaults)
-            for e in extra:
-                key, val = e.split("=")
-                kv[key] = int(val)
-            for key, val in kv.items():
-                clf.set_tuning(key, val)
-            parts = base.split(":")
-            p, R, S = parts[:3]
-            abl = int(parts[3]) if len(parts) > 3 else 0
-            nw = int(parts[4]) if len(parts) > 4 else 0
-            clf.set_tuning("nw", nw)
-            clf.set_precision(prec[p])
-            clf.set_tuning("mfma16", 1 if p == "m16" else (0 if p == "bf16x3" else -1))
-            clf.set_tuning("R", int(R))
-            clf.set_tuning("S", int(S))
-            clf.set_tuning("ablate", abl)
+            abl = apply_variant(knn, clf, v)
             if cnt_fn is not None:
                 cnt_fn(cbuf, 1)
-            clf.classify_device(Q.data_ptr(), a.m, a.k, knn.L2, out.data_ptr())
+            if r == 0 and gq is not None:
+                clf.classify_device(Q.data_ptr(), a.m, a.k, knn.L2, out.data_ptr(), idx.data_ptr(),
+                                    dist.data_ptr())
+            else:
+                clf.classify_device(Q.data_ptr(), a.m, a.k, knn.L2, out.data_ptr())
             clf.sync()
+            if r == 0 and gq is not None and not (abl & 27):
+                # parity gate (timing-only ablations, bits 1/2/8/16, give invalid results)
+                if bf is None:
+                    bf = brute_force_kdist(X, Q[gq], a.k)
+                got = dist.cpu().numpy()[gq]
+                bad = np.nonzero(~np.isclose(got, bf, rtol=1e-10, atol=0).all(1))[0]
+                if bad.size or (ref is not None and not torch.equal(ref, out)):
+                    print("PARITY GATE FAILED for %s: %d of %d gate queries miss a true neighbour "
+                          "(e.g. query %s), labels equal to the first variant: %s" %
+                          (v, bad.size, gq.size, gq[bad[:4]], ref is None or bool(torch.equal(ref, out))))
+                    sys.exit(3)
+                print("parity gate %s: %d queries optimal, labels %s" %
+                      (v, gq.size, "reference" if ref is None else "= first variant"))
             if cnt_fn is not None and r > 0:
                 cnt_fn(cbuf, 1)
                 if any(cbuf):
                     selc[v] = list(cbuf)
             if r == 0:
-                if ref is None:
+                if ref is None and not (abl & 27):
                     ref = out.clone()
-                info[v] = (clf.last_geometry(), clf.last_rescan_count(), bool(torch.equal(ref, out)))
+                info[v] = (clf.last_geometry(), clf.last_rescan_count(),
+                           ref is not None and bool(torch.equal(ref, out)))
                 continue
             res[v].append(clf.last_phase_ms(knn.PHASE_CANDIDATE))
             tot.setdefault(v, []).append(sum(clf.last_phase_ms(p) for p in range(4)))
