@@ -104,6 +104,17 @@ static_assert(KNN_RES_TPB * knnk::kTR == knnk::kResTileRows || KNN_RES_TPB != 2,
 #ifndef KNN_SLOWPRIO
 #define KNN_SLOWPRIO 2
 #endif
+// metric 6: waves NW/2 .. NW-1 walk a staged tile's sub-tiles rotated by
+// TPB/2 (a stagger, MI355X_MICROARCH.md "Two waves per SIMD" item 9): the
+// two halves' LDS bursts and selection slow paths then fall on different
+// sub-tiles instead of in lockstep
+#ifndef KNN_STAGGER
+#define KNN_STAGGER 0
+#endif
+// metric 6: the no-candidate test's max over 16 values as 7 v_max3 + 1 v_max
+#ifndef KNN_MAX3T
+#define KNN_MAX3T 0
+#endif
 
 
 namespace knnk {
@@ -259,6 +270,8 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int j = lane & 31, h = lane >> 5;
+  // (KNN_STAGGER: this wave's sub-tile rotation, wave-uniform)
+  const int rot = (KNN_STAGGER && METRIC == 6 && wv >= NW / 2) ? res_tpb<METRIC>() / 2 : 0;
   const int64_t qg = (int64_t)qt * (NW * 32) + wv * 32 + j;
   const float* qrow = Q32 + qg * DP;
   // METRIC 3 (bf16x3 on 16x16x32) and 4 (fp16 on 16x16x32): lane l holds
@@ -490,8 +503,15 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   };
   auto sel6 = [&](const auto& a, int row0, int smx, auto&& sd) {  // a: i32x16
    if constexpr (SMX && I8W) {
+#if KNN_MAX3T
+    // (each max(max(x, y), z) is one v_max3_i32)
+    auto m3 = [](int x, int y, int z) { return max(max(x, y), z); };
+    const int mx = max(m3(m3(a[0], a[1], a[2]), m3(a[3], a[4], a[5]), m3(a[6], a[7], a[8])),
+                       m3(m3(a[9], a[10], a[11]), m3(a[12], a[13], a[14]), a[15]));
+#else
     const int mx = max(max(max(max(a[0], a[1]), max(a[2], a[3])), max(max(a[4], a[5]), max(a[6], a[7]))),
                        max(max(max(a[8], a[9]), max(a[10], a[11])), max(max(a[12], a[13]), max(a[14], a[15]))));
+#endif
 #if KNN_COUNT_SEL
     selc.bcalls++;
     selc.bpass += __builtin_amdgcn_ballot_w64(mx > tn[0] - smx) != 0;
@@ -702,15 +722,19 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
     if constexpr (SMX) {
 #pragma unroll
       for (int u = 0; u < TPB / 4; ++u) {
+        const int uu = rot ? (u + rot / 4) % (TPB / 4) : u;  // (KNN_STAGGER: rotated with the sub-tiles)
         const i32x4 v = __builtin_bit_cast(
-            i32x4, *(const float4*)(lds + cur * BUFF + (128 * u + kI8SmaxRow) * RSF + SEED));
+            i32x4, *(const float4*)(lds + cur * BUFF + (128 * uu + kI8SmaxRow) * RSF + SEED));
 #pragma unroll
         for (int e = 0; e < 4; ++e) smt[4 * u + e] = __builtin_amdgcn_readfirstlane(v[e]);
       }
     }
 #pragma unroll
     for (int sub = 0; sub < TPB; ++sub) {
-    const float* base = lds + cur * BUFF + sub * kTR * RSF;
+    // ps: the staged sub-tile processed at step sub (KNN_STAGGER rotates it)
+    const int ps = I8W && KNN_STAGGER ? (sub + rot) & (TPB - 1) : sub;
+    const float* base = lds + cur * BUFF + ps * kTR * RSF;
+    const float* base_prev = lds + cur * BUFF + ((I8W && KNN_STAGGER ? (sub - 1 + rot) & (TPB - 1) : sub - 1)) * kTR * RSF;
 
     if constexpr (I8W) {
       // int8 codes on v_mfma_i32_32x32x32_i8, exact: lane (j, h) holds query
@@ -745,13 +769,13 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       for (int ks = 0; ks < DP / 32; ++ks)
         acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[ks], __builtin_bit_cast(i32x4, qf[ks]),
                                                     SMX && ks == 0 ? i32x16{} : acc, 0, 0, 0);
-      const int row0 = (t * TPB + sub) * kTR + 4 * h;
+      const int row0 = (t * TPB + ps) * kTR + 4 * h;
       if constexpr (SMX) {
         // the pending sub-tile's selection after this one's MFMAs (seeds of
         // the previous staged tile's last sub-tile from spre)
         if (!(abl & 2)) {
           if constexpr (PIPE) {
-            if (sub > 0) sel6(accw, rowp, smxp, [&](int c) { return seed_lds(base - kTR * RSF, c); });
+            if (sub > 0) sel6(accw, rowp, smxp, [&](int c) { return seed_lds(base_prev, c); });
             else sel6(accw, rowp, smxp, [&](int c) { return spre[c]; });
             accw = acc;
             rowp = row0;

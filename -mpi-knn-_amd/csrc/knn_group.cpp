@@ -24,6 +24,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -65,12 +66,20 @@ struct knn_group {
     if (e_ != hipSuccess)                                                                 \
       return knn_fail(KNN_ERR_DEVICE, std::string(#expr " failed: ") + hipGetErrorString(e_)); \
   } while (0)
-#define NCCL_G(expr)                                                                      \
+// An RCCL failure names the call, the collective it belongs to and the ranks
+// (and devices) involved: a G > 1 failure on the first multi-GPU run must be
+// attributable from its message alone (the driver exits 1 with it).
+#define NCCL_G(expr) NCCL_AT(expr, std::string())
+#define NCCL_AT(expr, where)                                                              \
   do {                                                                                    \
     ncclResult_t r_ = (expr);                                                             \
     if (r_ != ncclSuccess)                                                                \
-      return knn_fail(KNN_ERR_COMM, std::string(#expr " failed: ") + ncclGetErrorString(r_)); \
+      return knn_fail(KNN_ERR_COMM, std::string(#expr " failed") + (where) + ": " +      \
+                                        ncclGetErrorString(r_));                           \
   } while (0)
+
+// " in <what>, rank i (device d) of G" / " in <what>, ranks 0..G-1 (devices ...)"
+static std::string ranks_of(const knn_group* g, const char* what, int i = -1);
 
 // Runs f(g) for every device in its own host thread; first non-zero rc wins.
 template <class F>
@@ -91,6 +100,69 @@ static int for_each_dev(knn_group* g, F f) {
 }
 
 static hipStream_t stream_of(knn_group* g, int i) { return g->ctx[i]->stream; }
+
+// Waits for rank i's stream.  With RCCL the wait polls: an asynchronous RCCL
+// error on any rank, or no progress within KNN_GROUP_TIMEOUT_S seconds
+// (default 600), aborts the communicators and fails naming the step and the
+// rank -- a hang of a G > 1 collective ends the driver (exit 1) instead of
+// holding the GPUs.
+static int sync_rank(knn_group* g, int i, const char* what) {
+  if (hipSetDevice(g->devs[i]) != hipSuccess)
+    return knn_fail(KNN_ERR_DEVICE, std::string("hipSetDevice failed") + ranks_of(g, what, i));
+  hipStream_t st = stream_of(g, i);
+  if (g->transport != XPORT_RCCL) {
+    hipError_t e = hipStreamSynchronize(st);
+    if (e != hipSuccess)
+      return knn_fail(KNN_ERR_DEVICE, std::string("stream of ") + ranks_of(g, what, i).substr(4) +
+                                          " failed: " + hipGetErrorString(e));
+    return KNN_OK;
+  }
+  static const double limit = [] {
+    const char* e = getenv("KNN_GROUP_TIMEOUT_S");
+    const double v = e ? atof(e) : 0.0;
+    return v > 0 ? v : 600.0;
+  }();
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int polls = 0;; ++polls) {
+    hipError_t e = hipStreamQuery(st);
+    if (e == hipSuccess) return KNN_OK;
+    if (e != hipErrorNotReady)
+      return knn_fail(KNN_ERR_DEVICE, std::string("stream of ") + ranks_of(g, what, i).substr(4) +
+                                          " failed: " + hipGetErrorString(e));
+    for (int r = 0; r < g->ndev; r++) {
+      ncclResult_t ae = ncclSuccess;
+      if (g->comms[r] && ncclCommGetAsyncError(g->comms[r], &ae) == ncclSuccess &&
+          ae != ncclSuccess && ae != ncclInProgress) {
+        for (auto c : g->comms)
+          if (c) ncclCommAbort(c);
+        g->comms.assign(g->ndev, nullptr);
+        return knn_fail(KNN_ERR_COMM, std::string("RCCL asynchronous error") + ranks_of(g, what, r) +
+                                          ": " + ncclGetErrorString(ae));
+      }
+    }
+    const double el =
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (el > limit) {
+      for (auto c : g->comms)
+        if (c) ncclCommAbort(c);
+      g->comms.assign(g->ndev, nullptr);
+      return knn_fail(KNN_ERR_COMM, "no progress for " + std::to_string((int)el) +
+                                        " s waiting for" + ranks_of(g, what, i).substr(3) +
+                                        " (communicators aborted; KNN_GROUP_TIMEOUT_S)");
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(polls < 1000 ? 20 : 200));
+  }
+}
+
+static std::string ranks_of(const knn_group* g, const char* what, int i) {
+  std::string s = std::string(" in ") + what + ", ";
+  if (i >= 0)
+    return s + "rank " + std::to_string(i) + " (device " + std::to_string(g->devs[i]) + ") of " +
+           std::to_string(g->ndev);
+  s += "ranks 0.." + std::to_string(g->ndev - 1) + " (devices";
+  for (int d : g->devs) s += " " + std::to_string(d);
+  return s + ")";
+}
 
 // ---- collectives of the group (one call covers every rank)
 
@@ -114,10 +186,11 @@ static int lb_barrier(knn_group* g) {
 static int coll_bcast(knn_group* g, const std::vector<void*>& buf, size_t count,
                       ncclDataType_t type, size_t esize, int root) {
   if (g->transport == XPORT_RCCL) {
-    NCCL_G(ncclGroupStart());
+    NCCL_AT(ncclGroupStart(), ranks_of(g, "broadcast"));
     for (int i = 0; i < g->ndev; i++)
-      NCCL_G(ncclBroadcast(buf[root], buf[i], count, type, root, g->comms[i], stream_of(g, i)));
-    NCCL_G(ncclGroupEnd());
+      NCCL_AT(ncclBroadcast(buf[root], buf[i], count, type, root, g->comms[i], stream_of(g, i)),
+              ranks_of(g, "broadcast", i));
+    NCCL_AT(ncclGroupEnd(), ranks_of(g, "broadcast"));
   } else if (g->transport == XPORT_LOOPBACK) {
     int rc;
     if ((rc = lb_barrier(g))) return rc;
@@ -136,10 +209,11 @@ static int coll_bcast(knn_group* g, const std::vector<void*>& buf, size_t count,
 static int coll_allgather(knn_group* g, const std::vector<void*>& send,
                           const std::vector<void*>& recv, size_t bytes) {
   if (g->transport == XPORT_RCCL) {
-    NCCL_G(ncclGroupStart());
+    NCCL_AT(ncclGroupStart(), ranks_of(g, "all-gather"));
     for (int i = 0; i < g->ndev; i++)
-      NCCL_G(ncclAllGather(send[i], recv[i], bytes, ncclUint8, g->comms[i], stream_of(g, i)));
-    NCCL_G(ncclGroupEnd());
+      NCCL_AT(ncclAllGather(send[i], recv[i], bytes, ncclUint8, g->comms[i], stream_of(g, i)),
+              ranks_of(g, "all-gather", i));
+    NCCL_AT(ncclGroupEnd(), ranks_of(g, "all-gather"));
   } else if (g->transport == XPORT_LOOPBACK) {
     int rc;
     if ((rc = lb_barrier(g))) return rc;
@@ -158,13 +232,15 @@ static int coll_allgather(knn_group* g, const std::vector<void*>& send,
 // rest (≙ the two MPI_Allreduce of cpp:276-277)
 static int coll_allreduce_maxmin(knn_group* g, const std::vector<double*>& mm, int d) {
   if (g->transport == XPORT_RCCL) {
-    NCCL_G(ncclGroupStart());
+    NCCL_AT(ncclGroupStart(), ranks_of(g, "normalisation all-reduce"));
     for (int i = 0; i < g->ndev; i++) {
-      NCCL_G(ncclAllReduce(mm[i], mm[i], d, ncclFloat64, ncclMax, g->comms[i], stream_of(g, i)));
-      NCCL_G(ncclAllReduce(mm[i] + d, mm[i] + d, d, ncclFloat64, ncclMin, g->comms[i],
-                           stream_of(g, i)));
+      NCCL_AT(ncclAllReduce(mm[i], mm[i], d, ncclFloat64, ncclMax, g->comms[i], stream_of(g, i)),
+              ranks_of(g, "normalisation all-reduce (MAX)", i));
+      NCCL_AT(ncclAllReduce(mm[i] + d, mm[i] + d, d, ncclFloat64, ncclMin, g->comms[i],
+                            stream_of(g, i)),
+              ranks_of(g, "normalisation all-reduce (MIN)", i));
     }
-    NCCL_G(ncclGroupEnd());
+    NCCL_AT(ncclGroupEnd(), ranks_of(g, "normalisation all-reduce"));
   } else if (g->transport == XPORT_LOOPBACK) {
     // (test transport) folded on the host in rank order with strict compares
     std::vector<double> acc((size_t)2 * d), v((size_t)2 * d);
@@ -209,17 +285,19 @@ static int coll_alltoallv(knn_group* g, const std::vector<double*>& send,
   // the one-rank communicator of KNN_GROUP_RCCL then runs this exchange's
   // ncclSend / ncclRecv on a single GPU)
   if (g->transport == XPORT_RCCL) {
-    NCCL_G(ncclGroupStart());
+    NCCL_AT(ncclGroupStart(), ranks_of(g, "tie all-to-all"));
     for (int a = 0; a < G; a++)
       for (int b = 0; b < G; b++) {
         if (cnt[a][b] > 0)
-          NCCL_G(ncclSend(send[a] + soff[a][b], (size_t)cnt[a][b], ncclFloat64, b, g->comms[a],
-                          stream_of(g, a)));
+          NCCL_AT(ncclSend(send[a] + soff[a][b], (size_t)cnt[a][b], ncclFloat64, b, g->comms[a],
+                           stream_of(g, a)),
+                  ranks_of(g, ("tie all-to-all, to rank " + std::to_string(b)).c_str(), a));
         if (cnt[b][a] > 0)
-          NCCL_G(ncclRecv(recv[a] + roff[a][b], (size_t)cnt[b][a], ncclFloat64, b, g->comms[a],
-                          stream_of(g, a)));
+          NCCL_AT(ncclRecv(recv[a] + roff[a][b], (size_t)cnt[b][a], ncclFloat64, b, g->comms[a],
+                           stream_of(g, a)),
+                  ranks_of(g, ("tie all-to-all, from rank " + std::to_string(b)).c_str(), a));
       }
-    NCCL_G(ncclGroupEnd());
+    NCCL_AT(ncclGroupEnd(), ranks_of(g, "tie all-to-all"));
   }
   if (g->transport == XPORT_LOOPBACK) return lb_barrier(g);
   return KNN_OK;
@@ -257,7 +335,10 @@ int knn_group_create(knn_group** out, int ndev, const int* devs, int mode) {
     if (r != ncclSuccess) {
       g->comms.clear();
       knn_group_destroy(g);
-      return knn_fail(KNN_ERR_COMM, std::string("ncclCommInitAll failed: ") + ncclGetErrorString(r));
+      std::string devl;
+      for (int i = 0; i < ndev; i++) devl += " " + std::to_string(devs ? devs[i] : i);
+      return knn_fail(KNN_ERR_COMM, "ncclCommInitAll over ranks 0.." + std::to_string(ndev - 1) +
+                                        " (devices" + devl + ") failed: " + ncclGetErrorString(r));
     }
   }
   for (auto* v : {&g->X, &g->lab, &g->labA, &g->Q, &g->olab, &g->oidx, &g->odist, &g->oflags,
@@ -354,6 +435,8 @@ int knn_group_set_train(knn_group* g, const double* X, const int32_t* labels, in
     int rc;
     if ((rc = coll_bcast(g, xb, (size_t)n * d, ncclFloat64, 8, 0))) return rc;
     if ((rc = coll_bcast(g, lb, (size_t)n, ncclInt32, 4, 0))) return rc;
+    for (int i = 0; i < G; i++)  // (the watchdog: a hung broadcast fails here, naming the rank)
+      if ((rc = sync_rank(g, i, "train broadcast"))) return rc;
     rc = for_each_dev(g, [&](int i) {
       return knn_set_train_device(g->ctx[i], (const double*)g->X[i].p,
                                   (const int32_t*)g->lab[i].p, n, d, class_cnt, 0);
@@ -397,6 +480,7 @@ int knn_group_set_train(knn_group* g, const double* X, const int32_t* labels, in
 // distances to its rows, an all-to-all moves each owner's blocks to it, and
 // the owner re-sorts and votes (knn_tie_resolve_device).
 static int resolve_ties(knn_group* g, int64_t m, int k, int metric) {
+  int rc;
   const int G = g->ndev;
   const int64_t n = g->n;
   g->last_ties = 0;
@@ -409,7 +493,7 @@ static int resolve_ties(knn_group* g, int64_t m, int k, int metric) {
   int64_t total = 0;
   for (int i = 0; i < G; i++) {
     HIP_G(hipSetDevice(g->devs[i]));
-    HIP_G(hipStreamSynchronize(stream_of(g, i)));
+    if ((rc = sync_rank(g, i, "tie exchange (counts)"))) return rc;
     total += hc[i];
   }
   if (total == 0) return KNN_OK;
@@ -429,7 +513,6 @@ static int resolve_ties(knn_group* g, int64_t m, int k, int metric) {
   // queries per batch: the owner receives up to B x n distances (<= 1 GB)
   const int64_t B = std::max<int64_t>(1, std::min<int64_t>(4096, (1ll << 30) / (8 * n)));
   std::vector<size_t> pos(G, 0);
-  int rc;
   while (true) {
     std::vector<int64_t> cnt(G, 0);
     std::vector<int> sel;
@@ -491,7 +574,7 @@ static int resolve_ties(knn_group* g, int64_t m, int k, int metric) {
     }
     for (int i = 0; i < G; i++) {  // the host lists of this batch are reused
       HIP_G(hipSetDevice(g->devs[i]));
-      HIP_G(hipStreamSynchronize(stream_of(g, i)));
+      if ((rc = sync_rank(g, i, "tie exchange (resolve)"))) return rc;
     }
     g->last_ties += Bt;
   }
@@ -537,7 +620,7 @@ int knn_group_classify(knn_group* g, const double* Q, int64_t m, int32_t k, int3
     double span = 0.0;
     for (int i = 0; i < G; i++) {
       HIP_G(hipSetDevice(g->devs[i]));
-      HIP_G(hipStreamSynchronize(g->ctx[i]->stream));
+      if (int e = sync_rank(g, i, "classify")) return e;
       float ms = 0.f;
       if (hipEventElapsedTime(&ms, g->ev0[i], g->ev1[i]) == hipSuccess)
         span = std::max(span, (double)ms * 1e-3);
@@ -720,6 +803,8 @@ int knn_group_normalize(knn_group* g, double* const* sets, const int64_t* rows, 
   std::vector<double*> mm(G);
   for (int i = 0; i < G; i++) mm[i] = (double*)g->nmm[i].p;
   if ((rc = coll_allreduce_maxmin(g, mm, d))) return rc;  // ≙ MPI_Allreduce, cpp:276-277
+  for (int i = 0; i < G; i++)
+    if ((rc = sync_rank(g, i, "normalisation all-reduce"))) return rc;
   return for_each_dev(g, [&](int i) {  // cpp:279-305 on each shard, back to the host
     knn_ctx* c = g->ctx[i];
     const double* mx = (const double*)g->nmm[i].p;

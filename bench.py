@@ -38,6 +38,8 @@ import socket
 import subprocess
 import sys
 import time
+import traceback
+from datetime import timedelta
 
 import numpy as np
 import torch
@@ -56,6 +58,56 @@ def peak_of(path):
             5: PEAK_I8_TOPS, 6: PEAK_I8_TOPS}.get(path, PEAK_FP32_TFLOPS)
 METRIC = "queries/sec (node) + % MFMA peak, 1M train x 10k query d=128 k=10, 1/2/4/8 GPU"
 REF_SAMPLE = 512  # queries the reference program classifies in the bench's baseline leg
+
+
+PHASE = ["start"]  # what this rank is doing (named in a failure report)
+
+
+def phase(name):
+    PHASE[0] = name
+    log("phase: %s" % name)
+
+
+def _world():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(), dist.get_rank()
+    return 1, 0
+
+
+def gather_per_rank(vals, dev=None):
+    """This rank's numbers -> one list per rank (rank order), on every rank."""
+    world, _ = _world()
+    t = torch.tensor([float(v) for v in vals], dtype=torch.float64, device=dev)
+    if world == 1:
+        return [t.tolist()]
+    out = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [o.tolist() for o in out]
+
+
+def labels_sha1(t):
+    return hashlib.sha1(t.detach().to("cpu").to(torch.int32).numpy().tobytes()).hexdigest()
+
+
+def per_rank_report(dev, fields, labels=None):
+    """{field: [value of rank 0, rank 1, ...]} for the N-GPU line (every rank
+    must call it); labels: this rank's label slice, reported as one sha1 per
+    rank (the 1-GPU line's rank-0 sha1 is comparable with every N's: rank r
+    classifies the same query rows at every N)."""
+    names = list(fields)
+    vals = gather_per_rank([fields[k] for k in names], dev)
+    out = {k: [v[i] for v in vals] for i, k in enumerate(names)}
+    if labels is not None:
+        h = hashlib.sha1(labels.detach().to("cpu").to(torch.int32).numpy().tobytes()).digest()
+        ht = torch.tensor(list(h), dtype=torch.uint8, device=dev)
+        world, _ = _world()
+        if world > 1:
+            parts = [torch.empty_like(ht) for _ in range(world)]
+            dist.all_gather(parts, ht)
+        else:
+            parts = [ht]
+        out["labels_sha1"] = [bytes(p.cpu().tolist()).hex() for p in parts]
+    return out
 
 
 def log(*a):
@@ -86,29 +138,29 @@ def _grid(x, lo, hi):
 
 
 CHUNK = 1 << 20  # rows per generator chunk (a chunk's values depend only on its index)
+QCHUNK = 1 << 13  # the query sets' chunk: rank r's queries at every N (rows r m .. (r+1) m)
 
 
-def _rows(centres, n, row0, seed, device, classes, n_total=None):
-    """Rows [row0, row0+n) of a virtual Gaussian-mixture set of n_total rows
-    (default row0 + n), raw (unscaled) fp64, generated by global chunks of
-    CHUNK rows whose values depend only on the chunk's index: any shard of
-    the set is reproduced exactly whatever the shard boundaries (a shard
-    starting or ending inside a chunk generates that chunk and keeps its
-    part)."""
+def _rows(centres, n, row0, seed, device, classes, n_total=None, chunk=CHUNK):
+    """Rows [row0, row0+n) of a virtual Gaussian-mixture set, raw (unscaled)
+    fp64, generated by global chunks of `chunk` rows whose values depend only
+    on the chunk's index: every chunk draws all its `chunk` rows, whatever
+    n_total, so any shard of the set -- and any prefix, e.g. rank 0's queries
+    at 1 and at 8 GPUs -- is reproduced exactly whatever the shard boundaries
+    (a shard starting or ending inside a chunk generates that chunk and keeps
+    its part).  n_total is accepted for the callers' bookkeeping only."""
     d = centres.shape[1]
-    n_total = row0 + n if n_total is None else n_total
     X = torch.empty((n, d), device=device, dtype=torch.float64)
     lab = torch.empty(n, device=device, dtype=torch.int32)
-    for ci in range(row0 // CHUNK, (row0 + n + CHUNK - 1) // CHUNK):
-        g0 = ci * CHUNK                       # the chunk's global rows [g0, g1)
-        g1 = min(n_total, g0 + CHUNK)
-        a, b = max(row0, g0), min(row0 + n, g1)
+    for ci in range(row0 // chunk, (row0 + n + chunk - 1) // chunk):
+        g0 = ci * chunk                       # the chunk's global rows [g0, g0 + chunk)
+        a, b = max(row0, g0), min(row0 + n, g0 + chunk)
         if a >= b:
             continue
         gc = torch.Generator(device=device)
         gc.manual_seed(seed * 1000003 + ci)
-        lc = torch.randint(0, classes, (g1 - g0,), generator=gc, device=device, dtype=torch.int32)
-        xc = torch.randn((g1 - g0, d), generator=gc, device=device, dtype=torch.float64)
+        lc = torch.randint(0, classes, (chunk,), generator=gc, device=device, dtype=torch.int32)
+        xc = torch.randn((chunk, d), generator=gc, device=device, dtype=torch.float64)
         X[a - row0:b - row0] = centres[lc[a - g0:b - g0].long()] + xc[a - g0:b - g0]
         lab[a - row0:b - row0] = lc[a - g0:b - g0]
         del xc
@@ -158,7 +210,7 @@ def synth(n, m, d, classes, seed_train, seed_query, device, row0=0, n_total=None
     g.manual_seed(seed_train)
     centres = torch.rand((classes, d), generator=g, device=device, dtype=torch.float64) * 4 - 2
     X, lab = _rows(centres, n, row0, seed_train, device, classes, n_total)
-    Q, qlab = _rows(centres, m, q0, seed_query, device, classes, q_total)
+    Q, qlab = _rows(centres, m, q0, seed_query, device, classes, q_total, chunk=QCHUNK)
     if data == "grid":
         lo, hi = -2.0 - 4.5, 2.0 + 4.5  # fixed scale (centres in [-2,2] + N(0,1) tails)
         for s in (X, Q):
@@ -746,9 +798,10 @@ def train_sharded_leg(args, kd, knn, world, rank, local, dev, sync):
     flg = kd.gather_slices(o_flg[:q1 - q0], m, dev)
     sample = torch.arange(0, m, max(1, m // 64), device=dev)
     chk = verify_train_sharded(kd, X, lab, r0, r1, Q, k, got, idx, dst, sample, world)
-    kms = torch.tensor([r["t_cand"]], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(kms, op=dist.ReduceOp.MAX)
+    pr = per_rank_report(dev, {"kernel_ms": r["t_cand"] * 1e3, "rescanned_queries": r["resc"],
+                               "tie_resolved_queries": ties.resolved,
+                               "tie_pending_queries": int(((o_flg[:q1 - q0] & ties.FLAG_TIE_PENDING)
+                                                           != 0).sum().item())})
     flops = 2.0 * (r1 - r0) * d * m
     ach = flops / r["t_cand"] / 1e12
     out = {
@@ -757,7 +810,8 @@ def train_sharded_leg(args, kd, knn, world, rank, local, dev, sync):
                     % (n, world, r1 - r0, m, d, k, w),
         "value": m * steps / r["el"], "unit": "queries/s", "n_gpus": world, "steps": steps,
         "ms_per_step": r["el"] / steps * 1e3, "scaling": "strong",
-        "kernel": r["kernel"], "kernel_ms_max_over_ranks": float(kms.item()) * 1e3,
+        "kernel": r["kernel"], "kernel_ms_max_over_ranks": max(pr["kernel_ms"]),
+        "per_rank": pr, "labels_sha1": labels_sha1(got),
         "roofline_rank0": {"achieved": ach, "peak": peak_of(r["path"]), "unit": "TFLOP/s",
                            "frac": ach / peak_of(r["path"]), "candidate_path": r["path"]},
         "allgather_bytes_per_rank": (m * w * 20 + 15) // 16 * 16 if world > 1 else 0,
@@ -816,6 +870,23 @@ def cfg5_leg(args, kd, knn, dev, sync, stream):
 
 
 def main():
+    """Runs the bench; any failure on any rank exits non-zero naming the rank
+    and the phase it was in (a hung collective fails after the process
+    group's timeout, KNN_BENCH_COLL_TIMEOUT_S, default 600 s)."""
+    try:
+        _main()
+    except SystemExit:
+        raise
+    except BaseException as e:  # noqa: B902 -- report and exit 1 on anything
+        print("[bench.py] rank %s of %s FAILED in phase '%s': %s: %s"
+              % (os.environ.get("RANK", "0"), os.environ.get("WORLD_SIZE", "1"), PHASE[0],
+                 type(e).__name__, e), file=sys.stderr, flush=True)
+        traceback.print_exc()
+        sys.stderr.flush()
+        os._exit(1)
+
+
+def _main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -871,10 +942,13 @@ def main():
     dropin = None if args.no_dropin or args.mode != "query" else dropin_phase(
         world, rank, mnist=not args.no_mnist)
 
+    phase("device %d setup" % local)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        phase("init_process_group (nccl = RCCL) over %d ranks" % world)
+        dist.init_process_group("nccl", device_id=dev, timeout=timedelta(
+            seconds=float(os.environ.get("KNN_BENCH_COLL_TIMEOUT_S", "600"))))
     knn = load_knn()
     n, m, d, k, C = args.n_train, args.queries, args.dim, args.k, args.classes
     sync = torch.cuda.synchronize
@@ -891,10 +965,12 @@ def main():
     if args.mode == "query":
         # train generated on rank 0 and RCCL-broadcast (≙ MPI_Bcast cpp:224-225);
         # rank r's weak-scaling queries are rows [r m, (r+1) m) of one query set
+        phase("synthetic data (query mode)")
         X, lab, Q, _ = synth(n, m, d, C, 1234, 5678, dev, data=args.data, q0=rank * m,
                              reduce=allreduce_minmax, q_total=m * world)
         sync()
         if world > 1:
+            phase("train broadcast (RCCL, rank 0 -> all)")
             dist.barrier()
             sync()
             t0 = time.perf_counter()
@@ -906,6 +982,7 @@ def main():
             extra["train_broadcast_ms"] = float(bt.item()) * 1e3
             extra["train_broadcast_gbps"] = (X.numel() * 8 + lab.numel() * 4) / float(bt.item()) / 1e9
         log("synthetic train ready: %d rows x %d (%s data)" % (n, d, args.data))
+        phase("set_train (main leg)")
         t0 = time.perf_counter()
         clf.set_tuning("order", args.order)
         clf.set_train_device(X.data_ptr(), lab.data_ptr(), n, d, C, keep=(X, lab))
@@ -922,16 +999,21 @@ def main():
         flops = 2.0 * n * d * m  # algorithmic, per launch per GPU (norm terms excluded)
         prec_main = {"auto": knn.PRECISION_AUTO, "fp32": knn.PRECISION_FP32,
                      "fp16": knn.PRECISION_FP16}[args.precision]
+        phase("main leg (query-sharded, %d queries per rank)" % m)
         main_r = timed_run(kd, clf, step, args.steps, args.warmup, sync, dev, prec_main)
         clf.set_precision(knn.PRECISION_AUTO)
         log("default path done: %.3f ms/step" % (main_r["el"] / args.steps * 1e3))
         labels_auto = out_lab.clone()
         flags_auto = out_flags.clone()
         tie_vote = int(((flags_auto & knn.FLAG_TIE_VOTE) != 0).sum().item())
-        if world > 1:
-            tv = torch.tensor([tie_vote], dtype=torch.int64, device=dev)
-            dist.all_reduce(tv)
-            tie_vote = int(tv.item())
+        phase("main leg per-rank report")
+        pr = per_rank_report(dev, {"kernel_ms": main_r["t_cand"] * 1e3,
+                                   "rescanned_queries": main_r["resc"],
+                                   "tie_vote_queries": tie_vote,
+                                   "tie_reordered_queries": main_r["tie_reordered"]}, labels_auto)
+        extra["per_rank"] = pr
+        extra["labels_sha1_rank0"] = pr["labels_sha1"][0]
+        tie_vote = int(sum(pr["tie_vote_queries"]))
         extra["tie_vote_queries"] = tie_vote
         fp32_r = same = fp16_r = same16 = None
         if not args.no_fp32_path and world == 1:
@@ -970,6 +1052,7 @@ def main():
                                         None, flg3.data_ptr(), stream)
 
                 s3 = max(2, args.steps // 4)
+                phase("cfg3 strong-scaling leg (%d of %d queries)" % (q1 - q0, M))
                 r3 = timed_run(kd, clf, step3, s3, 1, sync, dev, knn.PRECISION_AUTO)
                 extra["cfg3_strong"] = {
                     "workload": "cfg3: %d train x %d queries in total split over %d GPU(s) "
@@ -984,6 +1067,12 @@ def main():
                 if world > 1:
                     dist.all_reduce(tv3)
                 extra["cfg3_strong"]["tie_vote_queries"] = int(tv3.item())
+                # every N classifies the same M queries: one sha1 of all M labels
+                all3 = kd.gather_slices(lab3, M, dev)
+                extra["cfg3_strong"]["labels_sha1"] = labels_sha1(all3)
+                extra["cfg3_strong"]["per_rank"] = per_rank_report(
+                    dev, {"kernel_ms": r3["t_cand"] * 1e3, "rescanned_queries": r3["resc"]})
+                del all3
                 log("cfg3 strong leg: %.1f ms/step" % (r3["el"] / s3 * 1e3))
                 del Q3, lab3, flg3
 
@@ -1077,6 +1166,7 @@ def main():
     ts = None
     if args.mode == "query" and not args.no_train_sharded:
         log("train-sharded leg: %d rows over %d rank(s) ..." % (args.ts_n_train, world))
+        phase("train-sharded leg (%d rows over %d ranks)" % (args.ts_n_train, world))
         ts = train_sharded_leg(args, kd, knn, world, rank, local, dev, sync)
         log("train-sharded leg: %.2f ms/step, labels_match %s" % (ts["ms_per_step"],
                                                                 ts["labels_match"]))
@@ -1257,7 +1347,9 @@ def dry_run(args, kd, world, rank):
     """Launcher + decomposition on CPU (gloo) with the torch stand-in: the
     line carries n_gpus and a checksum of the gathered labels, value null."""
     if world > 1:
+        phase("dry run: init_process_group (gloo) over %d ranks" % world)
         dist.init_process_group("gloo")
+    phase("dry run: synthetic data")
     n, m, d, k, C = args.n_train, args.queries, args.dim, args.k, args.classes
     cpu = torch.device("cpu")
     X, lab, Q, _ = synth(n, m * world, d, C, 1234, 5678, cpu, data=args.data)
@@ -1284,6 +1376,11 @@ def dry_run(args, kd, world, rank):
                                     Qa, m, w, k)
     ts_labels = kd.gather_slices(mine, m)
     ts_ok = bool(torch.equal(ts_labels, labels[:m]))
+    # the N-GPU line's per-rank fields, through the same code as the GPU run
+    pr = per_rank_report(None, {"kernel_ms": el / args.steps * 1e3, "rescanned_queries": 0,
+                                "tie_vote_queries": 0, "tie_reordered_queries": 0}, out["lab"])
+    ts_pr = per_rank_report(None, {"kernel_ms": 0.0, "rescanned_queries": 0,
+                                   "tie_resolved_queries": 0, "tie_pending_queries": 0})
     dropin = dropin_legs(world, shape=dict(n=3000, m=64, d=24, k=k, classes=min(C, 10)),
                          dry=True) if rank == 0 else None
     if rank == 0:
@@ -1291,8 +1388,10 @@ def dry_run(args, kd, world, rank):
             "group_query": dropin["group_query"], "group_train": dropin["group_train"],
             "dropin_inputs": dropin["inputs_written"],
             "train_sharded": {"value": None, "labels_match": ts_ok, "n_gpus": world,
+                              "per_rank": ts_pr, "labels_sha1": labels_sha1(ts_labels),
                               "workload": "dry-run: %d train rows over %d rank(s) x %d queries"
                                           % (n, world, m)},
+            "per_rank": pr, "labels_sha1_rank0": pr["labels_sha1"][0],
             "metric": METRIC, "value": None, "unit": "queries/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",

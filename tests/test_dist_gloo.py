@@ -243,3 +243,30 @@ def test_bench_launches_its_own_ranks():
     assert sorted(two["dropin_inputs"]) == ["mnist_test.csv", "mnist_train.csv",
                                             "mnist_validation.csv"]
     assert two["train_sharded"]["labels_match"] and one["train_sharded"]["labels_match"]
+    # the N-GPU line's self-checks: one entry per rank for the candidate
+    # kernel time, rescans and tie counts (main leg) and the tie resolutions
+    # (train-sharded leg); rank 0's label sha1 equals the 1-rank run over the
+    # same query rows; the train-sharded labels' sha1 is the same at every N
+    one48 = _bench_line(common + ["--gpus", "1", "--queries", "48"])
+    for key in ("kernel_ms", "rescanned_queries", "tie_vote_queries", "tie_reordered_queries",
+                "labels_sha1"):
+        assert len(two["per_rank"][key]) == 2 and len(one48["per_rank"][key]) == 1, key
+    assert two["per_rank"]["labels_sha1"][0] == one48["per_rank"]["labels_sha1"][0]
+    assert two["labels_sha1_rank0"] == one48["labels_sha1_rank0"]
+    assert two["per_rank"]["labels_sha1"][1] != two["per_rank"]["labels_sha1"][0]
+    for key in ("kernel_ms", "tie_resolved_queries", "tie_pending_queries"):
+        assert len(two["train_sharded"]["per_rank"][key]) == 2, key
+    assert two["train_sharded"]["labels_sha1"] == one48["train_sharded"]["labels_sha1"]
+
+
+def test_bench_failure_names_rank_and_phase():
+    """A failing rank exits non-zero and names itself and the phase it was in
+    (a negative --n-train makes the dry run's data generation fail)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--n-train",
+                          "-5", "--dim", "24", "--queries", "8", "--steps", "1", "--warmup", "0"],
+                         capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode != 0
+    assert "rank 0 of 1 FAILED in phase" in out.stderr, out.stderr[-1500:]
