@@ -111,6 +111,20 @@ static_assert(KNN_RES_TPB * knnk::kTR == knnk::kResTileRows || KNN_RES_TPB != 2,
 #ifndef KNN_STAGGER
 #define KNN_STAGGER 0
 #endif
+#ifndef KNN_STAGGER4
+#define KNN_STAGGER4 0
+#endif
+// metric 6: the exact seeds of a staged tile's last sub-tile (its selection
+// runs after the next tile's barrier, when the buffer may be refilled) are
+// read in the rare slow path from the image in HBM / L2 by wave-uniform
+// scalar loads (32 seeds per sub-tile, 8 x s_load_dwordx4) instead of being
+// held in 16 VGPRs from the sub-tile's LDS reads
+#ifndef KNN_SPRE_GLB
+#define KNN_SPRE_GLB 0
+#endif
+#ifndef KNN_I8W_PF
+#define KNN_I8W_PF 0
+#endif
 // metric 6: the no-candidate test's max over 16 values as 7 v_max3 + 1 v_max
 #ifndef KNN_MAX3T
 #define KNN_MAX3T 0
@@ -271,7 +285,9 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int j = lane & 31, h = lane >> 5;
   // (KNN_STAGGER: this wave's sub-tile rotation, wave-uniform)
-  const int rot = (KNN_STAGGER && METRIC == 6 && wv >= NW / 2) ? res_tpb<METRIC>() / 2 : 0;
+  // (KNN_STAGGER4: the same for the fp16 kernel, metric 4)
+  const int rot = (((KNN_STAGGER && METRIC == 6) || (KNN_STAGGER4 && METRIC == 4)) && wv >= NW / 2)
+                      ? res_tpb<METRIC>() / 2 : 0;
   const int64_t qg = (int64_t)qt * (NW * 32) + wv * 32 + j;
   const float* qrow = Q32 + qg * DP;
   // METRIC 3 (bf16x3 on 16x16x32) and 4 (fp16 on 16x16x32): lane l holds
@@ -464,6 +480,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
     for (int i = 0; i < 16; ++i) accw[i] = kI8Floor;
   }
   int rowp = 0;
+  int rowp_s = 0;  // (KNN_SPRE_GLB) the pending sub-tile's first image row, wave-uniform
   SelCount selc;
   // Seed-free int8 accumulation (KNN_I8_SMAX): a holds q.k of a sub-tile,
   // smx the largest seed of its rows.  Every value's exact accumulator q.k +
@@ -545,9 +562,29 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   // when the buffer may be refilled (a pending sub-tile starts empty: raw
   // accumulators kI8Floor and smx 0 never pass)
   int smt[SMX ? TPB : 1];
-  i32x4 spre[SMX ? NSG : 1];
+  constexpr bool SPG = I8W && SMX && KNN_SPRE_GLB;  // last sub-tile's seeds by scalar loads
+  // metric 6 (KNN_I8W_PF): the next sub-tile's A fragments in flight behind
+  // the current sub-tile's MFMAs (its LDS latency no longer ahead of them)
+  constexpr bool I8PF = I8W && KNN_I8W_PF;
+  i32x4 afn[I8PF ? DP / 32 : 1];
+  i32x4 spre[SMX && !SPG ? NSG : 1];
+  // (SPG) seed group c of the lane's rows of the sub-tile at image row r0s
+  // (wave-uniform): groups 2c and 2c + 1 by scalar loads, the lane's by h
+  // (inline asm: a plain load of a uniform address becomes a vector load,
+  // and its vmcnt wait would drain the staging pipeline's LDS-DMA pieces;
+  // scalar loads are waited for with lgkmcnt)
+  auto seed_glb = [&](int r0s, int c) {
+    const float* p = Xr + ((int64_t)r0s + 8 * c) * RSF + SEED;
+    const float* q = p + 4 * RSF;
+    i32x4 a, b;
+    asm volatile("s_load_dwordx4 %0, %2, 0x0\n\ts_load_dwordx4 %1, %3, 0x0\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&s"(a), "=&s"(b)
+                 : "s"(p), "s"(q)
+                 : "memory");
+    return h ? b : a;
+  };
 #pragma unroll
-  for (int c = 0; c < (SMX ? NSG : 1); ++c) spre[c] = i32x4{0, 0, 0, 0};
+  for (int c = 0; c < (SMX && !SPG ? NSG : 1); ++c) spre[c] = i32x4{0, 0, 0, 0};
   static_assert(!SMX || (TPB % 4 == 0 && kTR * 4 == 128), "sub-tile maxima are stored per 128-row group");
 
   // ---- staging: this wave's LDS-DMA pieces i = wv, wv+NW, ... of tile t ->
@@ -732,7 +769,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
 #pragma unroll
     for (int sub = 0; sub < TPB; ++sub) {
     // ps: the staged sub-tile processed at step sub (KNN_STAGGER rotates it)
-    const int ps = I8W && KNN_STAGGER ? (sub + rot) & (TPB - 1) : sub;
+    const int ps = (I8W && KNN_STAGGER) || (F16 && KNN_STAGGER4) ? (sub + rot) & (TPB - 1) : sub;
     const float* base = lds + cur * BUFF + ps * kTR * RSF;
     const float* base_prev = lds + cur * BUFF + ((I8W && KNN_STAGGER ? (sub - 1 + rot) & (TPB - 1) : sub - 1)) * kTR * RSF;
 
@@ -753,10 +790,23 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       // A fragment of k-step ks: row j, dims 32ks + 16h .. +15 (the image of
       // this kernel is not chunk-swizzled: the 32x32 reads are conflict-free)
       i32x4 af[DP / 32];
+      if (!I8PF || sub == 0) {
 #pragma unroll
-      for (int ks = 0; ks < DP / 32; ++ks)
-        af[ks] = __builtin_bit_cast(i32x4, *(const float4*)(base + j * RSF + 8 * ks + 4 * h));
-      if constexpr (SMX && PIPE) {
+        for (int ks = 0; ks < DP / 32; ++ks)
+          af[ks] = __builtin_bit_cast(i32x4, *(const float4*)(base + j * RSF + 8 * ks + 4 * h));
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < DP / 32; ++ks) af[ks] = afn[ks];
+      }
+      if (I8PF && sub + 1 < TPB) {
+        // (KNN_I8W_PF) the next sub-tile's A fragments, read behind this one's MFMAs
+        const float* bn =
+            lds + cur * BUFF + ((KNN_STAGGER ? (sub + 1 + rot) & (TPB - 1) : sub + 1)) * kTR * RSF;
+#pragma unroll
+        for (int ks = 0; ks < DP / 32; ++ks)
+          afn[ks] = __builtin_bit_cast(i32x4, *(const float4*)(bn + j * RSF + 8 * ks + 4 * h));
+      }
+      if constexpr (SMX && PIPE && !SPG) {
         if (sub == TPB - 1) {
 #pragma unroll
           for (int c = 0; c < NSG; ++c) spre[c] = seed_lds(base, c);
@@ -776,9 +826,11 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
         if (!(abl & 2)) {
           if constexpr (PIPE) {
             if (sub > 0) sel6(accw, rowp, smxp, [&](int c) { return seed_lds(base_prev, c); });
+            else if constexpr (SPG) sel6(accw, rowp, smxp, [&](int c) { return seed_glb(rowp_s, c); });
             else sel6(accw, rowp, smxp, [&](int c) { return spre[c]; });
             accw = acc;
             rowp = row0;
+            rowp_s = __builtin_amdgcn_readfirstlane((t * TPB + ps) * kTR);
             smxp = smt[sub];
           } else {
             sel6(acc, row0, smt[sub], [&](int c) { return seed_lds(base, c); });
@@ -953,7 +1005,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
         }
       }
       }
-      const int row0 = (t * TPB + sub) * kTR + 4 * g16;
+      const int row0 = (t * TPB + ps) * kTR + 4 * g16;
       if constexpr (PIPE) {
         if (!(abl & 2)) {
 #pragma unroll
@@ -1041,7 +1093,8 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   if constexpr (SMX && PIPE) {
     // the last tile's last sub-tile, seeds from spre
     if (!(abl & 2)) {
-      if constexpr (I8W) sel6(accw, rowp, smxp, [&](int c) { return spre[c]; });
+      if constexpr (SPG) sel6(accw, rowp, smxp, [&](int c) { return seed_glb(rowp_s, c); });
+      else if constexpr (I8W) sel6(accw, rowp, smxp, [&](int c) { return spre[c]; });
       else sel5(accp, rowp, smxp, [&](int c) { return spre[c]; });
     }
   } else if constexpr (PIPE && I8W) {

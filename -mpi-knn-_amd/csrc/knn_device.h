@@ -201,6 +201,32 @@ __device__ __forceinline__ void list_insert(float (&L)[R], int (&I)[R], float v,
   L[0] = __builtin_fminf(v, L[0]);
 }
 
+// fp16 kernel (KNN_M4_FAST): the fp16 resident kernel's no-candidate test as
+// a v_min3 tree + wave-uniform branch and med3 list shifts
+// (continuous cfg2: candidate kernel 2.43-2.44 -> 2.33-2.35 ms in 3
+// interleaved process pairs, profiles/ab_log.md r6f)
+#ifndef KNN_M4_FAST
+#define KNN_M4_FAST 1
+#endif
+// list_insert with each tail shift one v_med3_f32: for L[t-1] <= L[t] the
+// median of (v, L[t], L[t-1]) is max(L[t-1], min(v, L[t])) (no NaNs: the
+// candidate values are finite or +inf)
+template <int R>
+__device__ __forceinline__ void list_insert_med3(float (&L)[R], int (&I)[R], float v, int id) {
+  bool cc = true;  // v < L[R-1] by precondition
+#pragma unroll
+  for (int t = R - 1; t > 0; --t) {
+    const bool cp = v < L[t - 1];
+    float r;
+    asm("v_med3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(v), "v"(L[t]), "v"(L[t - 1]));
+    L[t] = r;
+    I[t] = cp ? I[t - 1] : (cc ? id : I[t]);
+    cc = cp;
+  }
+  I[0] = cc ? id : I[0];
+  L[0] = __builtin_fminf(v, L[0]);
+}
+
 // One 16-B-per-lane LDS-DMA piece (global_load_lds_dwordx4): 64 lanes x 16 B
 // from per-lane global addresses to LDS [lds_addr, lds_addr + 1 KiB).  Issued
 // from inline asm so hipcc neither counts it nor inserts its own
@@ -439,6 +465,25 @@ __device__ __forceinline__ float quad_union_kth16(const float (&t)[8], int K) {
 template <int R>
 __device__ __forceinline__ void select_quad_te(const f32x4& a, const f32x4& b, int row0,
                                                float (&L)[R], int (&I)[R], float& te) {
+#if KNN_M4_FAST
+  // 4 v_min3-shaped ops for 8 values and a wave-uniform branch (v_cmp into
+  // an SGPR pair + s_cbranch_vccz: no exec save / restore), as the int8
+  // kernels; insertions as v_med3_f32 shifts
+  const float m1 = __builtin_fminf(__builtin_fminf(a[0], a[1]), a[2]);
+  const float m2 = __builtin_fminf(__builtin_fminf(a[3], b[0]), b[1]);
+  const float m3 = __builtin_fminf(__builtin_fminf(b[2], b[3]), m1);
+  const float mn = __builtin_fminf(m2, m3);
+  if (__builtin_amdgcn_ballot_w64(mn < te)) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float v = i < 4 ? a[i] : b[i - 4];
+      if (v < te) {
+        list_insert_med3<R>(L, I, v, row_at(row0, i < 4 ? i : 16 + i - 4));
+        te = __builtin_fminf(te, L[R - 1]);
+      }
+    }
+  }
+#else
   const float mn = __builtin_fminf(__builtin_fminf(__builtin_fminf(a[0], a[1]),
                                                    __builtin_fminf(a[2], a[3])),
                                    __builtin_fminf(__builtin_fminf(b[0], b[1]),
@@ -453,6 +498,7 @@ __device__ __forceinline__ void select_quad_te(const f32x4& a, const f32x4& b, i
       }
     }
   }
+#endif
 }
 
 // int8 kernel (metric 5): the accumulators hold acc = q.k - ceil(||k||^2 / 2)

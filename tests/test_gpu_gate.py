@@ -3,8 +3,9 @@ library variant before timing it; with no KNN_GATE it checks the default
 build's AUTO path as part of the GPU suite).
 
 KNN_GATE: tune.py variant strings separated by ';' (e.g. "auto:0:0;auto:0:0,i8w=0"),
-KNN_GATE_N / KNN_GATE_M / KNN_GATE_D / KNN_GATE_K: the workload (default cfg2:
-1M x 10k, d = 128, k = 10, bench.synth's 8-bit grid data).  Per variant:
+KNN_GATE_N / KNN_GATE_M / KNN_GATE_D / KNN_GATE_K / KNN_GATE_DATA: the workload
+(default cfg2: 1M x 10k, d = 128, k = 10, bench.synth's 8-bit grid data;
+"continuous" for its min-max normalised form, the fp16 path).  Per variant:
   * the oracle (oracle/knn_oracle.cpp, pinned to the reference's own
     outputs) bit for bit on 8 queries -- labels, fp64 distances, indices
     except inside exact ties;
@@ -37,7 +38,8 @@ def test_variant_parity_gate():
     m = int(os.environ.get("KNN_GATE_M", 10_000))
     d = int(os.environ.get("KNN_GATE_D", 128))
     k = int(os.environ.get("KNN_GATE_K", 10))
-    X, lab, Q, _ = bench.synth(n, m, d, 10, 1234, 5678, DEV)
+    data = os.environ.get("KNN_GATE_DATA", "grid")
+    X, lab, Q, _ = bench.synth(n, m, d, 10, 1234, 5678, DEV, data=data)
     torch.cuda.synchronize()
     clf = knn.Classifier(0)
     clf.set_train_device(X.data_ptr(), lab.data_ptr(), n, d, 10, keep=(X, lab))
@@ -57,5 +59,5 @@ def test_variant_parity_gate():
         if first is None:
             first = got
         np.testing.assert_array_equal(got, first, err_msg="labels of %s differ from %s" % (v, variants[0]))
-        print("gate %s: 256 queries optimal, 8 = oracle, %s" % (v, clf.last_kernel_name()))
+        print("gate %s (%s data): 256 queries optimal, 8 = oracle, %s" % (v, data, clf.last_kernel_name()))
     clf.close()
