@@ -177,7 +177,8 @@ static int detect_i8(knn_ctx* ctx, const double* dX, int64_t n, int d) {
 // Region order of the train images (knn_order.hip): regions for n rows (0:
 // train order).  Only where the resident kernels run (d <= 256).  Auto: 64
 // regions (at most one per 16K rows) for integer-coded train sets (the int8
-// pass) whose image fits the 256 MB MALL with room to spare.  With the
+// pass) whose image fits the 256 MB MALL with room to spare, and for other
+// sets (the fp16 pass) whose fp16 image is at most 512 MB.  With the
 // order, a split's query tiles start their streams at different rows and no
 // longer share the staged tiles in L2, so a larger image is re-read from
 // HBM: the 12.5M x 96 shard ran 12.11 -> 13.87 ms, cfg2 1.342 -> 1.266 ms,
@@ -185,6 +186,13 @@ static int detect_i8(knn_ctx* ctx, const double* dX, int64_t n, int d) {
 // data gained nothing (2.343 / 2.342 ms; profiles/ab_log.md r4i, r4j).
 // 1: on at any size, 2..64: that many regions.
 constexpr int64_t kOrderMaxImage = 192ll << 20;
+// Train sets that are not integer-coded (the fp16 pass, continuous data):
+// auto on for fp16 images up to 512 MB.  Round 6, continuous cfg2 (272 MB
+// fp16 image): candidate kernel 2.353-2.363 -> 2.170-2.197 ms, rescans 2 ->
+// 1 per call, query ordering +17 us per call (profiles/ab_log.md r6h) --
+// the wave-uniform fp16 test (KNN_M4_FAST) turned the tight early
+// thresholds into skipped slow paths (round 4 measured 1.6 % without it).
+constexpr int64_t kOrderMaxImageF16 = 512ll << 20;
 // Query tiles start their streams at one of 8 phases of the region chain
 // (the first region of their region's eighth), not at their own region:
 // tiles of one phase share the staged tiles in L2 again -- cfg2 candidate
@@ -196,8 +204,10 @@ static int region_count(const knn_ctx* ctx, int64_t n, int d) {
   if (ctx->tune_order == 0 || pad_dim_fp16(d) <= 0) return 0;
   int P = (int)std::min<int64_t>(kRegionMax, n / 16384);
   if (ctx->tune_order < 0) {
-    const bool i8 = ctx->i8_ok && pad_dim_i8(d) > 0;
-    return i8 && P >= 8 && n * (pad_dim_i8(d) + 16) <= kOrderMaxImage ? P : 0;
+    if (ctx->i8_ok && pad_dim_i8(d) > 0)
+      return P >= 8 && n * (pad_dim_i8(d) + 16) <= kOrderMaxImage ? P : 0;
+    const int DPh = pad_dim_fp16(d);
+    return DPh > 0 && P >= 8 && n * (int64_t)(DPh / 2 + 4) * 4 <= kOrderMaxImageF16 ? P : 0;
   }
   if (ctx->tune_order >= 2) P = (int)std::min<int64_t>(ctx->tune_order, kRegionMax);
   P = (int)std::min<int64_t>(P, n / 256);

@@ -208,6 +208,10 @@ __device__ __forceinline__ void list_insert(float (&L)[R], int (&I)[R], float v,
 #ifndef KNN_M4_FAST
 #define KNN_M4_FAST 1
 #endif
+// the S3 kernel's quad selection (select_quad_f) in the same form
+#ifndef KNN_S3_FAST
+#define KNN_S3_FAST 0
+#endif
 // list_insert with each tail shift one v_med3_f32: for L[t-1] <= L[t] the
 // median of (v, L[t], L[t-1]) is max(L[t-1], min(v, L[t])) (no NaNs: the
 // candidate values are finite or +inf)
@@ -332,6 +336,23 @@ template <int R>
 __device__ __forceinline__ void select_quad_f(const f32x4& a, const f32x4& b, int row0,
                                               float (&L)[R], int (&I)[R], float tf) {
   float te = __builtin_fminf(tf, L[R - 1]);
+#if KNN_S3_FAST
+  // (as select_quad_te with KNN_M4_FAST: v_min3 tree, wave-uniform branch,
+  // med3 list shifts)
+  const float m1 = __builtin_fminf(__builtin_fminf(a[0], a[1]), a[2]);
+  const float m2 = __builtin_fminf(__builtin_fminf(a[3], b[0]), b[1]);
+  const float m3 = __builtin_fminf(__builtin_fminf(b[2], b[3]), m1);
+  if (__builtin_amdgcn_ballot_w64(__builtin_fminf(m2, m3) < te)) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float v = i < 4 ? a[i] : b[i - 4];
+      if (v < te) {
+        list_insert_med3<R>(L, I, v, row0 + (i < 4 ? i : 16 + i - 4));
+        te = __builtin_fminf(te, L[R - 1]);
+      }
+    }
+  }
+#else
   const float mn = __builtin_fminf(__builtin_fminf(__builtin_fminf(a[0], a[1]),
                                                    __builtin_fminf(a[2], a[3])),
                                    __builtin_fminf(__builtin_fminf(b[0], b[1]),
@@ -346,6 +367,7 @@ __device__ __forceinline__ void select_quad_f(const f32x4& a, const f32x4& b, in
       }
     }
   }
+#endif
 }
 
 // select_quad with the quad's filter te kept by the caller (refreshed from

@@ -276,9 +276,10 @@ const char* knn_last_kernel_name(knn_ctx* ctx);
  * "seed" (experiment: seeded global thresholds of the fp16 / int8 resident
  * kernels from a pre-pass over N strided train rows; 0 / -1 off, the
  * default -- measured slower; results stay exact); "order" (region order of
- * the train images, read by knn_set_train*: -1 auto -- on only for
- * integer-coded train sets (the int8 pass) whose int8 image (n x (padded d +
- * 16) bytes) is at most 192 MB, with P = min(64, n / 16384) regions and at
+ * the train images, read by knn_set_train*: -1 auto -- on for integer-coded
+ * train sets (the int8 pass) whose int8 image (n x (padded d + 16) bytes) is
+ * at most 192 MB and for other sets whose fp16 image (n x (2 padded d + 16)
+ * bytes) is at most 512 MB, with P = min(64, n / 16384) regions and at
  * least 8 of them -- 0 off, 1 on with P = min(64, n / 16384) regions (stays
  * off below n = 32768, where P < 2), 2..64 that many regions (at most n /
  * 256); queries of the resident fp16 / int8 kernels are then sorted by

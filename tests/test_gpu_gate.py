@@ -42,6 +42,7 @@ def test_variant_parity_gate():
     X, lab, Q, _ = bench.synth(n, m, d, 10, 1234, 5678, DEV, data=data)
     torch.cuda.synchronize()
     clf = knn.Classifier(0)
+    clf.set_tuning("order", int(os.environ.get("KNN_GATE_ORDER", -1)))  # the train layout
     clf.set_train_device(X.data_ptr(), lab.data_ptr(), n, d, 10, keep=(X, lab))
     lab_all = lab.cpu().numpy()
     first = None

@@ -43,16 +43,16 @@ fi
 # and workload); timing-only ablation variants (bits 1/2/8/16) are skipped
 gate_env() {
   local g="" prev="" t
-  GN=1000000; GM=10000; GD=128; GK=10; GDATA=grid
+  GN=1000000; GM=10000; GD=128; GK=10; GDATA=grid; GORD=-1
   for t in $1; do
-    case "$prev" in --n) GN=$t;; --m) GM=$t;; --d) GD=$t;; --k) GK=$t;; --data) GDATA=$t;; esac
+    case "$prev" in --n) GN=$t;; --m) GM=$t;; --d) GD=$t;; --k) GK=$t;; --data) GDATA=$t;; --order) GORD=$t;; esac
     case "$t" in
       *:*:*) a=$(echo "$t" | cut -d, -f1 | cut -d: -f4); a=${a:-0}
              [ $((a & 27)) = 0 ] && g="$g;$t";;
     esac
     prev=$t
   done
-  echo "KNN_GATE='${g#;}' KNN_GATE_N=$GN KNN_GATE_M=$GM KNN_GATE_D=$GD KNN_GATE_K=$GK KNN_GATE_DATA=$GDATA"
+  echo "KNN_GATE='${g#;}' KNN_GATE_N=$GN KNN_GATE_M=$GM KNN_GATE_D=$GD KNN_GATE_K=$GK KNN_GATE_DATA=$GDATA KNN_GATE_ORDER=$GORD"
 }
 run_gate() {  # $1 variant library ("base" = default), $2 tune.py arguments
   [ "${GATE:-1}" = 0 ] && return 0
