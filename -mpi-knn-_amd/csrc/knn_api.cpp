@@ -1126,6 +1126,16 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   rp.thr = (float*)ctx->fr_thr.p;
   rp.fcnt = (int*)ctx->fr_cnt.p;
   rp.cap = abl ? 0 : cap;
+  // the int8 rescan filter (metric 6's plain image; knn_select.hip)
+  // (tuning key "i8resc": -1 / 1 auto, 0 every failed query on the fp32 filter)
+  const bool i8resc = ctx->tune_i8resc != 0 && kmetric == 6 && ctx->i8_swz == 0 && DP <= 256 &&
+                      DP % 16 == 0;
+  if (i8resc) {
+    if ((rc = ctx->rescan_qc8.ensure((size_t)cap * 256 + 16))) return rc;
+    if ((rc = ctx->rescan_t8.ensure((size_t)cap * sizeof(long long) + 16))) return rc;
+    rp.qc8 = (signed char*)ctx->rescan_qc8.p;
+    rp.t8 = (long long*)ctx->rescan_t8.p;
+  }
   if (kmetric >= 5) {
     // int8 proxies are exact up to +1 (the odd-norm half of the seed): the
     // merge sees the pass's own centre and scale (codes (x - cent/2^s) 2^s),
@@ -1170,6 +1180,13 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   rb.S = sm.S;
   rb.trows = sm.trows;
   rb.cus = ctx->cu_count;
+  if (i8resc) {
+    rb.qc8 = rp.qc8;
+    rb.t8 = rp.t8;
+    rb.i8img = (const signed char*)ctx->XI.p;
+    rb.i8rb = DP + 16;
+    rb.i8dp = DP;
+  }
   launch_rescan(metric, t, dQ, rb, abl ? 0 : cap, W, err_factor(metric, t.DP), sink,
                 abl ? 0 : (int)std::min<int64_t>(m, ctx->cu_count), s);
   // (without the full-scan launch nothing writes this call's counts)
@@ -1587,6 +1604,9 @@ int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value) {
   } else if (!strcmp(key, "qblk")) {
     if (value < 0 || value > 1 << 20) return knn_fail(KNN_ERR_ARG, "qblk must be 0 (split-major) or >= 1");
     ctx->tune_qblk = (int)value;
+  } else if (!strcmp(key, "i8resc")) {
+    if (value < -1 || value > 1) return knn_fail(KNN_ERR_ARG, "i8resc must be -1 (auto), 0 or 1");
+    ctx->tune_i8resc = (int)value;
   } else if (!strcmp(key, "gg")) {
     if (value != -1 && value != 4 && value != 8) return knn_fail(KNN_ERR_ARG, "gg must be -1 (auto), 4 or 8");
     ctx->tune_gg = (int)value;

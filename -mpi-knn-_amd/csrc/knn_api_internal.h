@@ -77,6 +77,7 @@ struct knn_ctx {
   // 0 off, 1 on; ord_nb: the current layout has them (ord_perm / ord_ipos valid)
   int tune_nblk = -1;
   int tune_gg = -1;            // gthr slot groups of the resident kernel: -1 auto, 4 or 8
+  int tune_i8resc = -1;        // int8 rescan filter (metric 6): -1 auto (on), 0 off
   int tune_qblk = 0;           // resident kernel workgroup order: 0 split-major, B query blocks
   bool ord_nb = false;
   // ints of ord_bcnt known to be zero (the int8 query builder clears the
@@ -112,7 +113,7 @@ struct knn_ctx {
       ord_qperm, ord_qpos, ord_qstart, ord_perm0;
   // per-classify workspace
   DevBuf Q64, Q32, qvalid, cand_v, cand_i, gthr, rescan_q, rescan_tau, rescan_cnt, fr_cnt, fr_buf,
-      fr_q, fr_thr, slow_q, totals, lk, rescan_mask, rescan_nkeep;
+      fr_q, fr_thr, slow_q, totals, lk, rescan_mask, rescan_nkeep, rescan_qc8, rescan_t8;
   // train-sharded merge of unions beyond 4096 entries (rank merge scratch)
   DevBuf mrg;
   // reference tie order pass: queued queries, per-workgroup scratch
@@ -126,7 +127,7 @@ struct knn_ctx {
             &XH,      &XT16,    &XS16,  &mu,      &mu_part, &Q64, &Q32,    &qvalid, &cand_v,   &cand_i,
             &gthr,    &rescan_q, &rescan_tau, &rescan_cnt, &fr_cnt, &fr_buf, &fr_q, &fr_thr,
             &slow_q,  &totals,  &lk, &mrg, &tie_q, &tie_ws, &o_lab, &o_idx, &o_dist, &o_flags, &nrm_part, &nrm_mm, &nrm_X,
-            &rescan_mask, &rescan_nkeep, &smp_x64, &smp_xl2, &smp_img, &smp_scr, &smp_v, &smp_i,
+            &rescan_mask, &rescan_nkeep, &rescan_qc8, &rescan_t8, &smp_x64, &smp_xl2, &smp_img, &smp_scr, &smp_v, &smp_i,
             &ord_cent, &ord_cnorm, &ord_img, &ord_rank, &ord_rstart, &ord_perm, &ord_ipos, &ord_key, &ord_bcnt, &ord_tot,
             &ord_qkey, &ord_qperm, &ord_qpos, &ord_qstart, &ord_perm0};
   }

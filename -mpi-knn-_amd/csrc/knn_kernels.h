@@ -209,6 +209,13 @@ struct RescanPrep {
   float* thr = nullptr;  // [cap]
   int* fcnt = nullptr;   // [cap]
   int jx = 0, DP = 0, cap = 0;
+  // int8 pass with an unswizzled image (kernel metric 6): a failed query on
+  // the train grid is filtered on the codes instead (rescan_filter_i8_kernel):
+  // its codes [cap][256] and the largest exact integer squared distance
+  // (code units) a row may have to reach tau; t8 < 0: the fp32 filter's
+  // query (off the grid, tau unknown, or no int8 pass).  Null: none.
+  signed char* qc8 = nullptr;
+  long long* t8 = nullptr;
 };
 void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int R,
                          const TrainDev& t, const double* Q64, int64_t m, int W, int C,
@@ -236,6 +243,12 @@ struct RescanBufs {
   int S;                     // splits / tile rows of the candidate launch (mask bits)
   int64_t trows;
   int cus;                   // compute units (the staged filter's grid)
+  // int8 filter (RescanPrep::qc8 / t8; null: every query on the fp32 filter):
+  // the int8 image [n_pad][i8rb] bytes, codes of dims [0, i8dp) plain
+  const signed char* qc8 = nullptr;
+  const long long* t8 = nullptr;
+  const signed char* i8img = nullptr;
+  int i8rb = 0, i8dp = 0;
 };
 // Enqueues the rescan path (filter, exact finish, full scan; the merge did
 // each fast-path query's setup, RescanPrep); every kernel reads the counts on

@@ -615,7 +615,10 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
     // full scan takes the query)
     if (tid < 64 && s_f < rp.cap) {
       rescan_prep_query<METRIC>(rp, d, qv, KNN_INF_D, rp.qf + (int64_t)s_f * rp.DP, rp.thr + s_f);
-      if (tid == 0) rp.fcnt[s_f] = 0;
+      if (tid == 0) {
+        rp.fcnt[s_f] = 0;
+        if (rp.t8) rp.t8[s_f] = -1;  // (tau unknown: the full scan takes it)
+      }
     }
     return;
   }
@@ -698,9 +701,27 @@ merge_rerank_kernel(const float* __restrict__ cv, const int* __restrict__ ci, in
   __syncthreads();
   if (!s_cert) {
     // the fast rescan's setup of this query (tau: its W-th exact distance)
-    if (tid < 64 && s_f < rp.cap)
+    if (tid < 64 && s_f < rp.cap) {
       rescan_prep_query<METRIC>(rp, d, qv, cn >= W ? dk[W - 1] : KNN_INF_D,
                                 rp.qf + (int64_t)s_f * rp.DP, rp.thr + s_f);
+      if (METRIC == 0 && rp.t8) {
+        // on the train grid: the rescan filters on the codes, exactly.  The
+        // reference's r = (qq + xx - 2 q.x) 4^-s is exact there (DESIGN.md
+        // section 2), so a row reaches tau only if its integer r_int <=
+        // tau^2 4^s (+ a relative 1e-12 and 2 for the rounding of tau^2)
+        const bool ok = s_i8x && cn >= W;
+        if (ok)
+          for (int c = lane; c < 256; c += 64) rp.qc8[(int64_t)s_f * 256 + c] = s_qc[c];
+        if (lane == 0) {
+          long long T = -1;
+          if (ok) {
+            const double tt = __builtin_ldexp(dk[W - 1] * dk[W - 1], 2 * t.jx) * (1.0 + 1e-12);
+            T = tt < 0x1p62 ? (long long)tt + 2 : (1ll << 62);  // (the filter forms qq + xx - 2 q.x)
+          }
+          rp.t8[s_f] = T;
+        }
+      }
+    }
     return;
   }
 
@@ -765,6 +786,9 @@ void launch_merge_rerank(int metric, const float* cv, const int* ci, int NL, int
 }
 
 // ------------------------------------------------- rescan (device-driven)
+#ifndef KNN_DEBUG_RESCAN
+#define KNN_DEBUG_RESCAN 0  // (diagnostic builds: the filters' query modes)
+#endif
 // Queries whose candidate set was not certified (a list overflowed near the
 // top, heavy ties, operands out of the candidate format's range).  The
 // whole path is enqueued on every call and sized on the device: the merge
@@ -806,7 +830,7 @@ __global__ void __launch_bounds__(256)
 rescan_filter_kernel(TrainDev t, const float* __restrict__ qf, const float* __restrict__ thr,
                      const int* __restrict__ cnt, int cap, int* __restrict__ fcnt,
                      int* __restrict__ buf, const unsigned long long* __restrict__ mask, int S,
-                     int64_t trows) {
+                     int64_t trows, const long long* __restrict__ t8) {
   const int nf = min(cnt[0], cap);
   if (nf == 0) return;
   extern __shared__ __attribute__((aligned(16))) float fsm[];
@@ -824,7 +848,8 @@ rescan_filter_kernel(TrainDev t, const float* __restrict__ qf, const float* __re
     unsigned long long u = ~0ull;
     if (mask && nf <= 64) {
       u = 0;
-      for (int f = 0; f < nf; ++f) u |= mask[f];
+      for (int f = 0; f < nf; ++f)
+        if (!(t8 && t8[f] >= 0)) u |= mask[f];  // (int8-filtered queries: not here)
     }
     s_u = u;
     int ns = 0;
@@ -834,6 +859,11 @@ rescan_filter_kernel(TrainDev t, const float* __restrict__ qf, const float* __re
     s_ns = ns;
   }
   __syncthreads();
+#if KNN_DEBUG_RESCAN
+  if (blockIdx.x == 0 && tid == 0)
+    printf("fp32 filter: nf %d u %llx ns %d t8 %p mask %p\n", nf, s_u, s_ns, (const void*)t8,
+           (const void*)mask);
+#endif
   const unsigned long long need = s_u;
   // Units of 64 rows, one per wave; a workgroup's NWB waves take NWB
   // consecutive units per step (grid-stride).  A targeted rescan (every
@@ -883,7 +913,8 @@ rescan_filter_kernel(TrainDev t, const float* __restrict__ qf, const float* __re
       qs[e] = qi < nfg ? qf[(int64_t)g0 * DP + e] : 0.0f;
     }
     if (tid < FQ) {
-      thr_s[tid] = tid < nfg ? thr[g0 + tid] : -KNN_INF_F;  // absent: no row passes
+      // absent, or filtered on the int8 codes (rescan_filter_i8_kernel): no row passes
+      thr_s[tid] = tid < nfg && !(t8 && t8[g0 + tid] >= 0) ? thr[g0 + tid] : -KNN_INF_F;
       mask_s[tid] = tid < nfg && mask ? mask[g0 + tid] : ~0ull;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -921,6 +952,154 @@ rescan_filter_kernel(TrainDev t, const float* __restrict__ qf, const float* __re
     }
   }
   }  // units
+}
+
+// The fast rescan's filter on the int8 codes (kernel metric 6 images: plain
+// rows of i8rb bytes, codes of i8dp dims), for the failed queries on the
+// train grid (t8[f] >= 0; the others go through rescan_filter_kernel): lane =
+// image row, its codes read in place (i8dp / 16 x 16 B), the exact integer
+// squared distance qq + xx - 2 q.x (code units, v_dot4) against t8 -- 144 B
+// per row instead of the fp32 filter's 528 (cfg2), and no error bound: every
+// row within tau (and its ties) is appended exactly.  Same unit walk as the
+// fp32 filter: only the flagged splits' tiles of a targeted rescan.
+constexpr int kI8RescanRB = 272;  // LDS bytes per staged row of the int8 filter (>= the largest rb)
+template <int FQ>
+__global__ void __launch_bounds__(256)
+rescan_filter_i8_kernel(TrainDev t, const signed char* __restrict__ img, int rb, int dp,
+                        const signed char* __restrict__ qc8, const long long* __restrict__ t8,
+                        const int* __restrict__ cnt, int cap, int* __restrict__ fcnt,
+                        int* __restrict__ buf, const unsigned long long* __restrict__ mask, int S,
+                        int64_t trows) {
+  const int nf = min(cnt[0], cap);
+  if (nf == 0) return;
+  __shared__ __attribute__((aligned(16))) signed char qs[FQ][256];
+  __shared__ long long ts[FQ];
+  __shared__ int qqs[FQ];
+  __shared__ unsigned long long mask_s[FQ];
+  __shared__ unsigned long long s_u;
+  __shared__ int s_sp[64], s_ns, s_any;
+  // each wave's 64 staged rows (+ 1 KiB: the last piece may run past them)
+  __shared__ __attribute__((aligned(16))) signed char rows_s[4 * 64 * kI8RescanRB + 1024];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int NWB = blockDim.x >> 6;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nch = dp / 16;
+  if (tid == 0) {
+    // the splits the int8-mode queries flag (every row if any flags all, or
+    // more than 64 failed queries)
+    unsigned long long u = mask && nf <= 64 ? 0ull : ~0ull;
+    int any = 0;
+    for (int f = 0; f < nf; ++f)
+      if (t8[f] >= 0) {
+        any = 1;
+        if (mask && nf <= 64) u |= mask[f];
+      }
+    s_any = any;
+    s_u = u;
+    int ns = 0;
+    if (u != ~0ull)
+      for (int b = 0; b < 64; ++b)
+        if ((u >> b) & 1) s_sp[ns++] = b;
+    s_ns = ns;
+  }
+  __syncthreads();
+#if KNN_DEBUG_RESCAN
+  if (blockIdx.x == 0 && tid == 0)
+    for (int f = 0; f < nf; ++f)
+      printf("i8 filter: nf %d f %d t8 %lld mask %llx any %d u %llx ns %d\n", nf, f, t8[f],
+             mask ? mask[f] : 0ull, s_any, s_u, s_ns);
+#endif
+  if (!s_any) return;
+  const unsigned long long need = s_u;
+  const bool tgt = mask && need != ~0ull;
+  const int gpt = tgt ? (int)(trows / 64) : 1;
+  const int64_t ntile = tgt ? (t.n_pad + trows - 1) / trows : 0;
+  const int64_t units = tgt ? (int64_t)s_ns * ((ntile + S - 1) / S) * gpt : (t.n_pad + 63) / 64;
+  // every failed query in groups of FQ (fp32-mode ones get ts = -1: no row
+  // passes, r >= 0), the rows of each group's units re-read from L2
+  for (int g0 = 0; g0 < nf; g0 += FQ) {
+    const int nfg = min(FQ, nf - g0);
+    __syncthreads();  // the previous group's reads of qs are done
+    for (int e = tid; e < FQ * 256; e += blockDim.x) {
+      const int a = e >> 8;
+      qs[a][e & 255] = a < nfg && t8[g0 + a] >= 0 ? qc8[(int64_t)(g0 + a) * 256 + (e & 255)] : 0;
+    }
+    if (tid < FQ) {
+      ts[tid] = tid < nfg ? t8[g0 + tid] : -1;
+      mask_s[tid] = tid < nfg && mask ? mask[g0 + tid] : ~0ull;
+    }
+    __syncthreads();
+    if (tid < FQ) {
+      int qq = 0;
+      for (int c = 0; c < dp; ++c) qq += (int)qs[tid][c] * (int)qs[tid][c];
+      qqs[tid] = qq;
+    }
+    __syncthreads();
+    bool grp = false;  // (block-uniform) any int8-mode query in this group
+#pragma unroll
+    for (int a = 0; a < FQ; ++a) grp |= ts[a] >= 0;
+    if (!grp) continue;
+    for (int64_t u = (int64_t)blockIdx.x * NWB + wv; u < units; u += (int64_t)gridDim.x * NWB) {
+      int64_t row0 = -1;
+      int wsp = 0;
+      if (tgt) {
+        const int64_t r = u / gpt, k = r / s_ns;
+        const int sp = s_sp[r - k * s_ns];
+        const int64_t tile = sp + k * S;
+        if (tile < ntile) {
+          row0 = tile * trows + (u - r * gpt) * 64;
+          wsp = sp;
+        }
+      } else {
+        row0 = u * 64;
+        wsp = mask ? (int)((row0 / trows) % S) : 0;
+      }
+      if (row0 < 0) continue;  // (wave-uniform)
+      const int64_t row = row0 + lane;
+      // the wave's 64 rows are contiguous in the image: coalesced 1-KiB
+      // LDS-DMA pieces into its own LDS tile (at the image's row stride rb,
+      // an odd number of 16-B chunks: conflict-free ds_read_b128), then lane
+      // = row reads its row there
+      {
+        const char* src = (const char*)(img + row0 * rb) + lane * 16;
+        const uint32_t dst = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) signed char*)&rows_s[wv * 64 * kI8RescanRB];
+        for (int p = 0; p * 1024 < 64 * rb; ++p) glds16(src + p * 1024, dst + p * 1024);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      if (row >= t.n) continue;  // (image rows >= n are padding)
+      const signed char* xr = &rows_s[wv * 64 * kI8RescanRB + lane * rb];  // (copied at the image's stride)
+      int xx = 0;
+      int dot[FQ];
+#pragma unroll
+      for (int a = 0; a < FQ; ++a) dot[a] = 0;
+      for (int ch = 0; ch < nch; ++ch) {
+        const int4 xv = *(const int4*)(xr + 16 * ch);
+        xx = __builtin_amdgcn_sdot4(xv.x, xv.x, xx, false);
+        xx = __builtin_amdgcn_sdot4(xv.y, xv.y, xx, false);
+        xx = __builtin_amdgcn_sdot4(xv.z, xv.z, xx, false);
+        xx = __builtin_amdgcn_sdot4(xv.w, xv.w, xx, false);
+#pragma unroll
+        for (int a = 0; a < FQ; ++a) {
+          const int4 qv = *(const int4*)(&qs[a][16 * ch]);
+          int dd = dot[a];
+          dd = __builtin_amdgcn_sdot4(xv.x, qv.x, dd, false);
+          dd = __builtin_amdgcn_sdot4(xv.y, qv.y, dd, false);
+          dd = __builtin_amdgcn_sdot4(xv.z, qv.z, dd, false);
+          dd = __builtin_amdgcn_sdot4(xv.w, qv.w, dd, false);
+          dot[a] = dd;
+        }
+      }
+#pragma unroll
+      for (int a = 0; a < FQ; ++a) {
+        const long long r = (long long)qqs[a] + xx - 2ll * dot[a];
+        if (((mask_s[a] >> wsp) & 1) && r <= ts[a]) {
+          const int f = g0 + a;
+          const int pos = atomicAdd(&fcnt[f], 1);
+          if (pos < kRescanCap) buf[(int64_t)f * kRescanCap + pos] = train_row(t, (int)row);
+        }
+      }
+    }
+  }
 }
 
 // DP > 256 (rows too long to stage 64 per wave): 4 lanes per train row, 16
@@ -1203,12 +1382,20 @@ void launch_rescan(int metric, const TrainDev& t, const double* Q64, const Resca
       // no second one)
       const dim3 fg((unsigned)std::min<int64_t>((t.n_pad + rpb - 1) / rpb, std::max(1, rb.cus)));
       const size_t flds = qbytes + nwb * tile;
+      // the int8 filter first (its queries never pass the fp32 one): both
+      // exit at once when they have no query
+      const bool i8f = metric == 0 && rb.t8 && rb.qc8 && rb.i8img && rb.i8dp % 16 == 0 &&
+                       rb.i8dp <= 256;
+      if (i8f)
+        hipLaunchKernelGGL((rescan_filter_i8_kernel<4>), dim3(std::max(1, rb.cus)), dim3(256), 0, s,
+                           t, rb.i8img, rb.i8rb, rb.i8dp, rb.qc8, rb.t8, rb.cnt, cap, rb.fcnt,
+                           rb.buf, mk, mS, mT);
       if (metric == 0)
         hipLaunchKernelGGL((rescan_filter_kernel<0, FQ>), fg, dim3(64 * nwb), flds, s, t, rb.qf,
-                           rb.thr, rb.cnt, cap, rb.fcnt, rb.buf, mk, mS, mT);
+                           rb.thr, rb.cnt, cap, rb.fcnt, rb.buf, mk, mS, mT, i8f ? rb.t8 : nullptr);
       else
         hipLaunchKernelGGL((rescan_filter_kernel<1, FQ>), fg, dim3(64 * nwb), flds, s, t, rb.qf,
-                           rb.thr, rb.cnt, cap, rb.fcnt, rb.buf, mk, mS, mT);
+                           rb.thr, rb.cnt, cap, rb.fcnt, rb.buf, mk, mS, mT, nullptr);
     } else {
       // 64 rows per 4-wave block; 8 queries per pass (a failed query is rare
       // at d > 256: the LDS of 8 query rows leaves room for 5 blocks per CU,

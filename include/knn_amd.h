@@ -295,6 +295,9 @@ const char* knn_last_kernel_name(knn_ctx* ctx);
  * kernel's per-lane lists and the sub-tiles over the window's tiles, so rows
  * of adjacent norm share neither a list nor a split); "s3gq" (the fp16 d > 256 kernel's largest XCD grouping of query
  * tiles, 0 = 4); "xhswz" (the fp16 image's chunk swizzle: 1 on, 0 off);
+ * "i8resc" (the fast rescan of failed queries on the train grid filters the
+ * int8 32x32x32 kernel's image exactly on the codes: -1 auto = on, 0 every
+ * failed query on the fp32 filter);
  * all of them leave results exact. */
 int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value);
 

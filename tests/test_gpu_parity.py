@@ -369,7 +369,9 @@ def test_targeted_rescan(knn, path, order):
         X = cen[lab_all] + 0.35 * rng.standard_normal((20600, d))
         tr, te, lab = X[:20000].copy(), X[20000:].copy(), lab_all[:20000].copy()
     rescans = 0
-    for S in (2, 3):
+    # metric 6 (i8w): the failed queries' rescan filters the int8 image on the
+    # codes (i8resc auto) and, as a check of both filters, the fp32 image
+    for S, i8resc in ((2, -1), (3, -1)) + (((2, 0),) if path == "i8w" else ()):
         c = knn.Classifier(0)
         if path in ("i8", "i8w"):
             c.set_tuning("i8", 1)
@@ -377,6 +379,7 @@ def test_targeted_rescan(knn, path, order):
             c.set_precision(knn.PRECISION_FP16)
         c.set_tuning("S", S)
         c.set_tuning("order", order)
+        c.set_tuning("i8resc", i8resc)
         run_case(c, knn, tr, lab, te, k, 0, 6)
         assert c.last_candidate_path() == {"i8": 5, "i8w": 6}.get(path, 4)
         assert c.last_geometry()["splits"] == S
