@@ -125,6 +125,24 @@ static_assert(KNN_RES_TPB * knnk::kTR == knnk::kResTileRows || KNN_RES_TPB != 2,
 #ifndef KNN_I8W_PF
 #define KNN_I8W_PF 0
 #endif
+// metric 6: barrier-free staging (experiment).  Instead of one s_barrier per
+// staged tile, each buffer carries two LDS counters: ready (waves whose
+// pieces of the buffer's tile have landed) and done (waves that finished
+// reading it).  A wave starts tile it once every wave's pieces of it have
+// landed, and issues its pieces of tile it+1 into the other buffer as soon
+// as every wave has finished tile it-1 (polled after each sub-tile) -- so a
+// wave may run up to a tile ahead of the slowest one instead of waiting for
+// it at every tile (the no-barrier ablation: -16 %, round 5 r5e).
+#ifndef KNN_I8_CTR
+#define KNN_I8_CTR 0
+#endif
+// (KNN_I8_CTR) sub-tiles after issuing its pieces of the next tile at which a
+// wave waits for them (vmcnt) and counts them ready -- early enough that the
+// other waves need not wait for it to finish its tile, late enough that the
+// pieces have landed from L2 / HBM
+#ifndef KNN_CTR_SIGD
+#define KNN_CTR_SIGD 4
+#endif
 // metric 6: the no-candidate test's max over 16 values as 7 v_max3 + 1 v_max
 #ifndef KNN_MAX3T
 #define KNN_MAX3T 0
@@ -152,6 +170,18 @@ __device__ __forceinline__ void wait_barrier_x(int extra) {
   else if (extra == 2) wait_barrier<BASE + 2>();
   else if (extra == 1) wait_barrier<BASE + 1>();
   else wait_barrier<BASE>();
+}
+
+// (KNN_I8_CTR) wait until the LDS counter *p reaches target; bounded (a
+// protocol error ends the wait after ~2^22 sleeps instead of hanging the GPU;
+// the parity gate then sees wrong answers)
+__device__ __forceinline__ void ctr_wait(int* p, int target) {
+  for (int n = 0; n < (1 << 22); ++n) {
+    if (__builtin_amdgcn_readfirstlane(*(volatile int*)p) >= target) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 #ifndef KNN_PUB_EVERY
@@ -419,6 +449,13 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   constexpr int GW = QW > 32 ? 128 : 64;  // gls entries per wave
   constexpr int XMAX = GW == 128 ? 3 : 2;  // exchange ops in flight at most
   __shared__ __attribute__((aligned(16))) u32x4 gls[NW * GW];
+  // (KNN_I8_CTR) ready[2] | done[2] counters of the two staging buffers
+  constexpr bool CTR = METRIC == 6 && KNN_I8_CTR && KNN_I8_NB == 2;
+  __shared__ int s_ctr[CTR ? 4 : 1];
+  if constexpr (CTR) {
+    if (threadIdx.x < 4) s_ctr[threadIdx.x] = 0;
+    __syncthreads();
+  }
   const uint32_t gls_addr =
       (uint32_t)(uintptr_t)(__attribute__((address_space(3))) u32x4*)gls + wv * GW * 16;
   // An exchange at tile e issues (after that tile's DMA pieces) an atomic
@@ -629,6 +666,11 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
 
   const bool g_hi = wv < NG % NW || NG % NW == 0;
   int cur = 0, nxt = PD;  // buffer of tile it, buffer that tile it+PD goes to
+  // (CTR) whether this wave has issued its pieces of tile it / it+1 (tile 0:
+  // by the prologue)
+  bool issued_cur = true, issued_next = false;
+  bool signalled_cur = false, signalled_next = false;  // (CTR) counted ready
+  int sig_at = TPB;  // (CTR) the sub-tile at which to count the next tile's pieces ready
   for (int it = 0; it < my_nt; ++it) {
     const int t = tile_at(it);
 #if KNN_COUNT_SEL
@@ -655,7 +697,20 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
 #else
       const int extra = (x_age >= 1 && x_age <= XPD - 1) ? x_ops : 0;
 #endif
-      if (abl & 16) {
+      if constexpr (CTR) {
+        if (!issued_cur) {  // (this wave could not issue them during the previous tile)
+          ctr_wait(&s_ctr[2 + cur], NW * (it / 2));
+          KNN_ISSUE(tile_at(it), cur);
+        }
+        if (!signalled_cur) {
+          // this wave's pieces of tile it landed (and every older op)
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (lane == 0) atomicAdd(&s_ctr[cur], 1);
+        }
+        ctr_wait(&s_ctr[cur], NW * (it / 2 + 1));  // every wave's pieces landed
+        issued_next = signalled_next = false;
+        sig_at = TPB;
+      } else if (abl & 16) {
         // timing-only ablation: this wave's own waits, no workgroup barrier
         // (other waves' pieces may not have landed: results invalid)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -669,7 +724,18 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       __builtin_amdgcn_sched_barrier(0);
       // (abl bit 3: the same pieces, always of the split's first tile -- DMA
       // issue cost without the data stream; timing only)
-      if (it + PD < my_nt && !(abl & 1)) KNN_ISSUE((abl & 8) ? tile_at(0) : tile_at(it + PD), nxt);
+      if (CTR) {
+        // the next tile into the other buffer right away when every wave is
+        // done with it (always for tile 1)
+        if (it + 1 < my_nt &&
+            __builtin_amdgcn_readfirstlane(*(volatile int*)&s_ctr[2 + nxt]) >= NW * ((it + 1) / 2)) {
+          KNN_ISSUE(tile_at(it + 1), nxt);
+          issued_next = true;
+          sig_at = KNN_CTR_SIGD;
+        }
+      } else if (it + PD < my_nt && !(abl & 1)) {
+        KNN_ISSUE((abl & 8) ? tile_at(0) : tile_at(it + PD), nxt);
+      }
       if (gthr) {
         if (x_age == XPD) {
 #pragma unroll
@@ -819,6 +885,22 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       for (int ks = 0; ks < DP / 32; ++ks)
         acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[ks], __builtin_bit_cast(i32x4, qf[ks]),
                                                     SMX && ks == 0 ? i32x16{} : acc, 0, 0, 0);
+      if constexpr (CTR) {
+        // (poll) the next tile's pieces as soon as every wave is done with
+        // the tile before this one; SIGD sub-tiles later, counted ready
+        if (!issued_next) {
+          if (it + 1 < my_nt &&
+              __builtin_amdgcn_readfirstlane(*(volatile int*)&s_ctr[2 + nxt]) >= NW * ((it + 1) / 2)) {
+            KNN_ISSUE(tile_at(it + 1), nxt);
+            issued_next = true;
+            sig_at = sub + 1 + KNN_CTR_SIGD;
+          }
+        } else if (!signalled_next && sub >= sig_at) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (lane == 0) atomicAdd(&s_ctr[nxt], 1);
+          signalled_next = true;
+        }
+      }
       const int row0 = (t * TPB + ps) * kTR + 4 * h;
       if constexpr (SMX) {
         // the pending sub-tile's selection after this one's MFMAs (seeds of
@@ -1084,6 +1166,14 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
     if (!(abl & 2)) select_block<R>(acc, (t * TPB + sub) * kTR, h, L[0], I[0], thr[0], tq[0]);
     else if (acc[0] == 1234.5f && acc[15] == 1234.5f) thr[0] = acc[7];  // keep acc live
     }
+    }
+    if constexpr (CTR) {
+      // every read of this tile's buffer done (the last sub-tile's seeds are
+      // in spre), then counted: its refill may be issued
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) atomicAdd(&s_ctr[2 + cur], 1);
+      issued_cur = issued_next;
+      signalled_cur = signalled_next;
     }
     if (++cur == NB) cur = 0;
     if (++nxt == NB) nxt = 0;
