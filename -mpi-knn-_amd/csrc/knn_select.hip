@@ -292,15 +292,19 @@ __device__ void exact_sorted(const TrainDev& t, const double* qv, int* di, doubl
 template <int NT>
 __device__ void exact_sorted_i8(const TrainDev& t, const ProxyScale& ps, const signed char* qc,
                                 int qq, int* di, double* dk, int cn, int C2, int tid) {
-  constexpr int G = 8, RP = NT / G;
+  // 32 rows per pass (one wave: 2 lanes per row), so cfg2's ~13-27 selected
+  // rows take one dependent load round instead of 2-4; each row's train row
+  // (region order) is loaded with its codes, not in a second round
+  constexpr int G = NT / 32 < 1 ? 1 : NT / 32, RP = NT / G;
   const int g = tid & (G - 1);
   const int nch = ps.i8dp / 16;
   const double sc = __builtin_ldexp(1.0, -2 * t.jx);  // (t.jx = s: the pass's scale)
   for (int r0 = 0; r0 < cn; r0 += RP) {
     const int c = r0 + tid / G;
-    int dot = 0, xx = 0;
+    int dot = 0, xx = 0, tr = 0;
     if (c < cn) {
       const int p = di[c];
+      tr = t.perm && g == 0 ? t.perm[p] : p;
       const signed char* row = ps.i8x + (int64_t)p * ps.i8rb;
       const int sw = ps.i8swz ? xh_swz(p & 15) : 0;
       for (int ch = g; ch < nch; ch += G) {
@@ -321,11 +325,12 @@ __device__ void exact_sorted_i8(const TrainDev& t, const ProxyScale& ps, const s
       dot += __shfl_xor(dot, o, 64);
       xx += __shfl_xor(xx, o, 64);
     }
-    if (c < cn && g == 0) dk[c] = __builtin_sqrt((double)(qq + xx - 2 * dot) * sc);
+    if (c < cn && g == 0) {
+      dk[c] = __builtin_sqrt((double)(qq + xx - 2 * dot) * sc);
+      di[c] = tr;  // image position -> train row (its group has read di[c] already)
+    }
   }
   __syncthreads();
-  if (t.perm)  // image positions -> train rows (region order)
-    for (int c = tid; c < cn; c += NT) di[c] = t.perm[di[c]];
   for (int c = tid; c < C2; c += NT) {
     if (c >= cn) {
       dk[c] = KNN_INF_D;
