@@ -1040,8 +1040,17 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
                       (unsigned short*)ctx->Q32.p, 2 * DP, nullptr, nullptr, s);
   else
     launch_prep_queries(dQ, t.mu, m, t.d, DP, m_pad, qscale, t.jx, (float*)ctx->Q32.p, s);
-  if (hipEvent_t ev = timing_ev(tc, 1)) HIP_TRY(hipEventRecord(ev, s));
+  // launch_cand records the "cand" events with the kernel's own dispatch
+  // (hipExtLaunchKernelGGL), so that phase is the kernel alone (the seed pass
+  // and threshold fill fall into "prep"); the streamed kernels get separate
+  // event records around them
+  const bool ev_ext = !s3 && timing_ev(tc, 1) && timing_ev(tc, 2);
+  if (hipEvent_t ev = timing_ev(tc, 1); ev && !ev_ext) HIP_TRY(hipEventRecord(ev, s));
   CandLaunch cl{};
+  if (ev_ext) {
+    cl.ev_start = timing_ev(tc, 1);
+    cl.ev_stop = timing_ev(tc, 2);
+  }
   cl.metric = kmetric;
   cl.DP = DP;
   cl.R = R;
@@ -1080,6 +1089,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
       cs.out_i = (int*)ctx->smp_i.p;
       cs.gthr = nullptr;
       cs.ablate = 0;
+      cs.ev_start = cs.ev_stop = nullptr;
       if (launch_cand(cs, s)) {
         launch_seed_gthr((const float*)ctx->smp_v.p, m_pad, Us, gk ? G * gk : 4 * R, active,
                          cl.gthr, s);
@@ -1099,7 +1109,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   else if (!launch_cand(cl, s))
     return knn_fail(KNN_ERR_ARG, "no candidate kernel for this geometry (tuning overrides?)");
   HIP_TRY(hipGetLastError());
-  if (hipEvent_t ev = timing_ev(tc, 2)) HIP_TRY(hipEventRecord(ev, s));
+  if (hipEvent_t ev = timing_ev(tc, 2); ev && !ev_ext) HIP_TRY(hipEventRecord(ev, s));
   // the rescan / tie counters (the int8 query builder cleared them already)
   if (kmetric < 5) HIP_TRY(hipMemsetAsync(ctx->rescan_cnt.p, 0, 4 * sizeof(int), s));
   // per-split certification: a query failing only through some splits'

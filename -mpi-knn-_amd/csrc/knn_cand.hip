@@ -703,6 +703,7 @@ bool launch_cand(const CandLaunch& c, hipStream_t s) {
   if (c.DP == v) return launch_res_##v(c, s);
   KNN_DP_LIST(KNN_CASE)
 #undef KNN_CASE
+  if (c.ev_start) (void)hipEventRecord(c.ev_start, s);
   if (c.R == 8) {
     if (c.metric == 1) launch_str<8, 1>(c, s);
     else launch_str<8, 0>(c, s);
@@ -710,6 +711,7 @@ bool launch_cand(const CandLaunch& c, hipStream_t s) {
     if (c.metric == 1) launch_str<16, 1>(c, s);
     else launch_str<16, 0>(c, s);
   }
+  if (c.ev_stop) (void)hipEventRecord(c.ev_stop, s);
   return true;
 }
 

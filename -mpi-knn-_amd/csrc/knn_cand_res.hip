@@ -3,6 +3,8 @@
 // many (DP, R, metric, waves) instantiations build in parallel.
 #include "knn_device.h"
 
+#include <hip/hip_ext.h>
+
 // Staging geometry (build-time; tools/build_variant.sh overrides for A/B):
 // 2 LDS buffers of 64-row tiles (two 32-row MFMA sub-tiles per barrier).
 // Measured against 3 buffers of 32-row tiles: -5.5 % (bf16x3) / -3 % (fp32).
@@ -1268,10 +1270,16 @@ static void with_M(int M, F f) {
 
 template <int DP, int R, int METRIC, int NW>
 static void launch_res(const CandLaunch& c, hipStream_t s) {
-  hipLaunchKernelGGL((cand_kernel<DP, R, METRIC, NW>), dim3((unsigned)(c.n_qt * c.S)),
-                     dim3(NW * 64), 0, s, c.X32, c.Q32, (int)(c.n_pad / (kTR * res_tpb<METRIC>())), c.S,
-                     c.n_qt,
-                     c.out_v, c.out_i, c.ablate, c.gthr, c.gk, c.xsw, c.qstart, c.gmask, c.qblk);
+  const int nt = (int)(c.n_pad / (kTR * res_tpb<METRIC>()));
+  if (c.ev_start)
+    hipExtLaunchKernelGGL((cand_kernel<DP, R, METRIC, NW>), dim3((unsigned)(c.n_qt * c.S)),
+                          dim3(NW * 64), 0, s, c.ev_start, c.ev_stop, 0, c.X32, c.Q32, nt, c.S,
+                          c.n_qt, c.out_v, c.out_i, c.ablate, c.gthr, c.gk, c.xsw, c.qstart,
+                          c.gmask, c.qblk);
+  else
+    hipLaunchKernelGGL((cand_kernel<DP, R, METRIC, NW>), dim3((unsigned)(c.n_qt * c.S)),
+                       dim3(NW * 64), 0, s, c.X32, c.Q32, nt, c.S, c.n_qt,
+                       c.out_v, c.out_i, c.ablate, c.gthr, c.gk, c.xsw, c.qstart, c.gmask, c.qblk);
 }
 
 // Instantiated variants: R in {4, 8, 16}; METRIC 0/2 with NW in {4, 8};

@@ -131,6 +131,10 @@ struct CandLaunch {
   const int* qstart = nullptr;
   int gmask = 7;   // slot groups of gthr - 1: a split publishes into slot split & gmask
   int qblk = 0;    // workgroup order: 0 split-major, B: query blocks of B tiles (cand_kernel)
+  // "cand" timing events recorded by the resident kernel's own dispatch
+  // (hipExtLaunchKernelGGL), so the phase is the kernel's execution as
+  // rocprofv3 times it (profiles/ab_log.md r6u); null: none
+  hipEvent_t ev_start = nullptr, ev_stop = nullptr;
 };
 constexpr uint32_t kGthrInit = 0xFF800000u;  // order-preserving key of +inf
 constexpr int kGthrSlots = 8;                // slots per query in gthr
