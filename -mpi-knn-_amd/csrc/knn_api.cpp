@@ -476,6 +476,9 @@ static int ensure_i8(knn_ctx* ctx, int kmetric, hipStream_t s) {
 // The fp16 S3 image (d > 256, cand_s3_kernel<R, true>): 2^jx (x - mu) in
 // fp16 tile-chunk images + the L2 seeds; the representation error measured
 // as for the resident copy.
+// AUTO for the query-resident fp16 kernel (d > 256; profiles/ab_log.md r6v)
+constexpr bool kQresAuto = false;
+
 static int ensure_fp16_s3(knn_ctx* ctx, hipStream_t s) {
   const TrainDev& t = ctx->train;
   const int DPs = pad_dim_fp16_s3(t.d);
@@ -484,7 +487,8 @@ static int ensure_fp16_s3(knn_ctx* ctx, hipStream_t s) {
   int rc;
   const int64_t n3 = (t.n + kS3Rows - 1) / kS3Rows * kS3Rows;
   if ((rc = ctx->XT16.ensure((size_t)n3 * DPs * 2))) return rc;
-  if ((rc = ctx->XS16.ensure((size_t)n3 * sizeof(float)))) return rc;
+  // (+1 KB: cand_qres_kernel stages a sub-tile's 32 seeds as one 1-KB piece)
+  if ((rc = ctx->XS16.ensure((size_t)n3 * sizeof(float) + 1024))) return rc;
   unsigned long long* st_d = (unsigned long long*)ctx->stats.p + 3;
   HIP_TRY(hipMemsetAsync(st_d, 0, 8, s));
   launch_prep_half_tiled(t.X64, t.mu, t.n, t.d, DPs, n3, t.jx, 1.0, (unsigned short*)ctx->XT16.p,
@@ -903,6 +907,10 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   const int s3q_S = (W * 5 + 15) / 16;
   const bool s3q = s3h && ctx->tune_s3q != 0 && s3q_S <= kMaxUnion / 32 && s3q_S <= n_tiles;
   choose_geometry(ctx, kmetric, s3, DP, nw, n_qt, n_tiles, W, C, s3q, S, R);
+  // the query-resident kernel in place of S3's q16 form (same images, lists
+  // and thresholds; knn_cand_qres.hip); tuning key "qres": -1 auto (kQresAuto),
+  // 0 off, 1 on where supported
+  const bool qres = s3q && qres_supported(DP) && (ctx->tune_qres < 0 ? kQresAuto : ctx->tune_qres > 0);
   // metric 6: 4 lists of R = 4 per query per split (two per lane, one per
   // half of its rows: knn_cand_res.hip, KNN_I8W_Q4), the quad layout of the
   // 16x16 kernels; tuning "R" = 8 selects one list of 8 per lane (2 per
@@ -959,12 +967,14 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   if ((rc = ctx->rescan_nkeep.ensure((size_t)cap * sizeof(int) + 16))) return rc;
 
   ctx->last_kmetric = kmetric;
-  ctx->geom[0] = (int64_t)n_qt * S;
+  ctx->geom[0] = (int64_t)(qres ? 2 * n_qt : n_qt) * S;  // (qres: workgroup tiles of 128 queries)
   ctx->geom[1] = S;
   ctx->geom[2] = R;
   ctx->last_nw = nw;
   ctx->geom[3] = C;
-  if (s3)
+  if (qres)
+    snprintf(ctx->last_kernel, sizeof ctx->last_kernel, "cand_qres_kernel<%d>", DP / 32);
+  else if (s3)
     snprintf(ctx->last_kernel, sizeof ctx->last_kernel, "cand_s3_kernel<%d,%s,%s>", R,
              s3h ? "true" : "false", s3q ? "true" : "false");
   else if (DP <= 256)
@@ -1044,7 +1054,7 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   // (hipExtLaunchKernelGGL), so that phase is the kernel alone (the seed pass
   // and threshold fill fall into "prep"); the streamed kernels get separate
   // event records around them
-  const bool ev_ext = !s3 && timing_ev(tc, 1) && timing_ev(tc, 2);
+  const bool ev_ext = (!s3 || qres) && timing_ev(tc, 1) && timing_ev(tc, 2);
   if (hipEvent_t ev = timing_ev(tc, 1); ev && !ev_ext) HIP_TRY(hipEventRecord(ev, s));
   CandLaunch cl{};
   if (ev_ext) {
@@ -1098,7 +1108,12 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
     }
     if (!seeded && kmetric < 5) launch_fill_gthr(cl.gthr, m_pad, active, s);
   }
-  if (s3h)
+  if (qres) {
+    if (!launch_cand_qres((const unsigned short*)ctx->XT16.p, (const float*)ctx->XS16.p,
+                          (const unsigned short*)ctx->Q32.p, DP, n_pad3, S, n_qt, cl.out_v, cl.out_i,
+                          cl.gthr, gk, s, cl.ev_start, cl.ev_stop))
+      return knn_fail(KNN_ERR_ARG, "no query-resident kernel for this dimension");
+  } else if (s3h)
     launch_cand_s3h((const unsigned short*)ctx->XT16.p, (const float*)ctx->XS16.p,
                     (const unsigned short*)ctx->Q32.p, DP, n_pad3, R, S, n_qt, cl.out_v, cl.out_i,
                     cl.ablate, s3q, cl.gthr, gk, s, ctx->tune_s3gq > 0 ? ctx->tune_s3gq : kS3GqMax);
@@ -1585,6 +1600,9 @@ int knn_set_tuning(knn_ctx* ctx, const char* key, int64_t value) {
   } else if (!strcmp(key, "S")) {
     if (value < 0 || value > 64) return knn_fail(KNN_ERR_ARG, "S must be 0 (auto) .. 64");
     ctx->tune_S = (int)value;
+  } else if (!strcmp(key, "qres")) {
+    if (value < -1 || value > 1) return knn_fail(KNN_ERR_ARG, "qres must be -1, 0 or 1");
+    ctx->tune_qres = (int)value;
   } else if (!strcmp(key, "s3q")) {
     if (value < -1 || value > 1) return knn_fail(KNN_ERR_ARG, "s3q must be -1, 0 or 1");
     ctx->tune_s3q = (int)value;

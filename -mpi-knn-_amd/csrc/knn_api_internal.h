@@ -59,6 +59,7 @@ struct knn_ctx {
   int tune_ablate = 0;         // timing-only kernel ablations
   int tune_nw = 0;             // resident kernel waves per workgroup (0 = auto)
   int tune_s3q = -1;           // fp16 S3 on the 16x16x32 layout: -1 auto, 0 off, 1 on
+  int tune_qres = -1;          // query-resident fp16 kernel for d > 256 (knn_cand_qres.hip): -1 auto, 0 off
   int tune_gk = -1;            // what the lists publish into gthr (-1 auto, 0 list R-th, 1..16)
   int tune_xhswz = 1;          // fp16 train image chunk swizzle (xh_swz): 1 on, 0 off (A/B)
   int tune_fp16 = -1;          // fp16 candidate pass: -1 auto, 0 off, 1 on

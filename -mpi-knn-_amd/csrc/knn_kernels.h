@@ -86,6 +86,13 @@ void launch_cand_s3h(const unsigned short* XT, const float* XS, const unsigned s
                      bool q16, uint32_t* gthr, int gk, hipStream_t s, int gq_max = kS3GqMax);
 int s3h_blocks_per_cu(int R);
 int s3q_blocks_per_cu();
+// query-resident fp16 kernel for d > 256 (knn_cand_qres.hip): the S3 q16
+// kernel's outputs from the same images, 2 n_qt workgroup tiles of 128
+// queries; false: no instantiation for DP (run S3)
+bool qres_supported(int DP);
+bool launch_cand_qres(const unsigned short* XT, const float* XS, const unsigned short* QT, int DP,
+                      int64_t n_pad, int S, int n_qt, float* out_v, int* out_i, uint32_t* gthr, int gk,
+                      hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop);
 // S3 workgroup grouping for n_qt query tiles and S splits (knn_cand.hip, s3_map)
 int s3_group(int n_qt, int S, int gq_max = kS3GqMax);
 int pad_dim_fp16_s3(int d);         // padded dim of the fp16 S3 image (multiple of 32, > 256)

@@ -299,7 +299,7 @@ class Classifier:
 
     def set_tuning(self, key, value):
         """Experiment overrides (knn_amd.h, knn_set_tuning): "R", "S", "nw",
-        "ablate", "fp16", "mfma16", "i8", "i8w", "gk", "s3q", "s3gq", "xhswz",
+        "ablate", "fp16", "mfma16", "i8", "i8w", "gk", "s3q", "qres", "s3gq", "xhswz",
         "ties", "seed", "order", "ophase", "nblk"; 0 (or -1 where stated) =
         automatic.  "order" and "nblk" shape the train layout and are read by
         set_train: "order" -1 = region order only for integer-coded sets whose

@@ -267,7 +267,10 @@ const char* knn_last_kernel_name(knn_ctx* ctx);
  * knn_set_train*, whose norm blocks interleave the rows over that kernel's
  * lane lists -- set it before the train set: a later change keeps results
  * exact but loses the interleave's certification odds), "mfma16" (bf16x3 on the 16x16x32 layout: 0
- * off, 1 on), "s3q" (the fp16 d > 256 kernel on 16x16x32: 0 off, 1 on) and
+ * off, 1 on), "s3q" (the fp16 d > 256 kernel on 16x16x32: 0 off, 1 on), "qres"
+ * (1: where "s3q" runs and d pads to 32 x {9, 10, 12, 14, 16, 18, 20, 24,
+ * 25, 28, 30}, the query-resident kernel replaces it -- queries held in
+ * registers, rows streamed; 0 off: S3; -1 auto) and
  * "gk" (what the global threshold exchange publishes: 0 the lists' R-th
  * entries (resident kernel) / no exchange (S3), K = 1..16 the K-th smallest
  * of a workgroup's union of a query's lists; results stay exact); "ties"

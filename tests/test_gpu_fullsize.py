@@ -232,17 +232,20 @@ def test_cfg3_shard_1m_queries(knn):
 
 def test_cfg5_d960_k100(knn):
     """configs[4] at its full 10k-query batch: the benchmarked launch geometry
-    (40 query tiles of 256, the s3_map XCD groups over 1280 workgroups)."""
+    (the query-resident kernel: 80 query tiles of 128 x 32 splits), then the
+    S3 kernel's forms (40 query tiles of 256, the s3_map XCD groups) and the
+    bf16x3 S3 kernel with the same exact answer."""
     n, m, d, k, C = 1_000_000, 10_000, 960, 100, 10
     X, lab, Q, _ = bench.synth(n, m, d, C, 4321, 8765, DEV)
     torch.cuda.synchronize()
     clf = knn.Classifier(0)
     clf.set_train_device(X.data_ptr(), lab.data_ptr(), n, d, C, keep=(X, lab))
+    clf.set_tuning("qres", 1)
     got, idx, dist, flags = classify(knn, clf, Q, k)
-    assert clf.last_candidate_path() == 4, "cfg5 should run the fp16 candidate pass (S3 kernel)"
-    assert clf.last_kernel_name() == "cand_s3_kernel<8,true,true>"
+    assert clf.last_candidate_path() == 4, "cfg5 should run the fp16 candidate pass"
+    assert clf.last_kernel_name() == "cand_qres_kernel<30>"
     geom = clf.last_geometry()
-    assert geom["workgroups"] == 40 * geom["splits"], geom  # 40 query tiles of 256
+    assert geom["workgroups"] == 80 * geom["splits"], geom  # 80 query tiles of 128
     assert clf.last_rescan_count() * 16 <= m
     lab_all = lab.cpu().numpy()
     sample = np.arange(0, m, 4)                  # 2,500 queries
@@ -250,8 +253,13 @@ def test_cfg5_d960_k100(knn):
     check_optimal(X, Q, k, dist, np.arange(m))
     check_oracle(X, lab_all, Q, k, got, idx, dist, np.arange(0, m, m // 8))
     check_tie_votes(knn, X, lab_all, Q, k, got, flags)
-    # the fp16 S3 kernel on 32x32x16 and the bf16x3 S3 kernel give the same
-    # exact answer
+    # the fp16 S3 kernel on 16x16x32 and on 32x32x16 and the bf16x3 S3 kernel
+    # give the same exact answer
+    clf.set_tuning("qres", 0)
+    gotq, _, distq, _ = classify(knn, clf, Q, k)
+    assert clf.last_kernel_name() == "cand_s3_kernel<8,true,true>"
+    np.testing.assert_array_equal(gotq, got)
+    assert (distq.view(np.int64) == dist.view(np.int64)).all()
     clf.set_tuning("s3q", 0)
     gotw, _, distw, _ = classify(knn, clf, Q, k)
     assert clf.last_kernel_name() == "cand_s3_kernel<8,true,false>"

@@ -668,16 +668,39 @@ def test_global_threshold_ranks(knn, gk):
     c.close()
 
 
+@pytest.mark.parametrize("qres", [1, 0])
 @pytest.mark.parametrize("gk", [0, 1, 6, 16])
-def test_s3_global_threshold_ranks(knn, gk):
-    """The fp16 S3 kernel on 16x16x32 (d > 256) with its global threshold off
-    (gk 0) and published at ranks 1, 6 and 16 of each workgroup's quad union."""
+def test_s3_global_threshold_ranks(knn, gk, qres):
+    """The fp16 d > 256 kernels with quad lists -- the query-resident kernel
+    (qres 1) and S3 on 16x16x32 (qres 0) -- with the global
+    threshold off (gk 0) and published at ranks 1, 6 and 16 of each
+    workgroup's quad union."""
     rng = np.random.default_rng(50 + gk)
     tr, lab, te = _mix(rng, 6000, 300, 300, 5)
     c = knn.Classifier(0)
     c.set_precision(knn.PRECISION_FP16)
     c.set_tuning("gk", gk)
+    c.set_tuning("qres", qres)
     run_case(c, knn, tr, lab, te, 40, 0, 5)
+    assert c.last_kernel_name() == ("cand_qres_kernel<10>" if qres else "cand_s3_kernel<8,true,true>")
+    c.close()
+
+
+@pytest.mark.parametrize("d", [260, 300, 500, 784, 960])
+def test_query_resident_dims(knn, d):
+    """The query-resident fp16 kernel (knn_cand_qres.hip) at padded widths 288,
+    320, 512, 800 and 960 (9, 10, 16, 25 and 30 chunks: its chunkings of 3, 2
+    and 5 k-steps) on ragged n and m, against the oracle; the S3 kernel gives
+    the same answer."""
+    rng = np.random.default_rng(900 + d)
+    tr, lab, te = _mix(rng, 3001, 301, d, 6)
+    c = knn.Classifier(0)
+    c.set_precision(knn.PRECISION_FP16)
+    c.set_tuning("qres", 1)
+    run_case(c, knn, tr, lab, te, 12, 0, 6)
+    assert c.last_kernel_name() == "cand_qres_kernel<%d>" % ((d + 31) // 32)
+    c.set_tuning("qres", 0)
+    run_case(c, knn, tr, lab, te, 12, 0, 6)
     assert c.last_kernel_name() == "cand_s3_kernel<8,true,true>"
     c.close()
 

@@ -16,15 +16,18 @@ for g in ${VGROUPS:-0 1 2 3}; do
   /opt/rocm/bin/hipcc $HIPFLAGS "$@" -DKNN_GROUP=$g -c csrc/knn_cand_res.hip -o build/$name/res_$g.o 2>/dev/null &
 done
 [ "${VCAND:-1}" = 0 ] || /opt/rocm/bin/hipcc $HIPFLAGS "$@" -c csrc/knn_cand.hip -o build/$name/cand.o 2>/dev/null &
+rm -f build/$name/qres.o
+[ "${VQRES:-1}" = 0 ] || /opt/rocm/bin/hipcc $HIPFLAGS "$@" -c csrc/knn_cand_qres.hip -o build/$name/qres.o 2>/dev/null &
 wait
 [ -f build/$name/cand.o ] || cp build/knn_cand.o build/$name/cand.o
+[ -f build/$name/qres.o ] || cp build/knn_cand_qres.o build/$name/qres.o
 # a group whose kernels do not fit the variant's geometry (LDS) keeps the
 # default build's objects, so the library still links completely
 for g in 0 1 2 3; do
   [ -f build/$name/res_$g.o ] || cp build/knn_cand_res_$g.o build/$name/res_$g.o
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o lib/libknn_amd_$name.so \
-  build/knn_prep.o build/$name/cand.o build/knn_select.o build/knn_order.o build/$name/res_*.o \
+  build/knn_prep.o build/$name/cand.o build/$name/qres.o build/knn_select.o build/knn_order.o build/$name/res_*.o \
   build/knn_normalize.o build/knn_api.o build/knn_group.o \
   -L/opt/rocm/lib -lamdhip64 -lrccl -Wl,-rpath,/opt/rocm/lib
 echo "built lib/libknn_amd_$name.so"

@@ -16,7 +16,13 @@
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int DP = 960, DPF = DP / 2, RSF = DPF + 4;  // floats per row (odd 16-B stride)
+#ifndef RPAD
+#define RPAD 8
+#endif
+// floats per row: 488 (RPAD 8) makes the 16x16 fragment reads conflict-free
+// (484, the odd 16-B stride of the 32x32 layouts, is 2-way here: measured
+// SQ_LDS_BANK_CONFLICT = 4 cycles per ds_read_b128)
+constexpr int DP = 960, DPF = DP / 2, RSF = DPF + RPAD;
 #ifndef TRT
 #define TRT 32
 #endif

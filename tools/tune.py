@@ -34,7 +34,7 @@ import bench  # noqa: E402
 from test_gpu_fullsize import brute_force_kdist  # noqa: E402  (torch fp64 GEMM, not the oracle)
 
 DEFAULTS = {"gk": -1, "s3q": -1, "xhswz": 1, "i8": -1, "i8w": -1, "seed": 0, "ophase": -1, "s3gq": 0,
-            "gg": -1, "qblk": 0, "i8resc": -1}
+            "gg": -1, "qblk": 0, "i8resc": -1, "qres": -1}
 
 
 def apply_variant(knn, clf, v):
