@@ -15,6 +15,13 @@
 // (xcd_remap: consecutive query tiles of one split) share the row stream in
 // L2, and the queries are read once.
 //
+// Measured (profiles/ab_log.md r6v-r6w): SLOWER than S3 at cfg5 -- 24.0 ms
+// against 19.9-20.1 ms in the same process, although its bare loop (no
+// selection) runs 16.6 ms.  With one wave per SIMD nothing hides the
+// selection's VALU work (k = 100: 4 lists of 8 per query per split), which
+// S3's second wave per SIMD overlaps with MFMAs.  Opt-in (tuning "qres" 1;
+// AUTO off, kQresAuto in knn_api.cpp); parity-tested like every path.
+//
 // Outputs are the S3 q16 kernel's exactly: the 16x16 layout's quad lists of
 // R = 8 per query per split (split s = 256-row tiles s, s + S, ...: the same
 // row sets, so the merge, the certification and the targeted rescan are
@@ -35,12 +42,18 @@ namespace knnk {
 // passes) after them: with one wave per SIMD nothing else hides the
 // selection's VALU work; 0 none (timing only, results invalid)
 #ifndef KNN_QRES_SEL
-#define KNN_QRES_SEL 2
+#define KNN_QRES_SEL 1
 #endif
-// workgroup order: 1 xcd_remap (an XCD's concurrent workgroups are
-// consecutive query tiles of one split), 0 dispatch order
+// workgroup order: 2 (S % 8 == 0; else 1) XCD x runs splits x, x + 8, x +
+// 16, ... -- split-major over the query tiles, so its concurrent workgroups
+// share one split's row stream in its L2, and every query tile's first
+// workgroups cover all 8 slot groups of the global threshold (split % 8) at
+// once: its threshold is finite after their first exchanges, and later
+// workgroups start with it (KNN_X_START); 1 xcd_remap (an XCD's range of
+// consecutive logical ids: the first rounds hold only splits = 0 or 4 mod 8,
+// no query's threshold is finite until every group has run); 0 dispatch order
 #ifndef KNN_QRES_REMAP
-#define KNN_QRES_REMAP 1
+#define KNN_QRES_REMAP 2
 #endif
 
 template <int NCH>
@@ -61,8 +74,16 @@ cand_qres_kernel(const unsigned short* XT, const float* XS, const unsigned short
   __shared__ __attribute__((aligned(16))) unsigned char lds[2 * SUBB];
   __shared__ __attribute__((aligned(16))) u32x4 gls[4 * 64];
 
-  const int bid = KNN_QRES_REMAP ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-  const int split = bid / n_qt, qt = bid - split * n_qt;
+  int split, qt;
+  if (KNN_QRES_REMAP == 2 && (S & 7) == 0) {
+    const int r = blockIdx.x >> 3, j = r / n_qt;  // (gridDim.x = n_qt S, a multiple of 8)
+    qt = r - j * n_qt;
+    split = 8 * j + (blockIdx.x & 7);
+  } else {
+    const int bid = KNN_QRES_REMAP ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    split = bid / n_qt;
+    qt = bid - split * n_qt;
+  }
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c16 = lane & 15, g16 = lane >> 4, h = lane >> 5;
