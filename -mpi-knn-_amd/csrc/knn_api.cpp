@@ -885,6 +885,9 @@ int knn_run_search(knn_ctx* ctx, const double* dQ, int64_t m, int W, int metric,
   if (DP <= 256 && kmetric != 1) nw = ctx->tune_nw ? std::min(ctx->tune_nw, 8) : (m >= 4096 ? 8 : 4);
   if (kmetric >= 3) nw = 8;  // (the 16x16 layouts: fp16, bf16x3, int8)
   if (kmetric == 4 && !s3 && ctx->tune_nw) nw = ctx->tune_nw;  // 4, 8 or 16
+  // int8 32x32x32: 16 waves (512 queries per staged tile) only in builds
+  // with KNN_I8W_NW16 (otherwise the launch is refused: no such kernel)
+  if (kmetric == 6 && ctx->tune_nw == 16) nw = 16;
   // queries per wave of the resident kernel (int8: 16 x the build's query
   // blocks); the int8 kernel with 64 queries per wave also runs 4 waves
   const int qpw = !s3 && DP <= 256 ? cand_queries_per_wave(kmetric, DP) : 32;

@@ -127,6 +127,12 @@ static_assert(KNN_RES_TPB * knnk::kTR == knnk::kResTileRows || KNN_RES_TPB != 2,
 #ifndef KNN_I8W_PF
 #define KNN_I8W_PF 0
 #endif
+// metric 6 (experiment): also a 16-wave form (512 queries per staged tile:
+// half the L2 -> LDS staging bytes per MFMA; one workgroup per CU), selected
+// with tuning "nw" 16
+#ifndef KNN_I8W_NW16
+#define KNN_I8W_NW16 0
+#endif
 // metric 6: barrier-free staging (experiment).  Instead of one s_barrier per
 // staged tile, each buffer carries two LDS counters: ready (waves whose
 // pieces of the buffer's tile have landed) and done (waves that finished
@@ -1298,8 +1304,10 @@ constexpr bool kI8WQuad = KNN_I8W_Q4 && KNN_I8_ILIST && KNN_I8_SMAX;
 template <int DP, int R, int M, int NW>
 constexpr bool res_variant() {
   return (M != 6 || R != 4 || kI8WQuad) && (M != 2 || DP % 16 == 0) && (M != 1 || (NW == 4 && R != 4)) &&
-         (M < 3 || (DP % 32 == 0 && (R == 4 || (M >= 5 && R == 8)) && (NW == 8 || M >= 4))) && (NW != 16 || M == 4) &&
-         (M != 5 || (DP % 64 == 0 && (NW == 8 || NW == 4))) && (M != 6 || (NW == 8 && (R == 4 || R == 8)));
+         (M < 3 || (DP % 32 == 0 && (R == 4 || (M >= 5 && R == 8)) && (NW == 8 || M >= 4))) &&
+         (NW != 16 || M == 4 || (M == 6 && KNN_I8W_NW16 && R == 4 && DP <= 128)) &&
+         (M != 5 || (DP % 64 == 0 && (NW == 8 || NW == 4))) &&
+         (M != 6 || ((NW == 8 || (NW == 16 && KNN_I8W_NW16)) && (R == 4 || R == 8)));
 }
 
 template <int DP>

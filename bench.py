@@ -249,6 +249,8 @@ def pmc_traffic(kernel, workload, src_sha):
             continue
         if wl.get("data", "grid") != workload.get("data", "grid"):
             continue
+        if wl.get("tuning") != workload.get("tuning"):  # (a profiled tuning variant)
+            continue
         if rec.get("kernel_src_sha") != src_sha:
             continue
         kr = rec.get("kernels", {}).get(kernel)
@@ -922,6 +924,9 @@ def _main():
                     help="candidate pass of the main leg (profiling of the fp32 / fp16 kernels)")
     ap.add_argument("--order", type=int, default=-1,
                     help="region order of the train layout (tuning key 'order': -1 auto, 0 off)")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="extra knn_set_tuning key of the main leg (profiling of a variant, "
+                         "e.g. qres=1 for the query-resident d > 256 kernel); repeatable")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU/gloo plumbing check with a torch stand-in (no measurement)")
     args = ap.parse_args()
@@ -985,6 +990,9 @@ def _main():
         phase("set_train (main leg)")
         t0 = time.perf_counter()
         clf.set_tuning("order", args.order)
+        for kv in args.tune:
+            key, val = kv.split("=")
+            clf.set_tuning(key, int(val))
         clf.set_train_device(X.data_ptr(), lab.data_ptr(), n, d, C, keep=(X, lab))
         sync()
         extra["set_train_ms"] = (time.perf_counter() - t0) * 1e3
@@ -1189,6 +1197,8 @@ def _main():
     kname = main_r["kernel"]
     src_sha = kernel_src_sha()
     wl = {"n_train": n_rank, "queries": m_rank, "dim": d, "k": k, "data": args.data}
+    if args.tune:
+        wl["tuning"] = ",".join(args.tune)
     traffic, traffic_src = pmc_traffic(kname, wl, src_sha)
     result = {
         "metric": METRIC,
@@ -1212,7 +1222,8 @@ def _main():
                    "rerank": "fp64 exact (reference arithmetic), certified; labels exact",
                    "geometry": main_r["geom"], "rescanned_queries": main_r["resc"],
                    "full_scan_queries": main_r["full_scans"],
-                   "tie_reordered_queries": main_r["tie_reordered"]},
+                   "tie_reordered_queries": main_r["tie_reordered"],
+                   **({"tuning": list(args.tune)} if args.tune else {})},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                      "frac": achieved / peak, "traffic": traffic,
                      "traffic_unit": "bytes per launch (HBM, PMC)", "traffic_source": traffic_src,

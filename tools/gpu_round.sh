@@ -91,6 +91,24 @@ if [ -n "$AB_SETS" ]; then
     done
   done
 fi
+# AB_PAIRS: "<variant>|<tune.py arguments>" pairs separated by ';' (a library
+# variant with arguments of its own, e.g. a tuning only that build has),
+# each gated first, then REPS interleaved rounds -> $TAG_pair<i>_<rep>.log
+if [ -n "$AB_PAIRS" ]; then
+  IFS=';' read -ra pairs <<< "$AB_PAIRS"
+  for p in "${pairs[@]}"; do run_gate "${p%%|*}" "${p#*|}" || exit 1; done
+  for rep in $(seq 1 ${REPS:-2}); do
+    i=0
+    for p in "${pairs[@]}"; do
+      i=$((i + 1)); v=${p%%|*}
+      if [ $v = base ]; then unset KNN_AMD_VARIANT; else export KNN_AMD_VARIANT=$v; fi
+      timeout -k 10 300 python3 -u tools/tune.py ${p#*|} > $O/${TAG}_pair${i}_$rep.log 2>&1
+      rc=$?; echo "pair $i ($p) $rep rc=$rc"; grep " cand " $O/${TAG}_pair${i}_$rep.log
+      [ $rc = 0 ] || exit $rc
+    done
+  done
+  unset KNN_AMD_VARIANT
+fi
 # BENCH_SETS: bench.py argument sets separated by ';' (20 timed steps each,
 # main leg only), REPS rounds -> $TAG_bset<i>_<rep>.json
 if [ -n "$BENCH_SETS" ]; then

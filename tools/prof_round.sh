@@ -8,6 +8,7 @@
 #           (ncclSend / ncclRecv of the tie all-to-all included)
 #   PART=B  FETCH_SIZE / WRITE_SIZE passes of the same workloads
 #   PART=S  the two SQ passes over cfg2 and over the cfg4s shard
+#   PART=Q  cfg5 on the query-resident kernel: trace, FETCH/WRITE, SQ passes
 # Outputs under gpurun_out/prof_$TAG and gpurun_out/pmc_sq_$TAG[_cfg4s];
 # tools/profiles_commit.py --tag $TAG turns them into profiles/.
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -19,6 +20,9 @@ mkdir -p "$OUT"
 for part in ${PART:-A}; do
 case "$part" in
   A) bash tools/profile_all.sh stats api cfg4s cfg5 cfg2c cfg2f32 || exit $? ;;
+  # (the query-resident cfg5 kernel: trace, traffic and SQ passes)
+  Q) bash tools/profile_all.sh stats pmc cfg5q || exit $?
+     TAG=${TAG}_cfg5q WLARGS="--steps 2 --warmup 1 --dim 960 --k 100 --tune qres=1" bash tools/pmc_sq2.sh || exit $? ;;
   R) timeout -k 10 300 rocprofv3 --rccl-trace --kernel-trace --stats -d "$OUT/rccl" -o run --output-format csv -- \
        python3 -m pytest -x -q -m gpu --timeout 200 tests/test_gpu_sharded.py -k True \
        > "$OUT/rccl.log" 2>&1 || exit $?

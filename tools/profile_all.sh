@@ -5,7 +5,7 @@
 #          HBM section; each pass its own run, --kernel-trace only)
 #   api    rocprofv3 --hip-trace of a short cfg2 bench: the HIP calls made
 #          inside the timed knn_classify_device loop (no stream syncs)
-# Usage: TAG=r2 tools/profile_all.sh [stats] [pmc] [api] [cfg4] [cfg4s] [cfg5] [cfg2c] [cfg2f32]
+# Usage: TAG=r2 tools/profile_all.sh [stats] [pmc] [api] [cfg4] [cfg4s] [cfg5] [cfg5q] [cfg2c] [cfg2f32]
 # Outputs under gpurun_out/prof_$TAG/; tools/profiles_commit.py turns them
 # into the committed profiles/ files.  Every GPU step has its own time limit
 # and a failing step ends the script.
@@ -22,6 +22,8 @@ declare -A WL
 WL[cfg2]="--steps 10 --warmup 2"
 WL[cfg4]="--steps 3 --warmup 1 --mode train --n-train 100000000 --dim 96 --queries 10000"
 WL[cfg5]="--steps 4 --warmup 1 --dim 960 --k 100"
+# cfg5 on the query-resident fp16 kernel (tuning "qres" 1; AUTO keeps S3)
+WL[cfg5q]="--steps 4 --warmup 1 --dim 960 --k 100 --tune qres=1"
 # the general-data kernels: fp16 on continuous (min-max normalised) data and
 # the fp32 path, each as the main leg
 WL[cfg2c]="--steps 10 --warmup 2 --data continuous"
@@ -38,7 +40,7 @@ run() {  # run <name> <limit> <cmd...>
   [ $rc -eq 0 ] || exit $rc
 }
 cfgs="cfg2"
-for a in "$@"; do case $a in cfg4|cfg5|cfg4s|cfg2c|cfg2f32) cfgs="$cfgs $a" ;; esac; done
+for a in "$@"; do case $a in cfg4|cfg5|cfg5q|cfg4s|cfg2c|cfg2f32) cfgs="$cfgs $a" ;; esac; done
 for a in "$@"; do
   case $a in
     stats)

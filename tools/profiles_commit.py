@@ -35,6 +35,9 @@ WORKLOADS = {
     "cfg2": dict(steps=10, warmup=2, n_train=1_000_000, queries=10_000, dim=128, k=10),
     "cfg4": dict(steps=3, warmup=1, n_train=100_000_000, queries=10_000, dim=96, k=10),
     "cfg5": dict(steps=4, warmup=1, n_train=1_000_000, queries=10_000, dim=960, k=100),
+    # cfg5 on the query-resident fp16 kernel (tuning "qres" 1)
+    "cfg5q": dict(steps=4, warmup=1, n_train=1_000_000, queries=10_000, dim=960, k=100,
+                  tuning="qres=1"),
     "cfg4s": dict(steps=5, warmup=1, n_train=12_500_000, queries=10_000, dim=96, k=10),
     "cfg2c": dict(steps=10, warmup=2, n_train=1_000_000, queries=10_000, dim=128, k=10,
                   data="continuous"),
@@ -115,7 +118,7 @@ def main():
         if os.path.isdir(fdir) and os.path.isdir(wdir):
             fetch = traffic_json.per_launch(fdir, "FETCH_SIZE")
             write = traffic_json.per_launch(wdir, "WRITE_SIZE")
-            tr = {"workload": {key: wl[key] for key in ("n_train", "queries", "dim", "k", "data")
+            tr = {"workload": {key: wl[key] for key in ("n_train", "queries", "dim", "k", "data", "tuning")
                                if key in wl},
                   "kernel_src_sha": bench.kernel_src_sha(),
                   "formula": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE half-count "
