@@ -20,6 +20,12 @@
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 
+#ifndef NOLDS
+#define NOLDS 0
+#endif
+#ifndef NOBAR
+#define NOBAR 0
+#endif
 #ifndef PF
 #define PF 0
 #endif
@@ -75,6 +81,18 @@ bare(const char* __restrict__ X, const char* Q, int n_tiles, int S, int n_qt, in
       qf[qh][ks] = v;
     }
   }
+  // (NOLDS 3: 8 fragments of random rows in registers stand in for the rows:
+  // every MFMA gets an A operand unlike its neighbours' and unlike B)
+  i32x4 rf[NOLDS == 3 ? 8 : 1];
+  if constexpr (NOLDS == 3) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      i32x4 v;
+      asm volatile("global_load_dwordx4 %0, %1, off\n\ts_waitcnt vmcnt(0)"
+                   : "=&v"(v) : "v"(X + ((long)(bid * 8 + u) * 37 + j) * RSF * 4 + 16 * h) : "memory");
+      rf[u] = v;
+    }
+  }
   const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)lds;
   auto issue = [&](int t, int bsel) {
     const char* gp = X + (long)t * TBY + lane * 16;
@@ -90,7 +108,8 @@ bare(const char* __restrict__ X, const char* Q, int n_tiles, int S, int n_qt, in
   for (int qh = 0; qh < QH; ++qh) accp[qh] = i32x16{};
   int cur = 0;
   for (int it = 0; it < my_nt; ++it) {
-    wait_barrier0();
+    if (NOBAR) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else wait_barrier0();
     __builtin_amdgcn_sched_barrier(0);
     if (it + 1 < my_nt) issue(tile_of(it + 1), cur ^ 1);
     i32x4 afn[DP / 32];
@@ -98,7 +117,19 @@ bare(const char* __restrict__ X, const char* Q, int n_tiles, int S, int n_qt, in
     for (int sub = 0; sub < TPB; ++sub) {
       const float* base = lds + cur * BUFF + sub * 32 * RSF;
       i32x4 af[DP / 32];
-      if (!PF || sub == 0) {
+      if (NOLDS) {
+        // (NOLDS: the query fragments stand in for the rows -- no LDS read;
+        // NOLDS 2: the rows are still read, into a sink the MFMAs do not use)
+#pragma unroll
+        for (int ks = 0; ks < DP / 32; ++ks) af[ks] = NOLDS == 3 ? rf[(ks + sub) & 7] : qf[0][(ks + sub) & 3];
+        if (NOLDS == 2) {
+#pragma unroll
+          for (int ks = 0; ks < DP / 32; ++ks) {
+            const i32x4 x = __builtin_bit_cast(i32x4, *(const float4*)(base + j * RSF + 8 * ks + 4 * h));
+            hits ^= x[ks];
+          }
+        }
+      } else if (!PF || sub == 0) {
 #pragma unroll
         for (int ks = 0; ks < DP / 32; ++ks)
           af[ks] = __builtin_bit_cast(i32x4, *(const float4*)(base + j * RSF + 8 * ks + 4 * h));
@@ -112,7 +143,7 @@ bare(const char* __restrict__ X, const char* Q, int n_tiles, int S, int n_qt, in
         for (int ks = 0; ks < DP / 32; ++ks)
           afn[ks] = __builtin_bit_cast(i32x4, *(const float4*)(base + 32 * RSF + j * RSF + 8 * ks + 4 * h));
       }
-      if (!PF) __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_sched_barrier(0);  // (PF: the next sub-tile's reads stay ahead of these MFMAs)
       i32x16 acc[QH];
 #pragma unroll
       for (int ks = 0; ks < DP / 32; ++ks)
@@ -181,8 +212,8 @@ void run(const char* X, const char* Q, int n, int m, int S, int* out) {
   int occ = 0;
   CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, bare<QH, NW, WPE, SEL>, NW * 64, 0));
   const double ops = 2.0 * n * (double)(n_qt * QPWG) * DP;
-  printf("PF=%d QH=%d NW=%d WPE=%d SEL=%d nostage=%d S=%d grid=%d wg/CU=%d: mean %.3f ms best %.3f ms  %.0f TOPS = %.3f of 5 POPS\n",
-         PF, QH, NW, WPE, SEL, NOSTAGE, S, grid, occ, sum / reps, best, ops / (best * 1e-3) / 1e12,
+  printf("NOLDS=%d NOBAR=%d PF=%d QH=%d NW=%d WPE=%d SEL=%d nostage=%d S=%d grid=%d wg/CU=%d: mean %.3f ms best %.3f ms  %.0f TOPS = %.3f of 5 POPS\n",
+         NOLDS, NOBAR, PF, QH, NW, WPE, SEL, NOSTAGE, S, grid, occ, sum / reps, best, ops / (best * 1e-3) / 1e12,
          ops / (best * 1e-3) / 5e15);
   fflush(stdout);
 }
