@@ -1,0 +1,134 @@
+// Experiment (not part of the library): how fast a pure MFMA stream runs on
+// the whole chip when its operands repeat (every MFMA the same registers, as
+// tools/issue_probe.hip) and when they vary like streamed rows do (A rotates
+// over 8 fragments of random data, B over 4), for the shapes the candidate
+// kernels use: v_mfma_i32_32x32x32_i8, v_mfma_f32_16x16x32_f16,
+// v_mfma_f32_32x32x16_f16.  8 waves per workgroup, 2 workgroups per CU,
+// 4 independent accumulators per wave (no dependency stalls).
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/exp/mfma_rand.hip -o tools/exp/mfma_rand
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int ITERS = 2048;
+
+// SHAPE 0: i8 32x32x32, 1: f16 16x16x32, 2: f16 32x32x16; RAND 0: fixed operands, 1: rotating
+template <int SHAPE, int RAND>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4)))
+stream(const i32x4* __restrict__ src, float* out) {
+  const int lane = threadIdx.x & 63;
+  const long base = ((long)blockIdx.x * 512 + threadIdx.x) * 12;
+  i32x4 a[8], b[4];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) a[u] = src[(base + u) & ((1 << 22) - 1)];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) b[u] = src[(base + 8 + u) & ((1 << 22) - 1)];
+  float r = 0;
+  if constexpr (SHAPE == 0) {
+    i32x16 c[4] = {};
+    for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        c[u & 3] = __builtin_amdgcn_mfma_i32_32x32x32_i8(RAND ? a[u] : a[0], RAND ? b[u & 3] : b[0], c[u & 3], 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) r += (float)(c[u][0] ^ c[u][15]);
+  } else if constexpr (SHAPE == 1) {
+    f32x4 c[4] = {};
+    for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+      for (int v = 0; v < 2; ++v)
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          c[u & 3] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, RAND ? a[u] : a[0]),
+                                                           __builtin_bit_cast(f16x8, RAND ? b[u & 3] : b[0]),
+                                                           c[u & 3], 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) r += c[u][0] + c[u][3];
+  } else {
+    f32x16 c[4] = {};
+    for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        c[u & 3] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, RAND ? a[u] : a[0]),
+                                                         __builtin_bit_cast(f16x8, RAND ? b[u & 3] : b[0]),
+                                                         c[u & 3], 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) r += c[u][0] + c[u][15];
+  }
+  out[(long)blockIdx.x * 512 + threadIdx.x] = r + lane;
+}
+
+#define CK(x)                                                              \
+  do {                                                                     \
+    hipError_t e_ = (x);                                                   \
+    if (e_ != hipSuccess) {                                                \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));              \
+      exit(1);                                                             \
+    }                                                                      \
+  } while (0)
+
+template <int SHAPE, int RAND>
+void run(const i32x4* src, float* out, int grid) {
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  float best = 1e30f;
+  for (int r = 0; r < 6; ++r) {
+    CK(hipEventRecord(e0, 0));
+    hipLaunchKernelGGL((stream<SHAPE, RAND>), dim3(grid), dim3(512), 0, 0, src, out);
+    CK(hipGetLastError());
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    if (r) best = ms < best ? ms : best;
+  }
+  // ops per wave: ITERS x 8 MFMAs (shape 1: x 16 MFMAs of 16x16x32)
+  const double per_mfma = SHAPE == 0 ? 65536.0 : SHAPE == 1 ? 16384.0 : 32768.0;
+  const double n_mfma = (double)grid * 8 * ITERS * (SHAPE == 1 ? 16 : 8);
+  const double peak = SHAPE == 0 ? 5.0e15 : 2.5e15;
+  const double rate = n_mfma * per_mfma / (best * 1e-3);
+  printf("%s %s: best %.3f ms  %.0f T/s = %.3f of the dense peak\n",
+         SHAPE == 0 ? "i8 32x32x32 " : SHAPE == 1 ? "f16 16x16x32" : "f16 32x32x16",
+         RAND ? "random rotating operands" : "fixed operands          ", best, rate / 1e12, rate / peak);
+  fflush(stdout);
+}
+
+int main() {
+  // random bytes (int8 shape) and random halves in [-1, 1) (f16 shapes)
+  std::vector<int> hi((size_t)4 << 22), hh((size_t)4 << 22);
+  srand(3);
+  for (size_t i = 0; i < hi.size(); ++i) {
+    const _Float16 x = (_Float16)((rand() & 2047) / 1024.0f - 1.0f), y = (_Float16)((rand() & 2047) / 1024.0f - 1.0f);
+    hh[i] = (int)((uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16));
+    hi[i] = (rand() << 1) ^ rand();
+  }
+  i32x4 *srci, *srch;
+  float* out;
+  CK(hipMalloc(&srci, hi.size() * 4));
+  CK(hipMemcpy(srci, hi.data(), hi.size() * 4, hipMemcpyHostToDevice));
+  CK(hipMalloc(&srch, hh.size() * 4));
+  CK(hipMemcpy(srch, hh.data(), hh.size() * 4, hipMemcpyHostToDevice));
+  const int grid = 256 * 2 * 4;  // 4 rounds of 2 workgroups per CU
+  CK(hipMalloc(&out, (size_t)grid * 512 * 4));
+  for (int pass = 0; pass < 2; ++pass) {
+    run<0, 0>(srci, out, grid);
+    run<0, 1>(srci, out, grid);
+    run<1, 0>(srch, out, grid);
+    run<1, 1>(srch, out, grid);
+    run<2, 0>(srch, out, grid);
+    run<2, 1>(srch, out, grid);
+  }
+  return 0;
+}
