@@ -127,6 +127,17 @@ static_assert(KNN_RES_TPB * knnk::kTR == knnk::kResTileRows || KNN_RES_TPB != 2,
 #ifndef KNN_I8W_PF
 #define KNN_I8W_PF 0
 #endif
+// metric 6: early prune on a partial distance.  After the MFMAs of the first
+// i8_part_dims(DP) dims of a sub-tile (all but the last 32), the partial
+// accumulators q_A.k_A plus the sub-tile's largest partial seed bound every
+// full accumulator from above, up to the query's remaining norm:
+//   q.k - ceil(|k|^2/2) <= (q_A.k_A - ceil(|k_A|^2/2)) + (|q_B|^2 + 1) / 2
+// (|q_B - k_B|^2 >= 0), so a wave none of whose values passes tn - hq, hq =
+// ceil((|q_B|^2 + 1) / 2), has no candidate in the sub-tile and skips its
+// last MFMA; its pending selection then never passes (smx = kI8Pruned).
+#ifndef KNN_I8_PART
+#define KNN_I8_PART 0
+#endif
 // metric 6 (experiment): also a 16-wave form (512 queries per staged tile:
 // half the L2 -> LDS staging bytes per MFMA; one workgroup per CU), selected
 // with tuning "nw" 16
@@ -541,6 +552,25 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
     return __builtin_bit_cast(i32x4, *(const float4*)(sb + (I8W ? 8 * c + 4 * h : 16 * c + 4 * g16) * RSF + SEED));
   };
   int smxp = 0;  // PIPE: smx of the pending sub-tile
+  // KNN_I8_PART: the partial-distance prune (metric 6, PIPE, >= 2 k-steps)
+  constexpr bool PART = I8W && SMX && PIPE && KNN_I8_PART && i8_part_dims(DP) > 0;
+  constexpr int KA = PART ? i8_part_dims(DP) / 32 : DP / 32;  // k-steps before the test
+  constexpr int kI8Pruned = -(1 << 25);  // smx of a pruned sub-tile: tn - smx exceeds any q.k
+  static_assert(!PART || !(KNN_SPRE_GLB), "the partial prune selects the pending sub-tile with spre");
+  int hq = 0;  // ceil((|q_B|^2 + 1) / 2) of the lane's query (the dims after KA k-steps)
+  if constexpr (PART) {
+    int qb2 = 0;
+#pragma unroll
+    for (int ks = KA; ks < DP / 32; ++ks) {
+      const i32x4 v = __builtin_bit_cast(i32x4, qf[ks]);
+      qb2 = __builtin_amdgcn_sdot4(v.x, v.x, qb2, false);
+      qb2 = __builtin_amdgcn_sdot4(v.y, v.y, qb2, false);
+      qb2 = __builtin_amdgcn_sdot4(v.z, v.z, qb2, false);
+      qb2 = __builtin_amdgcn_sdot4(v.w, v.w, qb2, false);
+    }
+    qb2 += __shfl_xor(qb2, 32, 64);  // lanes j and j + 32 hold the two halves of query j
+    hq = (qb2 + 2) >> 1;
+  }
   [[maybe_unused]] int cnt_it = 0;  // (KNN_COUNT_SEL: the staged tile being selected)
   auto sel5 = [&](const auto& a, int row0, int smx, auto&& sd) {  // a: i32x4 [2][QB]
    if constexpr (SMX) {
@@ -577,8 +607,10 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
 #if KNN_COUNT_SEL
     selc.bcalls++;
     selc.bpass += __builtin_amdgcn_ballot_w64(mx > tn[0] - smx) != 0;
-    selc.bcold += cnt_it < 2;
-    selc.bpcold += cnt_it < 2 && __builtin_amdgcn_ballot_w64(mx > tn[0] - smx) != 0;
+    if (!(KNN_I8_PART)) {  // (with the partial prune these two count its tests)
+      selc.bcold += cnt_it < 2;
+      selc.bpcold += cnt_it < 2 && __builtin_amdgcn_ballot_w64(mx > tn[0] - smx) != 0;
+    }
 #endif
     if (__builtin_amdgcn_ballot_w64(mx > tn[0] - smx)) {
 #if KNN_SLOWPRIO
@@ -607,6 +639,7 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
   // when the buffer may be refilled (a pending sub-tile starts empty: raw
   // accumulators kI8Floor and smx 0 never pass)
   int smt[SMX ? TPB : 1];
+  int smtA[PART ? TPB : 1];  // (KNN_I8_PART) the sub-tiles' largest partial seeds
   constexpr bool SPG = I8W && SMX && KNN_SPRE_GLB;  // last sub-tile's seeds by scalar loads
   // metric 6 (KNN_I8W_PF): the next sub-tile's A fragments in flight behind
   // the current sub-tile's MFMAs (its LDS latency no longer ahead of them)
@@ -838,6 +871,12 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
             i32x4, *(const float4*)(lds + cur * BUFF + (128 * uu + kI8SmaxRow) * RSF + SEED));
 #pragma unroll
         for (int e = 0; e < 4; ++e) smt[4 * u + e] = __builtin_amdgcn_readfirstlane(v[e]);
+        if constexpr (PART) {
+          const i32x4 va = __builtin_bit_cast(
+              i32x4, *(const float4*)(lds + cur * BUFF + (128 * uu + kI8SmaxARow) * RSF + SEED));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) smtA[4 * u + e] = __builtin_amdgcn_readfirstlane(va[e]);
+        }
       }
     }
 #pragma unroll
@@ -890,9 +929,35 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
       __builtin_amdgcn_sched_barrier(0);
 #endif
 #pragma unroll
-      for (int ks = 0; ks < DP / 32; ++ks)
+      for (int ks = 0; ks < KA; ++ks)
         acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[ks], __builtin_bit_cast(i32x4, qf[ks]),
                                                     SMX && ks == 0 ? i32x16{} : acc, 0, 0, 0);
+      if constexpr (PART) {
+        // the pending sub-tile's selection first (it covers these MFMAs'
+        // latency), then the partial test, then the last k-steps or none
+        // (a pruned pending sub-tile skips its full test altogether: smxp is
+        // wave-uniform, so this is a scalar branch)
+        if (smxp != kI8Pruned) {
+          if (sub > 0) sel6(accw, rowp, smxp, [&](int c) { return seed_lds(base_prev, c); });
+          else sel6(accw, rowp, smxp, [&](int c) { return spre[c]; });
+        }
+        auto m3 = [](int x, int y, int z) { return max(max(x, y), z); };
+        const int mxa = max(m3(m3(acc[0], acc[1], acc[2]), m3(acc[3], acc[4], acc[5]), m3(acc[6], acc[7], acc[8])),
+                            m3(m3(acc[9], acc[10], acc[11]), m3(acc[12], acc[13], acc[14]), acc[15]));
+#if KNN_COUNT_SEL
+        // (partial tests and the waves passing them in the "cold" counters)
+        selc.bcold++;
+        selc.bpcold += __builtin_amdgcn_ballot_w64(mxa > tn[0] - hq - smtA[sub]) != 0;
+#endif
+        if (__builtin_amdgcn_ballot_w64(mxa > tn[0] - hq - smtA[sub])) {
+#pragma unroll
+          for (int ks = KA; ks < DP / 32; ++ks)
+            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[ks], __builtin_bit_cast(i32x4, qf[ks]), acc, 0, 0, 0);
+          smxp = smt[sub];
+        } else {
+          smxp = kI8Pruned;
+        }
+      }
       if constexpr (CTR) {
         // (poll) the next tile's pieces as soon as every wave is done with
         // the tile before this one; SIGD sub-tiles later, counted ready
@@ -914,7 +979,10 @@ cand_kernel(const float* __restrict__ Xr, const float* Q32, int n_tiles, int S,
         // the pending sub-tile's selection after this one's MFMAs (seeds of
         // the previous staged tile's last sub-tile from spre)
         if (!(abl & 2)) {
-          if constexpr (PIPE) {
+          if constexpr (PART) {
+            accw = acc;  // (selected, tested and completed above)
+            rowp = row0;
+          } else if constexpr (PIPE) {
             if (sub > 0) sel6(accw, rowp, smxp, [&](int c) { return seed_lds(base_prev, c); });
             else if constexpr (SPG) sel6(accw, rowp, smxp, [&](int c) { return seed_glb(rowp_s, c); });
             else sel6(accw, rowp, smxp, [&](int c) { return spre[c]; });

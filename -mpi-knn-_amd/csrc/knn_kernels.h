@@ -420,6 +420,14 @@ void launch_norm_blocks(const double* X, const double* cent, int s, const double
 // the 32-row sub-tiles 4u .. 4u+3 (the seed-free accumulation's bound,
 // knn_cand_res.hip)
 constexpr int kI8SmaxRow = 1;
+// ... and in the pad of row 128u + 2 the largest PARTIAL seed -ceil(||k_A||^2
+// / 2) over the first i8_part_dims(DP) dims of the same sub-tiles: the
+// metric-6 kernel's early prune after those dims' MFMAs (knn_cand_res.hip,
+// KNN_I8_PART).  0 dims: no partial test (the pads get 0, a valid bound).
+// Only for 128 <= DP <= 192: at DP = 96 the test after 64 of 96 dims prunes
+// too little to pay for its tree (the 12.5M x 96 shard +21 %, ab_log r6r).
+constexpr int kI8SmaxARow = 2;
+constexpr int i8_part_dims(int DP) { return DP >= 128 && DP <= 192 ? DP - 32 : 0; }
 
 // Min-max normalisation (knn_normalize.hip, cpp:229-306).  R = rows per
 // grid sweep; `partial` holds 2*d*R doubles.  launch_minmax folds the set's

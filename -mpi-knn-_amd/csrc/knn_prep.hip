@@ -449,9 +449,10 @@ prep_i8_train_kernel(const double* __restrict__ X64, const double* __restrict__ 
 
 // Sub-tile seed maxima: thread u4 = 32-row sub-tile, the max of its 32 seeds
 // (pads of its rows 4g) into int slot (u4 & 3) of the pad of row 128 (u4 >>
-// 2) + kI8SmaxRow.  An all-pad sub-tile gets kI8Floor.
+// 2) + kI8SmaxRow, and the max of its partial seeds into the pad of row
+// 128 (u4 >> 2) + kI8SmaxARow.  An all-pad sub-tile gets kI8Floor.
 __global__ void __launch_bounds__(256)
-prep_i8_smax_kernel(signed char* __restrict__ out, int DP, int64_t n_sub) {
+prep_i8_smax_kernel(signed char* __restrict__ out, int DP, int64_t n_sub, int swz) {
   const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (u >= n_sub) return;
   const int64_t row_bytes = DP + 16;
@@ -461,7 +462,27 @@ prep_i8_smax_kernel(signed char* __restrict__ out, int DP, int64_t n_sub) {
     const int4 sd = *(const int4*)(out + (u * 32 + 4 * g) * row_bytes + DP);
     mx = max(mx, max(max(sd.x, sd.y), max(sd.z, sd.w)));
   }
+  // the partial seeds: -ceil(||k_A||^2 / 2) over the first i8_part_dims(DP)
+  // dims (chunk ch of 16 codes sits at ch ^ xh_swz(row & 15) in a swizzled
+  // image); pad rows (all-zero codes) give 0, a valid upper bound
+  const int dA = i8_part_dims(DP);
+  int mxa = dA > 0 ? kI8Floor : 0;
+  for (int r = 0; r < 32 && dA > 0; ++r) {
+    const int64_t row = u * 32 + r;
+    const signed char* p = out + row * row_bytes;
+    const int sw = swz ? xh_swz((int)(row & 15)) : 0;
+    int kk = 0;
+    for (int ch = 0; ch < dA / 16; ++ch) {
+      const int4 v = *(const int4*)(p + ((ch ^ sw) << 4));
+      kk = __builtin_amdgcn_sdot4(v.x, v.x, kk, false);
+      kk = __builtin_amdgcn_sdot4(v.y, v.y, kk, false);
+      kk = __builtin_amdgcn_sdot4(v.z, v.z, kk, false);
+      kk = __builtin_amdgcn_sdot4(v.w, v.w, kk, false);
+    }
+    mxa = max(mxa, -((kk + 1) >> 1));
+  }
   ((int*)(out + ((u >> 2) * 128 + kI8SmaxRow) * row_bytes + DP))[u & 3] = mx;
+  ((int*)(out + ((u >> 2) * 128 + kI8SmaxARow) * row_bytes + DP))[u & 3] = mxa;
 }
 
 void launch_prep_i8_train(const double* X64, const double* cent, int64_t n, int d, int DP,
@@ -476,7 +497,7 @@ void launch_prep_i8_train(const double* X64, const double* cent, int64_t n, int 
   // tail group would place them past the image, so it gets none)
   const int64_t n_sub = n_pad / 128 * 4;
   hipLaunchKernelGGL(prep_i8_smax_kernel, dim3((unsigned)((n_sub + 255) / 256)), dim3(256), 0, st,
-                     out, DP, n_sub);
+                     out, DP, n_sub, swz);
 }
 
 // Query rows: int8 codes clamp(rint(q 2^s - c_i), -128, 127) (DP bytes,
