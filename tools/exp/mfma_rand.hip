@@ -4,7 +4,8 @@
 // over 8 fragments of random data, B over 4), for the shapes the candidate
 // kernels use: v_mfma_i32_32x32x32_i8, v_mfma_f32_16x16x32_f16,
 // v_mfma_f32_32x32x16_f16.  8 waves per workgroup, 2 workgroups per CU,
-// 4 independent accumulators per wave (no dependency stalls).
+// 4 independent accumulators per wave (no dependency stalls; the int8 shape
+// also with 2 and with 1: dependent chains).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/exp/mfma_rand.hip -o tools/exp/mfma_rand
 #include <hip/hip_runtime.h>
 
@@ -21,7 +22,7 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 constexpr int ITERS = 2048;
 
 // SHAPE 0: i8 32x32x32, 1: f16 16x16x32, 2: f16 32x32x16; RAND 0: fixed operands, 1: rotating
-template <int SHAPE, int RAND>
+template <int SHAPE, int RAND, int CH = 4>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4)))
 stream(const i32x4* __restrict__ src, float* out) {
   const int lane = threadIdx.x & 63;
@@ -37,7 +38,7 @@ stream(const i32x4* __restrict__ src, float* out) {
     for (int it = 0; it < ITERS; ++it) {
 #pragma unroll
       for (int u = 0; u < 8; ++u)
-        c[u & 3] = __builtin_amdgcn_mfma_i32_32x32x32_i8(RAND ? a[u] : a[0], RAND ? b[u & 3] : b[0], c[u & 3], 0, 0, 0);
+        c[u % CH] = __builtin_amdgcn_mfma_i32_32x32x32_i8(RAND ? a[u] : a[0], RAND ? b[u & 3] : b[0], c[u % CH], 0, 0, 0);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) r += (float)(c[u][0] ^ c[u][15]);
@@ -78,7 +79,7 @@ stream(const i32x4* __restrict__ src, float* out) {
     }                                                                      \
   } while (0)
 
-template <int SHAPE, int RAND>
+template <int SHAPE, int RAND, int CH = 4>
 void run(const i32x4* src, float* out, int grid) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
@@ -86,7 +87,7 @@ void run(const i32x4* src, float* out, int grid) {
   float best = 1e30f;
   for (int r = 0; r < 6; ++r) {
     CK(hipEventRecord(e0, 0));
-    hipLaunchKernelGGL((stream<SHAPE, RAND>), dim3(grid), dim3(512), 0, 0, src, out);
+    hipLaunchKernelGGL((stream<SHAPE, RAND, CH>), dim3(grid), dim3(512), 0, 0, src, out);
     CK(hipGetLastError());
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
@@ -99,9 +100,9 @@ void run(const i32x4* src, float* out, int grid) {
   const double n_mfma = (double)grid * 8 * ITERS * (SHAPE == 1 ? 16 : 8);
   const double peak = SHAPE == 0 ? 5.0e15 : 2.5e15;
   const double rate = n_mfma * per_mfma / (best * 1e-3);
-  printf("%s %s: best %.3f ms  %.0f T/s = %.3f of the dense peak\n",
+  printf("%s %s (%d accumulator chains per wave): best %.3f ms  %.0f T/s = %.3f of the dense peak\n",
          SHAPE == 0 ? "i8 32x32x32 " : SHAPE == 1 ? "f16 16x16x32" : "f16 32x32x16",
-         RAND ? "random rotating operands" : "fixed operands          ", best, rate / 1e12, rate / peak);
+         RAND ? "random rotating operands" : "fixed operands          ", CH, best, rate / 1e12, rate / peak);
   fflush(stdout);
 }
 
@@ -125,6 +126,8 @@ int main() {
   for (int pass = 0; pass < 2; ++pass) {
     run<0, 0>(srci, out, grid);
     run<0, 1>(srci, out, grid);
+    run<0, 1, 2>(srci, out, grid);
+    run<0, 1, 1>(srci, out, grid);
     run<1, 0>(srch, out, grid);
     run<1, 1>(srch, out, grid);
     run<2, 0>(srch, out, grid);
