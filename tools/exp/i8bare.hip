@@ -7,7 +7,7 @@
 //   workgroup, WPE waves per SIMD the registers are sized for.
 // SEL 1 adds the fast path of the selection (a v_max3 tree over the previous
 // sub-tile's 16 accumulators and a wave-uniform branch that never passes);
-// SEL 2 the same over 8 of them; SEL 0 none (the sub-tiles' MFMAs chain into
+// SEL 2 the same over 8 of them; SEL 3 the 16-value tree without the branch; SEL 0 none (the sub-tiles' MFMAs chain into
 // one accumulator, so none is dead code);
 // NOSTAGE re-reads the split's first tile (no row stream).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/exp/i8bare.hip -o tools/exp/i8bare
@@ -155,7 +155,9 @@ bare(const char* __restrict__ X, const char* Q, int n_tiles, int S, int n_qt, in
 #pragma unroll
         for (int qh = 0; qh < QH; ++qh) {
           const int mx = SEL == 2 ? max8(accp[qh]) : max16(accp[qh]);
-          if (__builtin_amdgcn_ballot_w64(mx > thr)) {
+          if constexpr (SEL == 3) {
+            hits += mx > thr;  // (SEL 3: the same tree, no ballot and no branch)
+          } else if (__builtin_amdgcn_ballot_w64(mx > thr)) {
             ++hits;
             mx_all = max(mx_all, mx);
           }
@@ -233,10 +235,10 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&out, (size_t)64 << 20));
   const int S = argc > 1 ? atoi(argv[1]) : 40;
   for (int pass = 0; pass < 2; ++pass) {
-    run<1, 8, 4, 0>(X, Q, n, m, S, out);
     run<1, 8, 4, 1>(X, Q, n, m, S, out);
-    run<2, 4, 2, 0>(X, Q, n, m, S, out);
+    run<1, 8, 4, 3>(X, Q, n, m, S, out);
     run<2, 4, 2, 1>(X, Q, n, m, S, out);
+    run<2, 4, 2, 3>(X, Q, n, m, S, out);
   }
   return 0;
 }
