@@ -20,6 +20,9 @@
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 
+#ifndef NODMA
+#define NODMA 0
+#endif
 #ifndef NOLDS
 #define NOLDS 0
 #endif
@@ -111,7 +114,7 @@ bare(const char* __restrict__ X, const char* Q, int n_tiles, int S, int n_qt, in
     if (NOBAR) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     else wait_barrier0();
     __builtin_amdgcn_sched_barrier(0);
-    if (it + 1 < my_nt) issue(tile_of(it + 1), cur ^ 1);
+    if (it + 1 < my_nt && !NODMA) issue(tile_of(it + 1), cur ^ 1);  // (NODMA: only the first tile)
     i32x4 afn[DP / 32];
 #pragma unroll
     for (int sub = 0; sub < TPB; ++sub) {
@@ -214,8 +217,8 @@ void run(const char* X, const char* Q, int n, int m, int S, int* out) {
   int occ = 0;
   CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, bare<QH, NW, WPE, SEL>, NW * 64, 0));
   const double ops = 2.0 * n * (double)(n_qt * QPWG) * DP;
-  printf("NOLDS=%d NOBAR=%d PF=%d QH=%d NW=%d WPE=%d SEL=%d nostage=%d S=%d grid=%d wg/CU=%d: mean %.3f ms best %.3f ms  %.0f TOPS = %.3f of 5 POPS\n",
-         NOLDS, NOBAR, PF, QH, NW, WPE, SEL, NOSTAGE, S, grid, occ, sum / reps, best, ops / (best * 1e-3) / 1e12,
+  printf("NODMA=%d NOLDS=%d NOBAR=%d PF=%d QH=%d NW=%d WPE=%d SEL=%d nostage=%d S=%d grid=%d wg/CU=%d: mean %.3f ms best %.3f ms  %.0f TOPS = %.3f of 5 POPS\n",
+         NODMA, NOLDS, NOBAR, PF, QH, NW, WPE, SEL, NOSTAGE, S, grid, occ, sum / reps, best, ops / (best * 1e-3) / 1e12,
          ops / (best * 1e-3) / 5e15);
   fflush(stdout);
 }
