@@ -20,6 +20,9 @@
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 
+#ifndef STG
+#define STG 0
+#endif
 #ifndef NODMA
 #define NODMA 0
 #endif
@@ -114,10 +117,30 @@ bare(const char* __restrict__ X, const char* Q, int n_tiles, int S, int n_qt, in
     if (NOBAR) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     else wait_barrier0();
     __builtin_amdgcn_sched_barrier(0);
-    if (it + 1 < my_nt && !NODMA) issue(tile_of(it + 1), cur ^ 1);  // (NODMA: only the first tile)
+    // STG: the next tile by plain loads into registers, written to LDS by
+    // ds_write_b128 at mid-tile (instead of LDS-DMA pieces)
+    constexpr int NPW = (NG + NW - 1) / NW;
+    i32x4 stg[STG ? NPW : 1];
+    if (STG && it + 1 < my_nt) {
+      const char* gp = X + (long)tile_of(it + 1) * TBY + lane * 16;
+#pragma unroll
+      for (int k = 0; k < NPW; ++k) {
+        const int i = wv + k * NW;
+        if (i < NG) stg[k] = *(const i32x4*)(gp + i * 1024);
+      }
+    } else if (!STG && it + 1 < my_nt && !NODMA) {
+      issue(tile_of(it + 1), cur ^ 1);  // (NODMA: only the first tile)
+    }
     i32x4 afn[DP / 32];
 #pragma unroll
     for (int sub = 0; sub < TPB; ++sub) {
+      if (STG && sub == TPB / 2 && it + 1 < my_nt) {
+#pragma unroll
+        for (int k = 0; k < NPW; ++k) {
+          const int i = wv + k * NW;
+          if (i < NG) *(i32x4*)((char*)(lds + (cur ^ 1) * BUFF) + i * 1024 + lane * 16) = stg[k];
+        }
+      }
       const float* base = lds + cur * BUFF + sub * 32 * RSF;
       i32x4 af[DP / 32];
       if (NOLDS) {
@@ -217,8 +240,8 @@ void run(const char* X, const char* Q, int n, int m, int S, int* out) {
   int occ = 0;
   CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, bare<QH, NW, WPE, SEL>, NW * 64, 0));
   const double ops = 2.0 * n * (double)(n_qt * QPWG) * DP;
-  printf("NODMA=%d NOLDS=%d NOBAR=%d PF=%d QH=%d NW=%d WPE=%d SEL=%d nostage=%d S=%d grid=%d wg/CU=%d: mean %.3f ms best %.3f ms  %.0f TOPS = %.3f of 5 POPS\n",
-         NODMA, NOLDS, NOBAR, PF, QH, NW, WPE, SEL, NOSTAGE, S, grid, occ, sum / reps, best, ops / (best * 1e-3) / 1e12,
+  printf("STG=%d NODMA=%d NOLDS=%d NOBAR=%d PF=%d QH=%d NW=%d WPE=%d SEL=%d nostage=%d S=%d grid=%d wg/CU=%d: mean %.3f ms best %.3f ms  %.0f TOPS = %.3f of 5 POPS\n",
+         STG, NODMA, NOLDS, NOBAR, PF, QH, NW, WPE, SEL, NOSTAGE, S, grid, occ, sum / reps, best, ops / (best * 1e-3) / 1e12,
          ops / (best * 1e-3) / 5e15);
   fflush(stdout);
 }
